@@ -1,0 +1,193 @@
+#!/usr/bin/env python3
+"""Benchmark: (spectrum x DLA-sample) log-evidence evaluations per second on MI355X.
+
+Workload (BASELINE.json configs[1]): 1024 synthetic spectra per GPU, n = 800 unmasked pixels,
+k = 20, S = 10^4 DLA samples, fp64.  One step = one pass of the hot path over the batch:
+spectrum preparation, the fused Voigt x low-rank-Gaussian likelihood for every (spectrum,
+sample) pair plus the null model, and the per-spectrum log-mean-exp.  Inputs are resident in HBM
+before timing starts; outputs (incl. the 1024 x 10^4 sample log-likelihoods) stay in HBM.
+
+Multi-GPU (torch.distributed.run, one process per GPU): spectra are sharded with no data-path
+collective (weak scaling: 1024 spectra per rank); the only collectives are the timing barrier
+and the max-over-ranks of the elapsed time, on the gloo backend (host-side: the hot path has no
+exchange step, so nothing needs RCCL).  Device buffers come from libgpdla itself, so the process
+holds a single HIP runtime (the system ROCm one the library was built against).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+FP64_PEAK_TFLOPS = 78.6     # MI355X FP64 (vector and matrix), datasheet
+HBM_PEAK_GBS = 8000.0       # MI355X HBM3E, datasheet
+
+
+def algorithmic_flops_per_eval(n: int, k: int) -> float:
+    """packed Gram + projection + per-pixel scalars + Cholesky + solve."""
+    return n * k * (k + 1) + 2 * n * k + 10 * n + k ** 3 / 3 + 2 * k ** 2
+
+
+def effective_bytes_per_eval(n: int, k: int, w: int = 8) -> float:
+    """SURVEY.md 8d streamed-panel accounting (north-star 'effective HBM')."""
+    return w * (n * (k + 5) + 8) + w
+
+
+def cpu_baseline(model, samples, spectra, budget_s: float) -> dict:
+    """The numpy oracle (MATLAB-order restatement) on one host core, on a bounded sample of the
+    same workload: spectra 0, 1, ... with all their DLA samples, until the time budget is spent."""
+    from threadpoolctl import threadpool_limits
+    from oracle import gpdla_oracle as O
+    done, nspec = 0, 0
+    with threadpool_limits(limits=1):
+        t0 = time.perf_counter()
+        for s in spectra:
+            prep = O.prepare_spectrum(s["wavelengths"], s["flux"], s["noise_variance"], s["pixel_mask"],
+                                      s["z_qso"], model)
+            zs = prep["zmin"] + (prep["zmax"] - prep["zmin"]) * samples["offset_samples"]
+            nspec += 1
+            for z, N in zip(zs, samples["nhi_samples"]):
+                O.sample_log_likelihood(prep, z, N, 3)
+                done += 1
+                if time.perf_counter() - t0 >= budget_s:
+                    break
+            if time.perf_counter() - t0 >= budget_s:
+                break
+        el = time.perf_counter() - t0
+    return {"value": done / el, "unit": "evals/s", "cores": 1, "kind": "port",
+            "sample": f"{done} (spectrum, DLA-sample) evaluations over the first {nspec} spectra of the bench "
+                      f"workload (n=800, k=20, 3 lines) in {el:.1f} s on 1 host core; numpy/scipy restatement "
+                      "of process_qsos.m:186-197 (MATLAB is not available)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--spectra", type=int, default=1024, help="spectra per GPU")
+    ap.add_argument("--samples", type=int, default=10000)
+    ap.add_argument("--k", type=int, default=20)
+    ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU-baseline work (0 = skip)")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    from gp_dla_detection_amd import _lib as L
+    from gp_dla_detection_amd import synthetic as syn
+    from gp_dla_detection_amd.engine import Engine
+    from gp_dla_detection_amd.parameters import set_parameters
+
+    model = syn.make_model(k=args.k)
+    samples = syn.make_samples(args.samples)
+    Q = args.spectra
+    spectra = [syn.make_spectrum(model, rank * Q + q) for q in range(Q)]
+    packed = syn.pack_spectra(spectra)
+    D = lambda a: L.DeviceArray.from_numpy(a, device=local_rank)
+    t = {key: D(packed[key]) for key in ("wavelengths", "flux", "noise_variance", "pixel_mask", "z_qsos")}
+    S = args.samples
+    o_null = L.DeviceArray(local_rank, Q, np.float64)
+    o_dla = L.DeviceArray(local_rank, Q, np.float64)
+    o_s = L.DeviceArray(local_rank, (Q, S), np.float64)
+    o_n = L.DeviceArray(local_rank, Q, np.int32)
+
+    eng = Engine(model, samples, set_parameters(k=args.k), device=local_rank)
+
+    def step():
+        eng.process_device(packed["offsets"], t["wavelengths"].ptr, t["flux"].ptr, t["noise_variance"].ptr,
+                           t["pixel_mask"].ptr, t["z_qsos"].ptr, o_null.ptr, o_dla.ptr, o_s.ptr, S,
+                           npix_ptr=o_n.ptr)
+
+    for _ in range(args.warmup):
+        step()
+    eng.synchronize()
+    eng.reset_stats()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    eng.synchronize()  # device-side completion of every enqueued step
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    st = eng.stats()
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+
+    # sanity: finite outputs and the calc_cddf.py:246 normalisation invariant
+    sll = o_s.numpy()
+    lld = o_dla.numpy()
+    npix = o_n.numpy()
+    ok = bool(np.all(np.isfinite(sll)) and np.all(np.isfinite(lld)))
+    inv = np.exp(sll - (lld[:, None] + np.log(S))).sum(axis=1)
+    ok = ok and bool(np.max(np.abs(inv - 1)) < 1e-10)
+
+    evals_total = world * Q * S * args.steps
+    value = evals_total / elapsed
+    n_mean = float(np.mean(npix))
+    launches = max(st["likelihood_launches"], 1)
+    avg_ms = st["likelihood_ms"] / launches
+    evals_per_launch = Q * (S + 1) * args.steps / launches  # incl. the null-model evaluation
+    flops_launch = algorithmic_flops_per_eval(n_mean, args.k) * evals_per_launch
+    achieved_tf = flops_launch / (avg_ms * 1e-3) / 1e12
+    eff_gbs = effective_bytes_per_eval(n_mean, args.k) * evals_per_launch / (avg_ms * 1e-3) / 1e9
+
+    result = {
+        "metric": "(spectrum x DLA-sample) log-evidence evals/sec",
+        "value": value,
+        "unit": "evals/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (seeded; SURVEY.md 8d model/spectra, unscrambled Halton samples)",
+        "config": {"workload": f"configs[1]: {Q} spectra/GPU x {S} DLA samples, n={n_mean:.0f}, k={args.k}, "
+                               f"3 Lyman lines, fp64", "spectra_per_gpu": Q, "num_samples": S,
+                   "k": args.k, "n_pixels": n_mean, "parallelism": f"spectrum-shard x{world}"},
+        "roofline": {"bound": "mfma", "achieved": achieved_tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": achieved_tf / FP64_PEAK_TFLOPS, "traffic": None,
+                     "kernel": "likelihood_kernel<20>", "avg_launch_ms": avg_ms,
+                     "flops_per_eval": algorithmic_flops_per_eval(n_mean, args.k),
+                     "evals_per_launch": evals_per_launch},
+        "hbm_effective": {"achieved": eff_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                          "frac": eff_gbs / HBM_PEAK_GBS,
+                          "bytes_per_eval": effective_bytes_per_eval(n_mean, args.k),
+                          "note": "north-star streamed-panel accounting (SURVEY.md 8d); compulsory DRAM bytes are ~24 B/eval"},
+        "kernel_ms": {"prep": st["prep_ms"] / max(st["prep_launches"], 1), "likelihood": avg_ms,
+                      "reduce": st["reduce_ms"] / max(st["reduce_launches"], 1)},
+        "checks_ok": ok,
+    }
+    if rank == 0 and world == 1 and args.cpu_budget > 0:
+        result["cpu_baseline"] = cpu_baseline(model, samples, spectra, args.cpu_budget)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    eng.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

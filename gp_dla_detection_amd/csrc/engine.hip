@@ -1,0 +1,631 @@
+// C-ABI of libgpdla.so (include/gpdla.h): engine lifecycle, device workspaces, batching,
+// kernel-time accounting and the standalone voigt / log_mvnpdf_low_rank entry points.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/gpdla.h"
+#include "internal.h"
+
+using namespace gpdla;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int set_error(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_last_error = buf;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                       \
+  do {                                                                                      \
+    hipError_t e_ = (expr);                                                                 \
+    if (e_ != hipSuccess)                                                                   \
+      return set_error(e_ == hipErrorOutOfMemory ? GPDLA_ENOMEM : GPDLA_EDEVICE,            \
+                       "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__,     \
+                       __LINE__);                                                           \
+  } while (0)
+
+// ---- line-profile tables (fitted once per process on the host) + per-line x factors
+// layout: [kMaxLines][kLineTableStride] tables, then [kMaxLines] factors
+//   factor_j = c / (lambda_j 1e8) / (sigma sqrt 2)  so that  x_j = lambda * factor_j / (1+z) - c/(sigma sqrt 2)
+const std::vector<double>& host_line_data() {
+  static std::vector<double> data;
+  static std::once_flag once;
+  std::call_once(once, [] {
+    data.assign((size_t)kMaxLines * kLineTableStride + kMaxLines, 0.0);
+    for (int j = 0; j < kMaxLines; ++j) fit_line_table(j, data.data() + (size_t)j * kLineTableStride);
+    for (int j = 0; j < kMaxLines; ++j) {
+      const long double f = (long double)kCcgs / ((long double)kTransitionWavelengths[j] * 1e8L) /
+                            ((long double)kSigma * std::sqrt(2.0L));
+      data[(size_t)kMaxLines * kLineTableStride + j] = (double)f;
+    }
+  });
+  return data;
+}
+
+int check_device(int32_t device) {
+  int count = 0;
+  hipError_t e = hipGetDeviceCount(&count);
+  if (e != hipSuccess || count == 0)
+    return set_error(GPDLA_EDEVICE, "no HIP device available (%s): libgpdla has no CPU fallback",
+                     hipGetErrorString(e));
+  if (device < 0 || device >= count)
+    return set_error(GPDLA_EINVAL, "device %d out of range (%d devices)", device, count);
+  return GPDLA_OK;
+}
+
+template <class T>
+int grow(T** p, size_t* cap, size_t count) {
+  if (count <= *cap && *p) return GPDLA_OK;
+  if (*p) (void)hipFree(*p);
+  *p = nullptr;
+  *cap = 0;
+  size_t want = std::max<size_t>(count, 1);
+  HIP_TRY(hipMalloc((void**)p, want * sizeof(T)));
+  *cap = want;
+  return GPDLA_OK;
+}
+
+struct TimedLaunch {
+  hipEvent_t start, stop;
+  int kind;  // 0 prep, 1 likelihood, 2 reduce
+};
+
+}  // namespace
+
+struct gpdla_engine {
+  int device = 0;
+  int K = 0;
+  int64_t S = 0;
+  gpdla_params params{};
+  hipStream_t own_stream = nullptr;
+  hipStream_t stream = nullptr;
+
+  // resident model / samples / line data
+  double *d_rest = nullptr, *d_mu = nullptr, *d_M = nullptr, *d_logom = nullptr;
+  int32_t num_rest = 0;
+  double c0 = 0, tau0 = 0, beta = 0;
+  double *d_off = nullptr, *d_nhi = nullptr;
+  double* d_lines = nullptr;
+  int32_t* d_status = nullptr;
+
+  // batch workspaces
+  size_t cap_meta = 0, cap_q = 0, cap_slots = 0, cap_lam = 0, cap_scr = 0, cap_sll = 0;
+  size_t cap_smap = 0, cap_wl = 0, cap_flux = 0, cap_noise = 0, cap_mask = 0, cap_z = 0;
+  int64_t* d_meta = nullptr;  // [offsets(Q+1) | slot_base | lam_base | slot_cap]
+  double *d_wl = nullptr, *d_flux = nullptr, *d_noise = nullptr;
+  uint8_t* d_mask = nullptr;
+  double* d_z = nullptr;
+  SpecInfo* d_info = nullptr;
+  double *d_panel = nullptr, *d_lam = nullptr;
+  int32_t* d_smap = nullptr;
+  double* d_scratch = nullptr;
+  double *d_sll = nullptr, *d_llnull = nullptr, *d_lldla = nullptr, *d_zmin = nullptr,
+         *d_zmax = nullptr;
+  int32_t* d_npix = nullptr;
+  size_t cap_qout = 0;
+
+  // pinned host metadata (reused after meta_ready completes)
+  int64_t* h_meta = nullptr;
+  size_t cap_hmeta = 0;
+  hipEvent_t meta_done = nullptr;
+
+  std::vector<TimedLaunch> pending;
+  gpdla_stats stats{};
+};
+
+namespace {
+
+int record_start(gpdla_engine* e, TimedLaunch* t, int kind) {
+  HIP_TRY(hipEventCreate(&t->start));
+  HIP_TRY(hipEventCreate(&t->stop));
+  t->kind = kind;
+  HIP_TRY(hipEventRecord(t->start, e->stream));
+  return GPDLA_OK;
+}
+
+int resolve_events(gpdla_engine* e) {
+  for (auto& t : e->pending) {
+    HIP_TRY(hipEventSynchronize(t.stop));
+    float ms = 0;
+    HIP_TRY(hipEventElapsedTime(&ms, t.start, t.stop));
+    if (t.kind == 0) { e->stats.prep_ms += ms; e->stats.prep_launches++; }
+    if (t.kind == 1) { e->stats.likelihood_ms += ms; e->stats.likelihood_launches++; }
+    if (t.kind == 2) { e->stats.reduce_ms += ms; e->stats.reduce_launches++; }
+    (void)hipEventDestroy(t.start);
+    (void)hipEventDestroy(t.stop);
+  }
+  e->pending.clear();
+  return GPDLA_OK;
+}
+
+int validate_params(const gpdla_params* p) {
+  if (p->num_lines < 1 || p->num_lines > kMaxLines)
+    return set_error(GPDLA_EINVAL, "num_lines=%d outside [1, %d] (voigt.c:16)", p->num_lines, kMaxLines);
+  if (p->width != kWidth)
+    return set_error(GPDLA_EINVAL, "width=%d but the instrument profile is compiled for %d (voigt.c:229)",
+                     p->width, kWidth);
+  if (p->absorption_mode != GPDLA_ABSORPTION_REFERENCE && p->absorption_mode != GPDLA_ABSORPTION_UNMASKED)
+    return set_error(GPDLA_EINVAL, "absorption_mode=%d", p->absorption_mode);
+  if (!(p->max_lambda > p->min_lambda) || !(p->pixel_spacing > 0) || !(p->lya_wavelength > 0))
+    return set_error(GPDLA_EINVAL, "invalid wavelength parameters");
+  if (p->max_batch_spectra < 0) return set_error(GPDLA_EINVAL, "max_batch_spectra < 0");
+  return GPDLA_OK;
+}
+
+int upload(void* dst, const void* src, size_t bytes, hipStream_t s) {
+  HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s));
+  return GPDLA_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int32_t gpdla_version(void) { return 1; }
+
+int32_t gpdla_device_count(void) {
+  int c = 0;
+  if (hipGetDeviceCount(&c) != hipSuccess) return 0;
+  return c;
+}
+
+const char* gpdla_last_error(void) { return g_last_error.c_str(); }
+
+int gpdla_diag_faddeeva_w(double x, double y, double* re, double* im);  // faddeeva_host.cpp
+
+int gpdla_diag_line_table_error(int32_t line, double* max_rel_err) {
+  if (line < 0 || line >= kMaxLines || !max_rel_err) return set_error(GPDLA_EINVAL, "bad line");
+  std::vector<double> tab(kLineTableStride);
+  *max_rel_err = fit_line_table(line, tab.data());
+  return GPDLA_OK;
+}
+
+void gpdla_engine_destroy(gpdla_engine* e) {
+  if (!e) return;
+  (void)hipSetDevice(e->device);
+  if (e->stream) (void)hipStreamSynchronize(e->stream);
+  for (auto& t : e->pending) { (void)hipEventDestroy(t.start); (void)hipEventDestroy(t.stop); }
+  void* bufs[] = {e->d_rest, e->d_mu, e->d_M, e->d_logom, e->d_off, e->d_nhi, e->d_lines,
+                  e->d_status, e->d_meta, e->d_wl, e->d_flux, e->d_noise, e->d_mask, e->d_z,
+                  e->d_info, e->d_panel, e->d_lam, e->d_smap, e->d_scratch, e->d_sll,
+                  e->d_llnull, e->d_lldla, e->d_zmin, e->d_zmax, e->d_npix};
+  for (void* b : bufs)
+    if (b) (void)hipFree(b);
+  if (e->h_meta) (void)hipHostFree(e->h_meta);
+  if (e->meta_done) (void)hipEventDestroy(e->meta_done);
+  if (e->own_stream) (void)hipStreamDestroy(e->own_stream);
+  delete e;
+}
+
+int gpdla_engine_create(int32_t device, const gpdla_model* model, const gpdla_samples* samples,
+                        const gpdla_params* params, gpdla_engine** out) {
+  if (!model || !samples || !params || !out) return set_error(GPDLA_EINVAL, "null argument");
+  *out = nullptr;
+  int rc = check_device(device);
+  if (rc) return rc;
+  if ((rc = validate_params(params))) return rc;
+  if (!rank_supported(model->k))
+    return set_error(GPDLA_EUNSUPPORTED, "rank k=%d not compiled (supported: 4 8 10 12 16 20 24)", model->k);
+  if (model->num_rest < 2 || !model->rest_wavelengths || !model->mu || !model->M || !model->log_omega)
+    return set_error(GPDLA_EINVAL, "invalid model");
+  for (int i = 1; i < model->num_rest; ++i)
+    if (!(model->rest_wavelengths[i] > model->rest_wavelengths[i - 1]))
+      return set_error(GPDLA_EINVAL, "rest_wavelengths must be strictly increasing");
+  if (samples->num_samples < 1 || !samples->offset_samples || !samples->nhi_samples)
+    return set_error(GPDLA_EINVAL, "invalid samples");
+
+  HIP_TRY(hipSetDevice(device));
+  gpdla_engine* e = new gpdla_engine();
+  e->device = device;
+  e->K = model->k;
+  e->S = samples->num_samples;
+  e->params = *params;
+  e->num_rest = model->num_rest;
+  e->c0 = std::exp(model->log_c_0);     // process_qsos.m:84-86
+  e->tau0 = std::exp(model->log_tau_0);
+  e->beta = std::exp(model->log_beta);
+  auto fail = [&](int code) { gpdla_engine_destroy(e); return code; };
+#define TRY_E(x) do { int r_ = (x); if (r_) return fail(r_); } while (0)
+  if (hipStreamCreateWithFlags(&e->own_stream, hipStreamNonBlocking) != hipSuccess)
+    return fail(set_error(GPDLA_EDEVICE, "hipStreamCreate failed"));
+  e->stream = e->own_stream;
+  if (hipEventCreateWithFlags(&e->meta_done, hipEventDisableTiming) != hipSuccess)
+    return fail(set_error(GPDLA_EDEVICE, "hipEventCreate failed"));
+
+  const size_t G = model->num_rest, K = model->k;
+  std::vector<double> Mrow(G * K);
+  for (size_t g = 0; g < G; ++g)
+    for (size_t c = 0; c < K; ++c) Mrow[g * K + c] = model->M[g + c * G];  // col-major -> row-major
+  size_t dummy = 0;
+  TRY_E(grow(&e->d_rest, &dummy, G)); dummy = 0;
+  TRY_E(grow(&e->d_mu, &dummy, G)); dummy = 0;
+  TRY_E(grow(&e->d_M, &dummy, G * K)); dummy = 0;
+  TRY_E(grow(&e->d_logom, &dummy, G)); dummy = 0;
+  TRY_E(grow(&e->d_off, &dummy, (size_t)e->S)); dummy = 0;
+  TRY_E(grow(&e->d_nhi, &dummy, (size_t)e->S)); dummy = 0;
+  const std::vector<double>& lines = host_line_data();
+  TRY_E(grow(&e->d_lines, &dummy, lines.size())); dummy = 0;
+  TRY_E(grow(&e->d_status, &dummy, 1));
+  TRY_E(upload(e->d_rest, model->rest_wavelengths, G * 8, e->stream));
+  TRY_E(upload(e->d_mu, model->mu, G * 8, e->stream));
+  TRY_E(upload(e->d_M, Mrow.data(), G * K * 8, e->stream));
+  TRY_E(upload(e->d_logom, model->log_omega, G * 8, e->stream));
+  TRY_E(upload(e->d_off, samples->offset_samples, (size_t)e->S * 8, e->stream));
+  TRY_E(upload(e->d_nhi, samples->nhi_samples, (size_t)e->S * 8, e->stream));
+  TRY_E(upload(e->d_lines, lines.data(), lines.size() * 8, e->stream));
+  if (hipMemsetAsync(e->d_status, 0, 4, e->stream) != hipSuccess ||
+      hipStreamSynchronize(e->stream) != hipSuccess)
+    return fail(set_error(GPDLA_EDEVICE, "engine upload failed"));
+#undef TRY_E
+  *out = e;
+  return GPDLA_OK;
+}
+
+int gpdla_engine_set_stream(gpdla_engine* e, void* hip_stream) {
+  if (!e) return set_error(GPDLA_EINVAL, "null engine");
+  HIP_TRY(hipSetDevice(e->device));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  e->stream = hip_stream ? (hipStream_t)hip_stream : e->own_stream;
+  return GPDLA_OK;
+}
+
+int gpdla_engine_process(gpdla_engine* e, const gpdla_spectra* sp, const gpdla_results* res) {
+  if (!e || !sp || !res) return set_error(GPDLA_EINVAL, "null argument");
+  const int64_t Q = sp->num_spectra;
+  if (Q < 0) return set_error(GPDLA_EINVAL, "num_spectra < 0");
+  if (Q == 0) return GPDLA_OK;
+  if (!sp->offsets || !sp->wavelengths || !sp->flux || !sp->noise_variance || !sp->pixel_mask || !sp->z_qsos)
+    return set_error(GPDLA_EINVAL, "null spectra array");
+  if (!res->log_likelihoods_no_dla || !res->log_likelihoods_dla)
+    return set_error(GPDLA_EINVAL, "null result array");
+  if (res->sample_log_likelihoods_dla && res->sample_ld < e->S)
+    return set_error(GPDLA_EINVAL, "sample_ld (%lld) < num_samples (%lld)", (long long)res->sample_ld,
+                     (long long)e->S);
+  if (sp->offsets[0] < 0) return set_error(GPDLA_EINVAL, "offsets[0] < 0");
+  for (int64_t q = 0; q < Q; ++q)
+    if (sp->offsets[q + 1] < sp->offsets[q]) return set_error(GPDLA_EINVAL, "offsets not monotone at %lld", (long long)q);
+  const bool in_dev = sp->memory == GPDLA_MEM_DEVICE, out_dev = res->memory == GPDLA_MEM_DEVICE;
+  HIP_TRY(hipSetDevice(e->device));
+  hipStream_t st = e->stream;
+
+  const int64_t QB = e->params.max_batch_spectra > 0 ? e->params.max_batch_spectra : 1024;
+  const int row = panel_row_doubles(e->K), es = scratch_doubles(e->K);
+  const int64_t blocks_x = (e->S + 1 + kSamplesPerBlock - 1) / kSamplesPerBlock;
+
+  // pinned metadata for every batch of this call: per batch (QB+1) + 3*QB int64
+  const size_t per_batch = (size_t)(QB + 1) + 3 * (size_t)QB;
+  const int64_t nbatch = (Q + QB - 1) / QB;
+  HIP_TRY(hipEventSynchronize(e->meta_done));
+  if (e->cap_hmeta < per_batch * nbatch) {
+    if (e->h_meta) (void)hipHostFree(e->h_meta);
+    e->h_meta = nullptr;
+    e->cap_hmeta = 0;
+    HIP_TRY(hipHostMalloc((void**)&e->h_meta, per_batch * nbatch * sizeof(int64_t)));
+    e->cap_hmeta = per_batch * nbatch;
+  }
+
+  for (int64_t bi = 0; bi < nbatch; ++bi) {
+    const int64_t q0 = bi * QB, q1 = std::min(Q, q0 + QB), nq = q1 - q0;
+    int64_t* hm = e->h_meta + bi * per_batch;
+    int64_t* h_off = hm;
+    int64_t* h_sb = hm + (QB + 1);
+    int64_t* h_lb = h_sb + QB;
+    int64_t* h_cap = h_lb + QB;
+    int64_t slots = 0, lams = 0;
+    for (int64_t q = 0; q < nq; ++q) {
+      h_off[q] = sp->offsets[q0 + q] - sp->offsets[q0];
+      const int64_t lpix = sp->offsets[q0 + q + 1] - sp->offsets[q0 + q];
+      const int64_t cap = 4 * ((lpix + 3) / 4) + 4 * kChunkSteps;
+      h_sb[q] = slots;
+      h_lb[q] = lams;
+      h_cap[q] = cap;
+      slots += cap;
+      lams += cap + 8;
+    }
+    h_off[nq] = sp->offsets[q1] - sp->offsets[q0];
+    const int64_t npix = h_off[nq];
+
+    int rc;
+    if ((rc = grow(&e->d_meta, &e->cap_meta, per_batch))) return rc;
+    if ((rc = grow(&e->d_info, &e->cap_q, (size_t)QB))) return rc;
+    if ((rc = grow(&e->d_panel, &e->cap_slots, (size_t)slots * row))) return rc;
+    if ((rc = grow(&e->d_lam, &e->cap_lam, (size_t)lams))) return rc;
+    if ((rc = grow(&e->d_smap, &e->cap_smap, (size_t)slots))) return rc;
+    if ((rc = grow(&e->d_scratch, &e->cap_scr, (size_t)blocks_x * nq * kSamplesPerBlock * es))) return rc;
+    HIP_TRY(hipMemcpyAsync(e->d_meta, hm, per_batch * sizeof(int64_t), hipMemcpyHostToDevice, st));
+
+    const double *wl, *fl, *nv, *zq;
+    const uint8_t* mk;
+    const int64_t pbase = sp->offsets[q0];
+    if (in_dev) {
+      wl = sp->wavelengths + pbase; fl = sp->flux + pbase; nv = sp->noise_variance + pbase;
+      mk = sp->pixel_mask + pbase; zq = sp->z_qsos + q0;
+    } else {
+      if ((rc = grow(&e->d_wl, &e->cap_wl, (size_t)npix))) return rc;
+      if ((rc = grow(&e->d_flux, &e->cap_flux, (size_t)npix))) return rc;
+      if ((rc = grow(&e->d_noise, &e->cap_noise, (size_t)npix))) return rc;
+      if ((rc = grow(&e->d_mask, &e->cap_mask, (size_t)npix))) return rc;
+      if ((rc = grow(&e->d_z, &e->cap_z, (size_t)nq))) return rc;
+      HIP_TRY(hipMemcpyAsync(e->d_wl, sp->wavelengths + pbase, npix * 8, hipMemcpyHostToDevice, st));
+      HIP_TRY(hipMemcpyAsync(e->d_flux, sp->flux + pbase, npix * 8, hipMemcpyHostToDevice, st));
+      HIP_TRY(hipMemcpyAsync(e->d_noise, sp->noise_variance + pbase, npix * 8, hipMemcpyHostToDevice, st));
+      HIP_TRY(hipMemcpyAsync(e->d_mask, sp->pixel_mask + pbase, npix, hipMemcpyHostToDevice, st));
+      HIP_TRY(hipMemcpyAsync(e->d_z, sp->z_qsos + q0, nq * 8, hipMemcpyHostToDevice, st));
+      wl = e->d_wl; fl = e->d_flux; nv = e->d_noise; mk = e->d_mask; zq = e->d_z;
+    }
+
+    // outputs: device results are written in place; host results go through workspaces
+    double *o_sll, *o_null, *o_dla, *o_zmin, *o_zmax;
+    int32_t* o_npix;
+    int64_t ld;
+    const bool need_internal_sll = !out_dev || !res->sample_log_likelihoods_dla;
+    if (need_internal_sll) {
+      if ((rc = grow(&e->d_sll, &e->cap_sll, (size_t)nq * e->S))) return rc;
+    }
+    if (out_dev) {
+      o_sll = res->sample_log_likelihoods_dla ? res->sample_log_likelihoods_dla + q0 * res->sample_ld : e->d_sll;
+      ld = res->sample_log_likelihoods_dla ? res->sample_ld : e->S;
+      o_null = res->log_likelihoods_no_dla + q0;
+      o_dla = res->log_likelihoods_dla + q0;
+      o_zmin = res->min_z_dlas ? res->min_z_dlas + q0 : nullptr;
+      o_zmax = res->max_z_dlas ? res->max_z_dlas + q0 : nullptr;
+      o_npix = res->num_pixels ? res->num_pixels + q0 : nullptr;
+    } else {
+      if (e->cap_qout < (size_t)QB) {
+        for (double** p : {&e->d_llnull, &e->d_lldla, &e->d_zmin, &e->d_zmax})
+          if (*p) { (void)hipFree(*p); *p = nullptr; }
+        if (e->d_npix) { (void)hipFree(e->d_npix); e->d_npix = nullptr; }
+        size_t a1 = 0, a2 = 0, a3 = 0, a4 = 0, a5 = 0;
+        if ((rc = grow(&e->d_llnull, &a1, (size_t)QB))) return rc;
+        if ((rc = grow(&e->d_lldla, &a2, (size_t)QB))) return rc;
+        if ((rc = grow(&e->d_zmin, &a3, (size_t)QB))) return rc;
+        if ((rc = grow(&e->d_zmax, &a4, (size_t)QB))) return rc;
+        if ((rc = grow(&e->d_npix, &a5, (size_t)QB))) return rc;
+        e->cap_qout = QB;
+      }
+      o_sll = e->d_sll; ld = e->S;
+      o_null = e->d_llnull; o_dla = e->d_lldla; o_zmin = e->d_zmin; o_zmax = e->d_zmax; o_npix = e->d_npix;
+    }
+
+    PrepArgs pa{};
+    pa.q_count = (int32_t)nq;
+    pa.offsets = e->d_meta;
+    pa.wavelengths = wl; pa.flux = fl; pa.noise = nv; pa.mask = mk; pa.z_qsos = zq;
+    pa.slot_base = e->d_meta + (QB + 1);
+    pa.lam_base = pa.slot_base + QB;
+    pa.slot_cap = pa.lam_base + QB;
+    pa.num_rest = e->num_rest;
+    pa.rest = e->d_rest; pa.mu = e->d_mu; pa.M_rowmajor = e->d_M; pa.log_omega = e->d_logom;
+    pa.c_0 = e->c0; pa.tau_0 = e->tau0; pa.beta = e->beta;
+    pa.min_lambda = e->params.min_lambda; pa.max_lambda = e->params.max_lambda;
+    pa.lya = e->params.lya_wavelength; pa.lyman_limit = e->params.lyman_limit;
+    pa.min_z_cut = e->params.min_z_cut; pa.max_z_cut = e->params.max_z_cut;
+    pa.pixel_spacing = e->params.pixel_spacing;
+    pa.absorption_mode = e->params.absorption_mode;
+    pa.info = e->d_info; pa.panel = e->d_panel; pa.lam_pad = e->d_lam; pa.slot_pixel = e->d_smap;
+
+    LikelihoodArgs la{};
+    la.q_count = (int32_t)nq;
+    la.info = e->d_info; la.panel = e->d_panel; la.lam_pad = e->d_lam;
+    la.offsets = e->d_off; la.nhi = e->d_nhi; la.S = e->S;
+    la.num_lines = e->params.num_lines;
+    la.line_tabs = e->d_lines;
+    la.line_mult = e->d_lines + (size_t)kMaxLines * kLineTableStride;
+    la.scratch = e->d_scratch;
+    la.sample_ll = o_sll; la.ld = ld; la.ll_null = o_null; la.status = e->d_status;
+
+    ReduceArgs ra{};
+    ra.q_count = (int32_t)nq; ra.info = e->d_info; ra.sample_ll = o_sll; ra.ld = ld; ra.S = e->S;
+    ra.ll_dla = o_dla; ra.zmin = o_zmin; ra.zmax = o_zmax; ra.num_pixels = o_npix;
+
+    TimedLaunch t0{}, t1{}, t2{};
+    if ((rc = record_start(e, &t0, 0))) return rc;
+    HIP_TRY(launch_prep(e->K, pa, st));
+    HIP_TRY(hipEventRecord(t0.stop, st));
+    e->pending.push_back(t0);
+    if ((rc = record_start(e, &t1, 1))) return rc;
+    HIP_TRY(launch_likelihood(e->K, la, st));
+    HIP_TRY(hipEventRecord(t1.stop, st));
+    e->pending.push_back(t1);
+    if ((rc = record_start(e, &t2, 2))) return rc;
+    HIP_TRY(launch_reduce(ra, st));
+    HIP_TRY(hipEventRecord(t2.stop, st));
+    e->pending.push_back(t2);
+
+    e->stats.spectra += nq;
+    e->stats.sample_evals += nq * e->S;
+
+    if (!out_dev) {
+      HIP_TRY(hipMemcpyAsync(res->log_likelihoods_no_dla + q0, o_null, nq * 8, hipMemcpyDeviceToHost, st));
+      HIP_TRY(hipMemcpyAsync(res->log_likelihoods_dla + q0, o_dla, nq * 8, hipMemcpyDeviceToHost, st));
+      if (res->min_z_dlas) HIP_TRY(hipMemcpyAsync(res->min_z_dlas + q0, o_zmin, nq * 8, hipMemcpyDeviceToHost, st));
+      if (res->max_z_dlas) HIP_TRY(hipMemcpyAsync(res->max_z_dlas + q0, o_zmax, nq * 8, hipMemcpyDeviceToHost, st));
+      if (res->num_pixels) HIP_TRY(hipMemcpyAsync(res->num_pixels + q0, o_npix, nq * 4, hipMemcpyDeviceToHost, st));
+      if (res->sample_log_likelihoods_dla)
+        HIP_TRY(hipMemcpy2DAsync(res->sample_log_likelihoods_dla + q0 * res->sample_ld, res->sample_ld * 8,
+                                 o_sll, e->S * 8, e->S * 8, nq, hipMemcpyDeviceToHost, st));
+      // host results: the workspaces are reused by the next batch, so drain here
+      HIP_TRY(hipStreamSynchronize(st));
+    } else if (!in_dev) {
+      // host inputs were staged in reusable workspaces
+      HIP_TRY(hipStreamSynchronize(st));
+    }
+    // otherwise the next batch reuses panel / scratch workspaces in stream order
+  }
+  HIP_TRY(hipEventRecord(e->meta_done, st));
+  if (!out_dev) return gpdla_engine_synchronize(e);
+  return GPDLA_OK;
+}
+
+int gpdla_engine_synchronize(gpdla_engine* e) {
+  if (!e) return set_error(GPDLA_EINVAL, "null engine");
+  HIP_TRY(hipSetDevice(e->device));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  int rc = resolve_events(e);
+  if (rc) return rc;
+  int32_t status = 0;
+  HIP_TRY(hipMemcpy(&status, e->d_status, 4, hipMemcpyDeviceToHost));
+  if (status) {
+    HIP_TRY(hipMemset(e->d_status, 0, 4));
+    return set_error(GPDLA_ENUMERIC, "non-positive pivot or non-finite likelihood (outputs NaN)");
+  }
+  return GPDLA_OK;
+}
+
+int gpdla_engine_get_stats(gpdla_engine* e, gpdla_stats* s) {
+  if (!e || !s) return set_error(GPDLA_EINVAL, "null argument");
+  HIP_TRY(hipSetDevice(e->device));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  int rc = resolve_events(e);
+  if (rc) return rc;
+  *s = e->stats;
+  return GPDLA_OK;
+}
+
+int gpdla_engine_reset_stats(gpdla_engine* e) {
+  if (!e) return set_error(GPDLA_EINVAL, "null engine");
+  HIP_TRY(hipSetDevice(e->device));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  int rc = resolve_events(e);
+  if (rc) return rc;
+  e->stats = gpdla_stats{};
+  return GPDLA_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// device buffer helpers
+// ---------------------------------------------------------------------------------------------
+int gpdla_device_malloc(int32_t device, int64_t bytes, void** ptr) {
+  if (!ptr || bytes < 0) return set_error(GPDLA_EINVAL, "bad argument");
+  *ptr = nullptr;
+  int rc = check_device(device);
+  if (rc) return rc;
+  HIP_TRY(hipSetDevice(device));
+  HIP_TRY(hipMalloc(ptr, bytes > 0 ? bytes : 1));
+  return GPDLA_OK;
+}
+
+int gpdla_device_free(int32_t device, void* ptr) {
+  int rc = check_device(device);
+  if (rc) return rc;
+  HIP_TRY(hipSetDevice(device));
+  if (ptr) HIP_TRY(hipFree(ptr));
+  return GPDLA_OK;
+}
+
+int gpdla_memcpy_htod(int32_t device, void* dst, const void* src, int64_t bytes) {
+  int rc = check_device(device);
+  if (rc) return rc;
+  HIP_TRY(hipSetDevice(device));
+  HIP_TRY(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
+  return GPDLA_OK;
+}
+
+int gpdla_memcpy_dtoh(int32_t device, void* dst, const void* src, int64_t bytes) {
+  int rc = check_device(device);
+  if (rc) return rc;
+  HIP_TRY(hipSetDevice(device));
+  HIP_TRY(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+  return GPDLA_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// standalone entry points (host buffers)
+// ---------------------------------------------------------------------------------------------
+static int lines_on_device(double** d_lines) {
+  static std::mutex mu;
+  static std::vector<double*> per_dev;
+  int dev = 0;
+  HIP_TRY(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> lock(mu);
+  if ((int)per_dev.size() <= dev) per_dev.resize(dev + 1, nullptr);
+  if (!per_dev[dev]) {
+    const std::vector<double>& lines = host_line_data();
+    double* p = nullptr;
+    HIP_TRY(hipMalloc((void**)&p, lines.size() * 8));
+    HIP_TRY(hipMemcpy(p, lines.data(), lines.size() * 8, hipMemcpyHostToDevice));
+    per_dev[dev] = p;
+  }
+  *d_lines = per_dev[dev];
+  return GPDLA_OK;
+}
+
+int gpdla_voigt_batch_f64(const double* lambdas, int64_t n_padded, const double* z, const double* N,
+                          int64_t count, int32_t num_lines, double* out) {
+  if (!lambdas || !z || !N || !out) return set_error(GPDLA_EINVAL, "null argument");
+  if (n_padded <= 2 * kWidth) return set_error(GPDLA_EINVAL, "need more than %d wavelengths", 2 * kWidth);
+  if (num_lines < 1 || num_lines > kMaxLines) return set_error(GPDLA_EINVAL, "num_lines=%d outside [1, 31]", num_lines);
+  if (count < 1) return GPDLA_OK;
+  int rc = check_device(0);
+  if (rc) return rc;
+  double* d_lines = nullptr;
+  if ((rc = lines_on_device(&d_lines))) return rc;
+  const int64_t n_out = n_padded - 2 * kWidth;
+  double *d_lam = nullptr, *d_z = nullptr, *d_N = nullptr, *d_out = nullptr;
+  auto cleanup = [&] { for (double* p : {d_lam, d_z, d_N, d_out}) if (p) (void)hipFree(p); };
+  hipError_t err = hipMalloc((void**)&d_lam, n_padded * 8);
+  if (err == hipSuccess) err = hipMalloc((void**)&d_z, count * 8);
+  if (err == hipSuccess) err = hipMalloc((void**)&d_N, count * 8);
+  if (err == hipSuccess) err = hipMalloc((void**)&d_out, count * n_out * 8);
+  if (err == hipSuccess) err = hipMemcpy(d_lam, lambdas, n_padded * 8, hipMemcpyHostToDevice);
+  if (err == hipSuccess) err = hipMemcpy(d_z, z, count * 8, hipMemcpyHostToDevice);
+  if (err == hipSuccess) err = hipMemcpy(d_N, N, count * 8, hipMemcpyHostToDevice);
+  if (err == hipSuccess) err = launch_voigt_batch(d_lam, n_padded, d_z, d_N, count, num_lines, d_lines, d_out, nullptr);
+  if (err == hipSuccess) err = hipMemcpy(out, d_out, count * n_out * 8, hipMemcpyDeviceToHost);
+  cleanup();
+  if (err != hipSuccess) return set_error(GPDLA_EDEVICE, "voigt: %s", hipGetErrorString(err));
+  return GPDLA_OK;
+}
+
+int gpdla_voigt_f64(const double* lambdas, int64_t n_padded, double z, double N, int32_t num_lines,
+                    double* out) {
+  return gpdla_voigt_batch_f64(lambdas, n_padded, &z, &N, 1, num_lines, out);
+}
+
+int gpdla_log_mvnpdf_low_rank_f64(const double* y, const double* mu, const double* M, const double* d,
+                                  int64_t n, int32_t k, double* out) {
+  if (!y || !mu || !M || !d || !out) return set_error(GPDLA_EINVAL, "null argument");
+  if (n < 1 || k < 1) return set_error(GPDLA_EINVAL, "n=%lld k=%d", (long long)n, k);
+  if (k > 64) return set_error(GPDLA_EUNSUPPORTED, "k=%d > 64 in the standalone entry point", k);
+  int rc = check_device(0);
+  if (rc) return rc;
+  double *dy = nullptr, *dmu = nullptr, *dM = nullptr, *dd = nullptr, *dout = nullptr;
+  int32_t* dst = nullptr;
+  hipError_t err = hipMalloc((void**)&dy, n * 8);
+  if (err == hipSuccess) err = hipMalloc((void**)&dmu, n * 8);
+  if (err == hipSuccess) err = hipMalloc((void**)&dM, n * k * 8);
+  if (err == hipSuccess) err = hipMalloc((void**)&dd, n * 8);
+  if (err == hipSuccess) err = hipMalloc((void**)&dout, 8);
+  if (err == hipSuccess) err = hipMalloc((void**)&dst, 4);
+  if (err == hipSuccess) err = hipMemset(dst, 0, 4);
+  if (err == hipSuccess) err = hipMemcpy(dy, y, n * 8, hipMemcpyHostToDevice);
+  if (err == hipSuccess) err = hipMemcpy(dmu, mu, n * 8, hipMemcpyHostToDevice);
+  if (err == hipSuccess) err = hipMemcpy(dM, M, n * k * 8, hipMemcpyHostToDevice);
+  if (err == hipSuccess) err = hipMemcpy(dd, d, n * 8, hipMemcpyHostToDevice);
+  if (err == hipSuccess) err = launch_mvn_single(dy, dmu, dM, dd, n, k, dout, dst, nullptr);
+  int32_t status = 0;
+  if (err == hipSuccess) err = hipMemcpy(out, dout, 8, hipMemcpyDeviceToHost);
+  if (err == hipSuccess) err = hipMemcpy(&status, dst, 4, hipMemcpyDeviceToHost);
+  for (void* p : {(void*)dy, (void*)dmu, (void*)dM, (void*)dd, (void*)dout, (void*)dst})
+    if (p) (void)hipFree(p);
+  if (err != hipSuccess) return set_error(GPDLA_EDEVICE, "log_mvnpdf_low_rank: %s", hipGetErrorString(err));
+  if (status) return set_error(GPDLA_ENUMERIC, "B = I + M'D^-1M is not positive definite");
+  return GPDLA_OK;
+}
+
+}  // extern "C"

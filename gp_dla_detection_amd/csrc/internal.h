@@ -1,0 +1,140 @@
+// Internal declarations shared by the kernels and the C-ABI layer.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+#include "line_profile.h"
+#include "lyman_series.h"
+
+namespace gpdla {
+
+// ---------------------------------------------------------------------------------------------
+// Device data layout (HBM)
+//
+// A spectrum is turned into J "slots" (pixels the likelihood sweeps).  In reference mode slot j is
+// the j-th unmasked in-range pixel and its absorption is the j-th value of the m-point profile
+// (process_qsos.m:180,189); in unmasked mode J = m and masked slots carry weight 0.
+//
+// The sweep is split into 4 contiguous segments of L = ceil(J/4) slots (segment g = slots
+// [gL, gL+L)); lanes g = 0..3 of a wave walk their segment in step, so the 7-tap instrument
+// convolution is a register sliding window and the 4 segments form the K=4 dimension of a
+// v_mfma_f64_4x4x4_4b.
+//
+// Panel row (one per slot, kRow doubles, 16-byte aligned): the Khatri-Rao row
+//     e < NGRAM      : M_r * M_c  for Gram pair e = (r, c), r <= c (row-major upper triangle)
+//     NGRAM..4GT-1   : 0 (tile padding)
+//     4GT + i, i < K : M_i                       (the u = M' D^-1 diag(a) r contraction)
+// stored permuted as row[(e & 3) * JS + (e >> 2)], so a lane with j = e & 3 reads consecutive
+// tiles with one ds_read_b128.  Spare words per j hold the slot scalars.
+// ---------------------------------------------------------------------------------------------
+template <int K>
+struct Layout {
+  static constexpr int kNGram = K * (K + 1) / 2;
+  static constexpr int kGT = (kNGram + 3) / 4;  // Gram tiles (4 entries each)
+  static constexpr int kUT = (K + 3) / 4;       // u tiles
+  static constexpr int kTiles = kGT + kUT;
+  static constexpr int kJS = ((kTiles + 2) + 1) & ~1;  // per-j stride (doubles), even
+  static constexpr int kRow = 4 * kJS;                 // doubles per slot row
+  static constexpr int kES = 4 * kTiles + 8;           // scratch doubles per sample
+  // slot scalars in the spare words
+  static constexpr int kLam = 0 * kJS + kTiles;        // padded wavelength at slot + 6
+  static constexpr int kY = 0 * kJS + kTiles + 1;
+  static constexpr int kNoise = 1 * kJS + kTiles;
+  static constexpr int kMu = 1 * kJS + kTiles + 1;
+  static constexpr int kOmega2 = 2 * kJS + kTiles;
+  static constexpr int kValid = 2 * kJS + kTiles + 1;
+};
+
+struct SpecInfo {
+  int32_t J;          // slots (0 => unusable spectrum)
+  int32_t L;          // segment length ceil(J/4)
+  int32_t n;          // unmasked in-range pixels (the n in n*log(2 pi))
+  int32_t m;          // in-range pixels including masked
+  double zmin, zmax;  // process_qsos.m:160-161
+  int64_t slot_base;  // first panel row of this spectrum
+  int64_t lam_base;   // first element of this spectrum's padded-wavelength array
+  int32_t flags;
+  int32_t pad_;
+};
+
+constexpr int kChunkSteps = 4;       // pixel steps staged per LDS chunk
+constexpr int kSamplesPerWave = 16;
+constexpr int kWavesPerBlock = 4;
+constexpr int kSamplesPerBlock = kSamplesPerWave * kWavesPerBlock;
+
+struct PrepArgs {
+  int32_t q_count;
+  const int64_t* offsets;        // device, [q_count + 1], relative to the pixel arrays below
+  const double* wavelengths;
+  const double* flux;
+  const double* noise;
+  const uint8_t* mask;
+  const double* z_qsos;          // device, [q_count]
+  const int64_t* slot_base;      // device, [q_count]
+  const int64_t* lam_base;       // device, [q_count]
+  const int64_t* slot_cap;       // device, [q_count]
+  // model (device, rest grid row-major [G][K])
+  int32_t num_rest;
+  const double* rest;
+  const double* mu;
+  const double* M_rowmajor;
+  const double* log_omega;
+  double c_0, tau_0, beta;
+  // params
+  double min_lambda, max_lambda, lya, lyman_limit, min_z_cut, max_z_cut, pixel_spacing;
+  int32_t absorption_mode;
+  // outputs
+  SpecInfo* info;
+  double* panel;
+  double* lam_pad;
+  int32_t* slot_pixel;           // scratch map slot -> pixel (size = total slot capacity)
+};
+
+struct LikelihoodArgs {
+  int32_t q_count;
+  const SpecInfo* info;
+  const double* panel;
+  const double* lam_pad;
+  const double* offsets;         // [S] offset samples
+  const double* nhi;             // [S]
+  int64_t S;
+  int32_t num_lines;
+  const double* line_tabs;       // [num_lines][kLineTableStride]
+  const double* line_mult;       // [num_lines] c / lambda_j (host-precomputed pieces), see kernel
+  double* scratch;               // [grid blocks][64][kES]
+  double* sample_ll;             // [q_count][ld] or nullptr
+  int64_t ld;
+  double* ll_null;               // [q_count]
+  int32_t* status;
+};
+
+struct ReduceArgs {
+  int32_t q_count;
+  const SpecInfo* info;
+  const double* sample_ll;
+  int64_t ld;
+  int64_t S;
+  double* ll_dla;
+  double* zmin;
+  double* zmax;
+  int32_t* num_pixels;
+};
+
+hipError_t launch_prep(int K, const PrepArgs& a, hipStream_t s);
+hipError_t launch_likelihood(int K, const LikelihoodArgs& a, hipStream_t s);
+hipError_t launch_reduce(const ReduceArgs& a, hipStream_t s);
+hipError_t launch_voigt_batch(const double* lambdas, int64_t n_padded, const double* z,
+                              const double* N, int64_t count, int32_t num_lines,
+                              const double* line_tabs, double* out, hipStream_t s);
+hipError_t launch_mvn_single(const double* y, const double* mu, const double* M_colmajor,
+                             const double* d, int64_t n, int32_t k, double* out,
+                             int32_t* status, hipStream_t s);
+bool rank_supported(int K);
+int panel_row_doubles(int K);
+int scratch_doubles(int K);
+
+// host-side table fitting (faddeeva_host.cpp)
+double fit_line_table(int line, double* tab);
+
+}  // namespace gpdla

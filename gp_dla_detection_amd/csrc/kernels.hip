@@ -1,0 +1,766 @@
+// HIP kernels for gfx950 (MI355X): spectrum preparation, the fused
+// Voigt x low-rank-Gaussian likelihood sweep, and the per-spectrum log-mean-exp.
+//
+// Reference path (sbird/gp_dla_detection): process_qsos.m:96-212, voigt.c:253-304,
+// log_mvnpdf_low_rank.m:5-33.  See DESIGN.md for the data layout and roofline.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+
+#include "internal.h"
+
+namespace gpdla {
+
+namespace {
+
+constexpr double kLog2Pi = 1.83787706640934534;  // log_mvnpdf_low_rank.m:7
+constexpr double kLn2 = 0.693147180559945309417;
+
+// ---------------------------------------------------------------------------------------------
+// small device helpers
+// ---------------------------------------------------------------------------------------------
+__device__ inline double rcp_nr(double d) {
+  // v_rcp_f64 (~2^-26) refined by two Newton steps -> within 1 ulp of 1/d
+  double r = __builtin_amdgcn_rcp(d);
+  double e = fma(-d, r, 1.0);
+  r = fma(r, e, r);
+  e = fma(-d, r, 1.0);
+  return fma(r, e, r);
+}
+
+template <int SRC>
+__device__ inline double quad_bcast_c(double v) {
+  int lo = __double2loint(v), hi = __double2hiint(v);
+  lo = __builtin_amdgcn_mov_dpp(lo, SRC * 0x55, 0xF, 0xF, false);
+  hi = __builtin_amdgcn_mov_dpp(hi, SRC * 0x55, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+
+// value of lane (quad_base + src) broadcast to the 4 lanes of each quad; src folds to a
+// constant after unrolling
+__device__ inline double quad_bcast(double v, int src) {
+  switch (src & 3) {
+    case 0: return quad_bcast_c<0>(v);
+    case 1: return quad_bcast_c<1>(v);
+    case 2: return quad_bcast_c<2>(v);
+    default: return quad_bcast_c<3>(v);
+  }
+}
+
+__device__ inline int wave_incl_scan(int v) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    int t = __shfl_up(v, off);
+    if (lane >= off) v += t;
+  }
+  return v;
+}
+
+// exclusive block scan over 256 threads; returns exclusive prefix, total via *total
+__device__ inline int block_excl_scan(int v, int* lds4, int* total) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  int inc = wave_incl_scan(v);
+  if (lane == 63) lds4[wave] = inc;
+  __syncthreads();
+  int woff = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    int c = lds4[w];
+    if (w < wave) woff += c;
+    tot += c;
+  }
+  __syncthreads();
+  *total = tot;
+  return woff + inc - v;
+}
+
+__device__ inline double block_reduce_min(double v, double* lds4) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = fmin(v, __shfl_xor(v, off));
+  if (lane == 0) lds4[wave] = v;
+  __syncthreads();
+  double r = fmin(fmin(lds4[0], lds4[1]), fmin(lds4[2], lds4[3]));
+  __syncthreads();
+  return r;
+}
+
+__device__ inline double block_reduce_max(double v, double* lds4) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = fmax(v, __shfl_xor(v, off));
+  if (lane == 0) lds4[wave] = v;
+  __syncthreads();
+  double r = fmax(fmax(lds4[0], lds4[1]), fmax(lds4[2], lds4[3]));
+  __syncthreads();
+  return r;
+}
+
+__device__ inline double block_reduce_sum(double v, double* lds4) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+  if (lane == 0) lds4[wave] = v;
+  __syncthreads();
+  double r = (lds4[0] + lds4[1]) + (lds4[2] + lds4[3]);
+  __syncthreads();
+  return r;
+}
+
+// Gram pair e -> (r, c), row-major upper triangle (r <= c)
+template <int K>
+__device__ inline void gram_pair(int e, int& r, int& c) {
+  int rr = 0, start = 0;
+  while (rr < K - 1 && e >= start + (K - rr)) {
+    start += K - rr;
+    ++rr;
+  }
+  r = rr;
+  c = rr + (e - start);
+}
+
+template <int K>
+__device__ __host__ constexpr int gram_index(int r, int c) {
+  return r * K - r * (r - 1) / 2 + (c - r);
+}
+
+// numpy.interp-style linear interpolation index on a strictly increasing grid
+__device__ inline int interp_index(const double* xp, int G, double x) {
+  int lo = 0, hi = G - 1;  // invariant xp[lo] <= x < xp[hi] (x inside the grid)
+  while (hi - lo > 1) {
+    int mid = (lo + hi) >> 1;
+    if (xp[mid] <= x) lo = mid; else hi = mid;
+  }
+  return lo;
+}
+
+__device__ inline double interp_eval(const double* xp, const double* fp, int G, int j, double x) {
+  if (x >= xp[G - 1]) return fp[G - 1];
+  const double slope = (fp[j + 1] - fp[j]) / (xp[j + 1] - xp[j]);
+  return slope * (x - xp[j]) + fp[j];
+}
+
+// ---------------------------------------------------------------------------------------------
+// Voigt raw profile at one padded wavelength: exp(N * total), total = -sum_j lc_j V_j(v_j)
+// (voigt.c:282-292).  `a_j` = c/(lambda_j 1e8) / (1+z) / (sigma sqrt 2) per line is formed from
+// the host-computed line factor and the lane's 1/(1+z).
+// ---------------------------------------------------------------------------------------------
+__device__ inline double raw_profile(double lam, double zfac, double N, int num_lines,
+                                     const double* __restrict__ line_tabs,
+                                     const double* __restrict__ line_mult) {
+  constexpr double kC2 = kCcgs / (kSigma * 1.41421356237309504880);  // c / (sigma sqrt 2)
+  double total = 0.0;
+  for (int j = 0; j < num_lines; ++j) {
+    const double aj = line_mult[j] * zfac;
+    const double x = fma(lam, aj, -kC2);
+    total -= line_profile_eval(line_tabs + j * kLineTableStride, x);
+  }
+  return exp(N * total);
+}
+
+// ---------------------------------------------------------------------------------------------
+// prep: process_qsos.m:96-177 for one spectrum per block.  Builds the slot panel (interpolated
+// model, Khatri-Rao rows, slot scalars), the padded wavelength grid and the spectrum info.
+// ---------------------------------------------------------------------------------------------
+template <int K>
+__global__ __launch_bounds__(256) void prep_kernel(PrepArgs a) {
+  using Lay = Layout<K>;
+  __shared__ int s_i4[4];
+  __shared__ double s_d4[4];
+  const int q = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int64_t pb = a.offsets[q];
+  const int Lpix = (int)(a.offsets[q + 1] - pb);
+  const double z = a.z_qsos[q];
+  const double* wl = a.wavelengths + pb;
+  const uint8_t* mk = a.mask + pb;
+
+  const int chunk = (Lpix + 255) / 256;
+  const int i0 = min(tid * chunk, Lpix), i1 = min(i0 + chunk, Lpix);
+  int c_in = 0, c_un = 0;
+  double mn_in = INFINITY, mx_in = -INFINITY, mn_un = INFINITY, mx_un = -INFINITY;
+  for (int i = i0; i < i1; ++i) {
+    const double lam = wl[i];
+    const double rest = lam / (1 + z);                                  // :102
+    const bool inr = (rest >= a.min_lambda) && (rest <= a.max_lambda);  // :104-105
+    const bool un = inr && (mk[i] == 0);                                // :111
+    c_in += inr;
+    c_un += un;
+    if (inr) { mn_in = fmin(mn_in, lam); mx_in = fmax(mx_in, lam); }
+    if (un) { mn_un = fmin(mn_un, lam); mx_un = fmax(mx_un, lam); }
+  }
+  int m = 0, n = 0;
+  int pos_in = block_excl_scan(c_in, s_i4, &m);
+  int pos_un = block_excl_scan(c_un, s_i4, &n);
+  mn_in = block_reduce_min(mn_in, s_d4);
+  mx_in = block_reduce_max(mx_in, s_d4);
+  mn_un = block_reduce_min(mn_un, s_d4);
+  mx_un = block_reduce_max(mx_un, s_d4);
+
+  const int J = (n > 0 && m > 0) ? (a.absorption_mode ? m : n) : 0;
+  const int L = (J + 3) / 4;
+  const int64_t sb = a.slot_base[q], lb = a.lam_base[q];
+  const int64_t cap = a.slot_cap[q];
+  double* lam_pad = a.lam_pad + lb;
+  int32_t* smap = a.slot_pixel + sb;
+
+  // pass 2: scatter in-range wavelengths and the slot -> pixel map
+  for (int i = i0; i < i1; ++i) {
+    const double lam = wl[i];
+    const double rest = lam / (1 + z);
+    const bool inr = (rest >= a.min_lambda) && (rest <= a.max_lambda);
+    const bool un = inr && (mk[i] == 0);
+    if (inr) {
+      lam_pad[3 + pos_in] = lam;                                        // :109,173
+      if (a.absorption_mode) smap[pos_in] = un ? i : -1;
+      ++pos_in;
+    }
+    if (un) {
+      if (!a.absorption_mode) smap[pos_un] = i;
+      ++pos_un;
+    }
+  }
+  // padded ends: [logspace(lo - w s, lo - s, w)'; lambda_m; logspace(hi + s, hi + w s, w)'] (:169-177)
+  if (m > 0 && tid < 2 * kWidth) {
+    const double sp = a.pixel_spacing;
+    const double ws = kWidth * sp;
+    if (tid < kWidth) {
+      const double lo = log10(mn_in);
+      const double d1 = lo - ws, d2 = lo - sp;
+      const double v = (tid == kWidth - 1) ? d2 : d1 + tid * ((d2 - d1) / (kWidth - 1));
+      lam_pad[tid] = pow(10.0, v);
+    } else {
+      const int t = tid - kWidth;
+      const double hi = log10(mx_in);
+      const double d1 = hi + sp, d2 = hi + ws;
+      const double v = (t == kWidth - 1) ? d2 : d1 + t * ((d2 - d1) / (kWidth - 1));
+      lam_pad[3 + m + t] = pow(10.0, v);
+    }
+  }
+  // replicate the last padded wavelength over the capacity tail (keeps every window finite)
+  {
+    const double last = m > 0 ? pow(10.0, log10(mx_in) + kWidth * a.pixel_spacing) : 1.0;
+    const int64_t first = m > 0 ? (int64_t)m + 2 * kWidth : 0;
+    for (int64_t i = first + tid; i < cap + 8; i += 256) lam_pad[i] = last;
+  }
+  if (tid == 0) {
+    SpecInfo inf;
+    inf.J = J;
+    inf.L = L;
+    inf.n = n;
+    inf.m = m;
+    inf.zmin = n > 0 ? fmax(mn_un / a.lya - 1, (a.lyman_limit * (1 + z)) / a.lya - 1 + a.min_z_cut) : NAN;
+    inf.zmax = n > 0 ? (mx_un / a.lya - 1) - a.max_z_cut : NAN;
+    inf.slot_base = sb;
+    inf.lam_base = lb;
+    inf.flags = (J == 0);
+    inf.pad_ = 0;
+    a.info[q] = inf;
+  }
+  __syncthreads();
+
+  // pass 3: panel rows, one wave per slot, lanes over entries
+  const int lane = tid & 63, wave = tid >> 6;
+  const double* rest_g = a.rest;
+  const int G = a.num_rest;
+  for (int64_t j = wave; j < cap; j += 4) {
+    double* row = a.panel + (sb + j) * Lay::kRow;
+    const int pix = (j < J) ? smap[j] : -1;
+    const double lam_lead = lam_pad[j + 2 * kWidth];
+    if (pix >= 0) {
+      const double lam = wl[pix];
+      const double rest = lam / (1 + z);
+      const int gi = interp_index(rest_g, G, rest);
+      const bool at_end = rest >= rest_g[G - 1];
+      const double* M0 = a.M_rowmajor + (int64_t)gi * K;
+      const double* M1 = a.M_rowmajor + (int64_t)(at_end ? gi : gi + 1) * K;
+      const double x0 = rest_g[gi], x1 = rest_g[at_end ? gi : gi + 1];
+      auto Mi = [&](int col) {
+        if (at_end) return a.M_rowmajor[(int64_t)(G - 1) * K + col];
+        const double slope = (M1[col] - M0[col]) / (x1 - x0);
+        return slope * (rest - x0) + M0[col];
+      };
+      for (int e = lane; e < 4 * Lay::kTiles; e += 64) {
+        double v = 0.0;
+        if (e < Lay::kNGram) {
+          int r, c;
+          gram_pair<K>(e, r, c);
+          v = Mi(r) * Mi(c);
+        } else if (e >= 4 * Lay::kGT && e - 4 * Lay::kGT < K) {
+          v = Mi(e - 4 * Lay::kGT);
+        }
+        row[(e & 3) * Lay::kJS + (e >> 2)] = v;
+      }
+      if (lane == 0) {
+        const double mu = interp_eval(rest_g, a.mu, G, gi, rest);             // :139
+        const double lom = interp_eval(rest_g, a.log_omega, G, gi, rest);     // :142
+        const double lya_z = (lam - a.lya) / a.lya;                           // :118-120
+        double om2 = exp(2 * lom);                                            // :143
+        const double sf = 1 - exp(-a.tau_0 * pow(1 + lya_z, a.beta)) + a.c_0;  // :145
+        om2 = om2 * (sf * sf);                                                // :147
+        row[Lay::kLam] = lam_lead;
+        row[Lay::kY] = a.flux[pb + pix];
+        row[Lay::kNoise] = a.noise[pb + pix];
+        row[Lay::kMu] = mu;
+        row[Lay::kOmega2] = om2;
+        row[Lay::kValid] = 1.0;
+      }
+    } else {
+      for (int e = lane; e < 4 * Lay::kTiles; e += 64) row[(e & 3) * Lay::kJS + (e >> 2)] = 0.0;
+      if (lane == 0) {
+        row[Lay::kLam] = lam_lead;
+        row[Lay::kY] = 0.0;
+        row[Lay::kNoise] = 1.0;
+        row[Lay::kMu] = 0.0;
+        row[Lay::kOmega2] = 0.0;
+        row[Lay::kValid] = 0.0;
+      }
+    }
+    // zero the remaining spare words
+    for (int w = lane; w < Lay::kRow; w += 64) {
+      const int jj = w / Lay::kJS, t = w % Lay::kJS;
+      if (t >= Lay::kTiles && !((jj == 0 || jj == 1 || jj == 2) && t < Lay::kTiles + 2)) row[w] = 0.0;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// likelihood: for one spectrum (blockIdx.y) and 64 samples (4 waves x 16), sweep all slots:
+//   per lane (sample s = lane & 15, segment g = lane >> 4): Voigt raw profile at the leading
+//   padded wavelength, 7-tap convolution from a register window, DLA-modulated pixel terms
+//   a^2/d and a r/d (process_qsos.m:189-197), then v_mfma_f64_4x4x4_4b over the 58 Khatri-Rao
+//   tiles (Gram + u).  Epilogue: per-sample augmented LDL^T (quad of lanes per sample) ->
+//   log N(y; a mu, diag(a) M M' diag(a) + diag(a^2 w^2 + sigma^2)) (log_mvnpdf_low_rank.m).
+// ---------------------------------------------------------------------------------------------
+template <int K>
+__global__ __launch_bounds__(256) void likelihood_kernel(LikelihoodArgs a) {
+  using Lay = Layout<K>;
+  constexpr int kTiles = Lay::kTiles;
+  constexpr int kGT = Lay::kGT;
+  constexpr int kRow = Lay::kRow;
+  constexpr int kJS = Lay::kJS;
+  __shared__ __attribute__((aligned(16))) double lds[4 * kChunkSteps * kRow];
+
+  const int q = blockIdx.y;
+  const SpecInfo inf = a.info[q];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t block_lin = (int64_t)blockIdx.y * gridDim.x + blockIdx.x;
+  const int64_t s_base = (int64_t)blockIdx.x * kSamplesPerBlock + wave * kSamplesPerWave;
+
+  if (inf.J == 0) {  // unusable spectrum: NaN outputs (MATLAB would have errored)
+    const int64_t s = s_base + (lane & 15);
+    if (lane < 16 && s < a.S && a.sample_ll) a.sample_ll[q * a.ld + s] = NAN;
+    if (lane < 16 && s == a.S) a.ll_null[q] = NAN;
+    return;
+  }
+
+  // ---- per-lane sample constants (MFMA A-operand layout: sample = lane & 15, segment = lane >> 4)
+  const int g = lane >> 4;
+  const int64_t s = s_base + (lane & 15);
+  const bool active = s <= a.S;
+  const bool is_null = s == a.S;
+  const double off = (s < a.S) ? a.offsets[s] : 0.5;
+  const double N = (s < a.S) ? a.nhi[s] : 0.0;
+  const double zdla = inf.zmin + (inf.zmax - inf.zmin) * off;  // process_qsos.m:163-165
+  const double zfac = 1.0 / (1 + zdla);
+  const int L = inf.L;
+
+  // ---- sliding window: raw profile at padded positions gL + 0..5
+  const double* lamp = a.lam_pad + inf.lam_base + (int64_t)g * L;
+  double w0 = raw_profile(lamp[0], zfac, N, a.num_lines, a.line_tabs, a.line_mult);
+  double w1 = raw_profile(lamp[1], zfac, N, a.num_lines, a.line_tabs, a.line_mult);
+  double w2 = raw_profile(lamp[2], zfac, N, a.num_lines, a.line_tabs, a.line_mult);
+  double w3 = raw_profile(lamp[3], zfac, N, a.num_lines, a.line_tabs, a.line_mult);
+  double w4 = raw_profile(lamp[4], zfac, N, a.num_lines, a.line_tabs, a.line_mult);
+  double w5 = raw_profile(lamp[5], zfac, N, a.num_lines, a.line_tabs, a.line_mult);
+
+  double acc[kTiles];
+#pragma unroll
+  for (int t = 0; t < kTiles; ++t) acc[t] = 0.0;
+  double q1 = 0.0;       // sum r^2 / d
+  double pm = 1.0;       // prod d = pm * 2^pe
+  int pe = 0;
+
+  const int nchunks = (L + kChunkSteps - 1) / kChunkSteps;
+  const double* panel = a.panel + inf.slot_base * kRow;
+  for (int c = 0; c < nchunks; ++c) {
+    __syncthreads();
+    {  // stage 4 segments x kChunkSteps rows (double2 granules)
+      constexpr int kHalfRow = kRow / 2;
+      constexpr int kTotal = 4 * kChunkSteps * kHalfRow;
+      for (int idx = threadIdx.x; idx < kTotal; idx += 256) {
+        const int r = idx / kHalfRow, o = idx - r * kHalfRow;
+        const int tt = r >> 2, gg = r & 3;
+        const int64_t slot = (int64_t)gg * L + c * kChunkSteps + tt;
+        reinterpret_cast<double2*>(lds)[idx] = reinterpret_cast<const double2*>(panel + slot * kRow)[o];
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int tt = 0; tt < kChunkSteps; ++tt) {
+      const int t = c * kChunkSteps + tt;
+      const double* row = lds + (tt * 4 + g) * kRow;
+      const double lam = row[Lay::kLam];
+      const double y = row[Lay::kY];
+      const double noise = row[Lay::kNoise];
+      const double mu = row[Lay::kMu];
+      const double om2 = row[Lay::kOmega2];
+      const bool valid = row[Lay::kValid] != 0.0;
+      const double w6 = raw_profile(lam, zfac, N, a.num_lines, a.line_tabs, a.line_mult);
+      // instrumental broadening, voigt.c:297-299 (zero-initialised accumulator, taps in order)
+      double ab = 0.0;
+      ab += w0 * kInstrumentProfile[0];
+      ab += w1 * kInstrumentProfile[1];
+      ab += w2 * kInstrumentProfile[2];
+      ab += w3 * kInstrumentProfile[3];
+      ab += w4 * kInstrumentProfile[4];
+      ab += w5 * kInstrumentProfile[5];
+      ab += w6 * kInstrumentProfile[6];
+      w0 = w1; w1 = w2; w2 = w3; w3 = w4; w4 = w5; w5 = w6;
+      if (is_null) ab = 1.0;  // null model: no absorption (process_qsos.m:150-152)
+      // process_qsos.m:191-197 and log_mvnpdf_low_rank.m:11-15
+      const double r = y - mu * ab;
+      const double a2 = ab * ab;
+      const double d = om2 * a2 + noise;
+      const double dinv = rcp_nr(d);
+      const bool use = active && valid && (t < L);
+      const double wg = use ? a2 * dinv : 0.0;
+      const double wu = use ? ab * r * dinv : 0.0;
+      q1 += use ? r * r * dinv : 0.0;
+      pm *= use ? d : 1.0;
+      // B operands: tile t, entry 4t + (lane & 3) of this lane's segment row
+      const double* brow = row + (lane & 3) * kJS;
+#pragma unroll
+      for (int tp = 0; tp < kTiles; tp += 2) {
+        if (tp + 1 < kTiles) {
+          const double2 b = *reinterpret_cast<const double2*>(brow + tp);
+          acc[tp] = __builtin_amdgcn_mfma_f64_4x4x4f64(tp < kGT ? wg : wu, b.x, acc[tp], 0, 0, 0);
+          acc[tp + 1] = __builtin_amdgcn_mfma_f64_4x4x4f64(tp + 1 < kGT ? wg : wu, b.y, acc[tp + 1], 0, 0, 0);
+        } else {
+          acc[tp] = __builtin_amdgcn_mfma_f64_4x4x4f64(tp < kGT ? wg : wu, brow[tp], acc[tp], 0, 0, 0);
+        }
+      }
+    }
+    {  // keep the running product in range
+      int ex;
+      pm = frexp(pm, &ex);
+      pe += ex;
+    }
+  }
+
+  // ---- combine the 4 segments of each sample (lanes l, l^16, l^32, l^48)
+  q1 += __shfl_xor(q1, 16);
+  q1 += __shfl_xor(q1, 32);
+#pragma unroll
+  for (int off2 = 16; off2 <= 32; off2 <<= 1) {
+    const double pm2 = __shfl_xor(pm, off2);
+    const int pe2 = __shfl_xor(pe, off2);
+    int ex;
+    pm = frexp(pm * pm2, &ex);
+    pe += pe2 + ex;
+  }
+
+  // ---- epilogue 1: accumulators -> scratch (sample-major); D lane map of 4x4x4_4b:
+  //      sample 4*((lane>>2)&3) + (lane>>4), entry 4t + (lane&3)
+  double* scr = a.scratch + (block_lin * kSamplesPerBlock + wave * kSamplesPerWave) * Lay::kES;
+  {
+    const int sd = 4 * ((lane >> 2) & 3) + (lane >> 4);
+    double* dst = scr + sd * Lay::kES + (lane & 3);
+#pragma unroll
+    for (int t = 0; t < kTiles; ++t) dst[4 * t] = acc[t];
+    if (lane < 16) {
+      double* sc = scr + lane * Lay::kES + 4 * kTiles;
+      sc[0] = q1;
+      sc[1] = pm;
+      sc[2] = (double)pe;
+    }
+  }
+  __syncthreads();
+
+  // ---- epilogue 2: augmented LDL^T per sample, one quad of lanes per sample.
+  //      Lane jq owns Gram columns c = 4jj + jq (rows 0..4jj+3) and u rows i = 4m + jq.
+  constexpr int NJJ = (K + 3) / 4;
+  const int jq = lane & 3, sq = lane >> 2;
+  const double* srow = scr + sq * Lay::kES;
+  double A[NJJ][4 * NJJ];
+  double U[NJJ];
+#pragma unroll
+  for (int jj = 0; jj < NJJ; ++jj) {
+    const int c = 4 * jj + jq;
+#pragma unroll
+    for (int i = 0; i < 4 * jj + 4; ++i) {
+      double v = 0.0;
+      if (i <= c && c < K) {
+        v = srow[gram_index<K>(i, c)];
+        if (i == c) v += 1.0;  // B = I + M' D^-1 M (log_mvnpdf_low_rank.m:23)
+      }
+      A[jj][i] = v;
+    }
+    U[jj] = (c < K) ? srow[4 * kGT + c] : 0.0;
+  }
+  double quad = srow[4 * kTiles];
+  const double dm = srow[4 * kTiles + 1];
+  const double de = srow[4 * kTiles + 2];
+  double pb = 1.0;
+  int eb = 0;
+  bool bad = false;
+#pragma unroll
+  for (int p = 0; p < K; ++p) {
+    const double Dp = quad_bcast(A[p >> 2][p], p & 3);
+    bad |= !(Dp > 0.0) || !(Dp < INFINITY);
+    const double invD = 1.0 / Dp;
+    pb *= Dp;
+    if ((p & 3) == 3) {
+      int ex;
+      pb = frexp(pb, &ex);
+      eb += ex;
+    }
+    const double up = quad_bcast(U[p >> 2], p & 3);
+    const double upinv = up * invD;
+    double rowp[K];
+#pragma unroll
+    for (int i = p + 1; i < K; ++i) rowp[i] = quad_bcast(A[i >> 2][p], i & 3);
+#pragma unroll
+    for (int jj = p >> 2; jj < NJJ; ++jj) {
+      const double sc = A[jj][p] * invD;
+#pragma unroll
+      for (int i = p + 1; i < 4 * jj + 4 && i < K; ++i) A[jj][i] = fma(-rowp[i], sc, A[jj][i]);
+    }
+#pragma unroll
+    for (int mm = 0; mm < NJJ; ++mm) {
+      if (4 * mm + 3 > p) {
+        const bool cnd = (4 * mm + jq) > p;
+        U[mm] = cnd ? fma(-A[mm][p], upinv, U[mm]) : U[mm];
+      }
+    }
+    quad = fma(-up, upinv, quad);
+  }
+  const int64_t s2 = s_base + sq;
+  if (jq == 0 && s2 <= a.S) {
+    const double logdet_b = log(pb) + eb * kLn2;
+    const double logdet_d = log(dm) + de * kLn2;
+    double ll = -0.5 * (quad + (logdet_d + logdet_b) + inf.n * kLog2Pi);  // log_mvnpdf_low_rank.m:30-32
+    if (bad || !(fabs(ll) < INFINITY)) {
+      ll = NAN;
+      atomicOr(a.status, 1);
+    }
+    if (s2 == a.S) a.ll_null[q] = ll;
+    else if (a.sample_ll) a.sample_ll[q * a.ld + s2] = ll;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// log-mean-exp over samples, process_qsos.m:202-209
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void reduce_kernel(ReduceArgs a) {
+  __shared__ double s_d4[4];
+  const int q = blockIdx.x;
+  const double* ll = a.sample_ll + q * a.ld;
+  double mx = -INFINITY;
+  bool nan = false;
+  for (int64_t s = threadIdx.x; s < a.S; s += 256) {
+    const double v = ll[s];
+    nan |= (v != v);
+    mx = fmax(mx, v);
+  }
+  mx = block_reduce_max(mx, s_d4);
+  double sum = 0.0;
+  for (int64_t s = threadIdx.x; s < a.S; s += 256) sum += exp(ll[s] - mx);
+  sum = block_reduce_sum(sum, s_d4);
+  const double anynan = block_reduce_max(nan ? 1.0 : 0.0, s_d4);
+  if (threadIdx.x == 0) {
+    const SpecInfo inf = a.info[q];
+    double r = mx + log(sum / (double)a.S);
+    if (anynan > 0 || inf.J == 0) r = NAN;
+    a.ll_dla[q] = r;
+    if (a.zmin) a.zmin[q] = inf.zmin;
+    if (a.zmax) a.zmax[q] = inf.zmax;
+    if (a.num_pixels) a.num_pixels[q] = inf.n;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// standalone voigt (MEX replacement): one block per (z, N); raw profile staged in LDS
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void voigt_batch_kernel(const double* __restrict__ lambdas,
+                                                          int64_t n_padded,
+                                                          const double* __restrict__ zs,
+                                                          const double* __restrict__ Ns,
+                                                          int32_t num_lines,
+                                                          const double* __restrict__ line_tabs,
+                                                          const double* __restrict__ line_mult,
+                                                          double* __restrict__ out) {
+  __shared__ double raw[256 + 2 * kWidth];
+  const int64_t sidx = blockIdx.x;
+  const double zfac = 1.0 / (1 + zs[sidx]);
+  const double N = Ns[sidx];
+  const int64_t n_out = n_padded - 2 * kWidth;
+  double* o = out + sidx * n_out;
+  for (int64_t base = 0; base < n_out; base += 256) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < 256 + 2 * kWidth; i += 256) {
+      const int64_t p = base + i;
+      raw[i] = (p < n_padded) ? raw_profile(lambdas[p], zfac, N, num_lines, line_tabs, line_mult) : 0.0;
+    }
+    __syncthreads();
+    const int64_t i = base + threadIdx.x;
+    if (i < n_out) {
+      double acc = 0.0;
+#pragma unroll
+      for (int k = 0; k <= 2 * kWidth; ++k) acc += raw[threadIdx.x + k] * kInstrumentProfile[k];
+      o[i] = acc;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// standalone log_mvnpdf_low_rank: one block; Gram + u + scalars by block reduction, then a
+// Cholesky by one lane (not the hot path: the engine fuses this into likelihood_kernel)
+// ---------------------------------------------------------------------------------------------
+constexpr int kMvnMaxK = 64;
+__global__ __launch_bounds__(256) void mvn_single_kernel(const double* __restrict__ y,
+                                                         const double* __restrict__ mu,
+                                                         const double* __restrict__ M,
+                                                         const double* __restrict__ d, int64_t n,
+                                                         int32_t k, double* out, int32_t* status) {
+  __shared__ double B[kMvnMaxK * kMvnMaxK];
+  __shared__ double u[kMvnMaxK];
+  __shared__ double s_d4[4];
+  const int nent = k * (k + 1) / 2;
+  for (int e = threadIdx.x; e < nent + k; e += 256) {
+    double acc = 0.0;
+    if (e < nent) {
+      int r = 0, start = 0;
+      while (e >= start + (k - r)) { start += k - r; ++r; }
+      const int c = r + (e - start);
+      for (int64_t i = 0; i < n; ++i) acc += M[i + r * n] * (M[i + c * n] / d[i]);
+      B[r * k + c] = acc + (r == c ? 1.0 : 0.0);
+      B[c * k + r] = B[r * k + c];
+    } else {
+      const int r = e - nent;
+      for (int64_t i = 0; i < n; ++i) acc += M[i + r * n] * ((y[i] - mu[i]) / d[i]);
+      u[r] = acc;
+    }
+  }
+  double q1 = 0.0, ld = 0.0;
+  for (int64_t i = threadIdx.x; i < n; i += 256) {
+    const double r = y[i] - mu[i];
+    q1 += r * (r / d[i]);
+    ld += log(d[i]);
+  }
+  q1 = block_reduce_sum(q1, s_d4);
+  ld = block_reduce_sum(ld, s_d4);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    // upper Cholesky R'R = B in place (row-major upper triangle)
+    bool bad = false;
+    double logdet = 0.0;
+    for (int p = 0; p < k; ++p) {
+      double v = B[p * k + p];
+      for (int t = 0; t < p; ++t) v -= B[t * k + p] * B[t * k + p];
+      if (!(v > 0.0)) bad = true;
+      const double rpp = sqrt(v);
+      B[p * k + p] = rpp;
+      logdet += log(rpp);
+      for (int c = p + 1; c < k; ++c) {
+        double w = B[p * k + c];
+        for (int t = 0; t < p; ++t) w -= B[t * k + p] * B[t * k + c];
+        B[p * k + c] = w / rpp;
+      }
+    }
+    // t = R^-T u, quad = q1 - t't
+    double tt = 0.0;
+    for (int p = 0; p < k; ++p) {
+      double v = u[p];
+      for (int t = 0; t < p; ++t) v -= B[t * k + p] * u[t];
+      u[p] = v / B[p * k + p];
+      tt += u[p] * u[p];
+    }
+    double r = -0.5 * ((q1 - tt) + (ld + 2 * logdet) + n * kLog2Pi);
+    if (bad || !(fabs(r) < INFINITY)) {
+      r = NAN;
+      *status = 1;
+    }
+    *out = r;
+  }
+}
+
+template <int K>
+hipError_t launch_prep_k(const PrepArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(prep_kernel<K>, dim3(a.q_count), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+template <int K>
+hipError_t launch_likelihood_k(const LikelihoodArgs& a, hipStream_t s) {
+  const int64_t blocks_x = (a.S + 1 + kSamplesPerBlock - 1) / kSamplesPerBlock;
+  hipLaunchKernelGGL(likelihood_kernel<K>, dim3((unsigned)blocks_x, a.q_count), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+#define GPDLA_FOR_EACH_RANK(X) X(4) X(8) X(10) X(12) X(16) X(20) X(24)
+
+bool rank_supported(int K) {
+#define X(k) if (K == k) return true;
+  GPDLA_FOR_EACH_RANK(X)
+#undef X
+  return false;
+}
+
+int panel_row_doubles(int K) {
+#define X(k) if (K == k) return Layout<k>::kRow;
+  GPDLA_FOR_EACH_RANK(X)
+#undef X
+  return 0;
+}
+
+int scratch_doubles(int K) {
+#define X(k) if (K == k) return Layout<k>::kES;
+  GPDLA_FOR_EACH_RANK(X)
+#undef X
+  return 0;
+}
+
+hipError_t launch_prep(int K, const PrepArgs& a, hipStream_t s) {
+#define X(k) if (K == k) return launch_prep_k<k>(a, s);
+  GPDLA_FOR_EACH_RANK(X)
+#undef X
+  return hipErrorInvalidValue;
+}
+
+hipError_t launch_likelihood(int K, const LikelihoodArgs& a, hipStream_t s) {
+#define X(k) if (K == k) return launch_likelihood_k<k>(a, s);
+  GPDLA_FOR_EACH_RANK(X)
+#undef X
+  return hipErrorInvalidValue;
+}
+
+hipError_t launch_reduce(const ReduceArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(reduce_kernel, dim3(a.q_count), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_voigt_batch(const double* lambdas, int64_t n_padded, const double* z,
+                              const double* N, int64_t count, int32_t num_lines,
+                              const double* line_tabs_and_mult, double* out, hipStream_t s) {
+  const double* tabs = line_tabs_and_mult;
+  const double* mult = line_tabs_and_mult + (int64_t)kMaxLines * kLineTableStride;
+  hipLaunchKernelGGL(voigt_batch_kernel, dim3((unsigned)count), dim3(256), 0, s, lambdas,
+                     n_padded, z, N, num_lines, tabs, mult, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_mvn_single(const double* y, const double* mu, const double* M_colmajor,
+                             const double* d, int64_t n, int32_t k, double* out, int32_t* status,
+                             hipStream_t s) {
+  if (k > kMvnMaxK) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(mvn_single_kernel, dim3(1), dim3(256), 0, s, y, mu, M_colmajor, d, n, k,
+                     out, status);
+  return hipGetLastError();
+}
+
+}  // namespace gpdla

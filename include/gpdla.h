@@ -1,0 +1,161 @@
+/* gpdla.h -- C ABI of the MI355X GP-DLA likelihood engine (libgpdla.so).
+ *
+ * Drop-in boundary for the hot path of sbird/gp_dla_detection (paths are relative to the
+ * reference repository):
+ *
+ *   reference interface                                  replaced by
+ *   ---------------------------------------------------  -------------------------------------
+ *   voigt MEX: absorption = voigt(lambdas, z, N, nl)     gpdla_voigt_f64
+ *     (voigt.c:253-304, called at process_qsos.m:186)
+ *   log_p = log_mvnpdf_low_rank(y, mu, M, d)             gpdla_log_mvnpdf_low_rank_f64
+ *     (log_mvnpdf_low_rank.m:5-33, process_qsos.m:151,196)
+ *   process_qsos.m:88-220 per-spectrum loop + parfor    gpdla_engine_create / _process /
+ *     over DLA samples (process_qsos.m:184-198)            _synchronize / _destroy
+ *
+ * Conventions
+ *   - Plain pointers and sizes only.  The caller owns every buffer; the engine owns only its
+ *     device workspaces.  Nothing allocated by the library is returned across the ABI.
+ *   - Matrices follow MATLAB: M is (rows x k) COLUMN-major.
+ *   - Every function returns an int status: GPDLA_OK (0), a negative error, or GPDLA_ENUMERIC
+ *     (a non-positive Cholesky/LDL pivot or a non-finite value was met; the affected outputs
+ *     are NaN -- MATLAB's chol would have raised, log_mvnpdf_low_rank.m:24).
+ *     A message is available from gpdla_last_error() (thread-local).
+ *   - Reentrant.  One engine is driven by one host thread; engines on different devices (or
+ *     the same device) may run concurrently.
+ *   - There is no CPU fallback: without a usable HIP device every compute entry point fails
+ *     with GPDLA_EDEVICE.
+ */
+#ifndef GPDLA_H
+#define GPDLA_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GPDLA_OK 0
+#define GPDLA_ENUMERIC 1
+#define GPDLA_EINVAL (-1)
+#define GPDLA_EDEVICE (-2)
+#define GPDLA_ENOMEM (-3)
+#define GPDLA_EUNSUPPORTED (-4)
+
+#define GPDLA_MEM_HOST 0
+#define GPDLA_MEM_DEVICE 1
+
+/* absorption-index handling (process_qsos.m:180,189) */
+#define GPDLA_ABSORPTION_REFERENCE 0 /* reproduce the quirk: absorption(1:n) of the m in-range values */
+#define GPDLA_ABSORPTION_UNMASKED 1  /* pair every unmasked pixel with its own profile value */
+
+/* Learned null model (learned_qso_model_<set>.mat, read at process_qsos.m:30-35).  Host memory. */
+typedef struct gpdla_model {
+  int32_t num_rest;              /* rest-grid size (1,217 for 911.75:0.25:1215.75) */
+  int32_t k;                     /* rank (set_parameters.m:36) */
+  const double* rest_wavelengths;/* [num_rest], strictly increasing */
+  const double* mu;              /* [num_rest] */
+  const double* M;               /* [num_rest x k], column-major */
+  const double* log_omega;       /* [num_rest] */
+  double log_c_0, log_tau_0, log_beta;
+} gpdla_model;
+
+/* DLA parameter samples (dla_samples.mat, read at process_qsos.m:38-40).  Host memory. */
+typedef struct gpdla_samples {
+  int64_t num_samples;           /* S (set_parameters.m:48) */
+  const double* offset_samples;  /* [S] in [0,1] */
+  const double* nhi_samples;     /* [S] N_HI in cm^-2 (10.^log_nhi_samples) */
+} gpdla_samples;
+
+/* set_parameters.m knobs the path reads. */
+typedef struct gpdla_params {
+  int32_t num_lines;             /* 1..31 (set_parameters.m:63; voigt.c:16) */
+  int32_t width;                 /* must be 3 (set_parameters.m:59 == voigt.c:229) */
+  double pixel_spacing;          /* 1e-4 dex (set_parameters.m:60) */
+  double min_lambda, max_lambda; /* 911.75, 1215.75 (set_parameters.m:33-34) */
+  double lya_wavelength;         /* 1215.6701 (set_parameters.m:5) */
+  double lyman_limit;            /* 911.7633 (set_parameters.m:7) */
+  double min_z_cut, max_z_cut;   /* kms_to_z(3000) (set_parameters.m:65,69) */
+  int32_t absorption_mode;       /* GPDLA_ABSORPTION_* */
+  int32_t max_batch_spectra;     /* spectra per device batch; 0 = library default */
+} gpdla_params;
+
+/* Preloaded spectra (preloaded_qsos.mat cells, process_qsos.m:46-61), CSR-packed.
+ * `offsets` is ALWAYS host memory; the pixel arrays and z_qsos live in `memory`. */
+typedef struct gpdla_spectra {
+  int32_t memory;                /* GPDLA_MEM_HOST or GPDLA_MEM_DEVICE */
+  int64_t num_spectra;           /* Q */
+  const int64_t* offsets;        /* [Q+1] host; spectrum q = pixels offsets[q]..offsets[q+1]-1 */
+  const double* wavelengths;     /* observed, Angstrom */
+  const double* flux;
+  const double* noise_variance;
+  const uint8_t* pixel_mask;     /* nonzero = masked */
+  const double* z_qsos;          /* [Q] */
+} gpdla_spectra;
+
+/* Per-spectrum outputs (the hot-path subset of processed_qsos_<set>.mat, process_qsos.m:235-249). */
+typedef struct gpdla_results {
+  int32_t memory;                      /* GPDLA_MEM_HOST or GPDLA_MEM_DEVICE */
+  double* log_likelihoods_no_dla;      /* [Q]   process_qsos.m:150-152 */
+  double* sample_log_likelihoods_dla;  /* [Q x sample_ld] spectrum-major, or NULL (process_qsos.m:195) */
+  int64_t sample_ld;                   /* >= S */
+  double* log_likelihoods_dla;         /* [Q]   process_qsos.m:202-209 */
+  double* min_z_dlas;                  /* [Q]   process_qsos.m:160 (may be NULL) */
+  double* max_z_dlas;                  /* [Q]   process_qsos.m:161 (may be NULL) */
+  int32_t* num_pixels;                 /* [Q]   n, unmasked in-range pixels (may be NULL) */
+} gpdla_results;
+
+/* Kernel-time accounting (HIP events on the engine's stream), cumulative since create/reset. */
+typedef struct gpdla_stats {
+  double prep_ms, likelihood_ms, reduce_ms;
+  int64_t prep_launches, likelihood_launches, reduce_launches;
+  int64_t spectra, sample_evals;       /* sample_evals = sum over spectra of S (null evals excluded) */
+} gpdla_stats;
+
+typedef struct gpdla_engine gpdla_engine;
+
+int gpdla_engine_create(int32_t device, const gpdla_model* model, const gpdla_samples* samples,
+                        const gpdla_params* params, gpdla_engine** out);
+/* Enqueue the whole pipeline for all spectra.  With GPDLA_MEM_HOST results the call blocks until
+ * the outputs are copied back; with device results it returns after enqueueing (use
+ * gpdla_engine_synchronize).  Spectra may be processed in several device batches. */
+int gpdla_engine_process(gpdla_engine* engine, const gpdla_spectra* spectra,
+                         const gpdla_results* results);
+/* Wait for enqueued work; returns GPDLA_ENUMERIC if any pivot was non-positive since the last call. */
+int gpdla_engine_synchronize(gpdla_engine* engine);
+/* Use an external hipStream_t (NULL restores the engine's own stream). */
+int gpdla_engine_set_stream(gpdla_engine* engine, void* hip_stream);
+int gpdla_engine_get_stats(gpdla_engine* engine, gpdla_stats* stats);
+int gpdla_engine_reset_stats(gpdla_engine* engine);
+void gpdla_engine_destroy(gpdla_engine* engine);
+
+/* voigt MEX replacement (voigt.c:253-304).  Host buffers.  out has n_padded - 6 values. */
+int gpdla_voigt_f64(const double* lambdas, int64_t n_padded, double z, double N,
+                    int32_t num_lines, double* out);
+/* Batched form: out[s*(n_padded-6) + i] for `count` (z, N) pairs over one padded grid. */
+int gpdla_voigt_batch_f64(const double* lambdas, int64_t n_padded, const double* z,
+                          const double* N, int64_t count, int32_t num_lines, double* out);
+/* log N(y; mu, M M' + diag(d)) (log_mvnpdf_low_rank.m:5-33).  Host buffers, M n x k column-major. */
+int gpdla_log_mvnpdf_low_rank_f64(const double* y, const double* mu, const double* M,
+                                  const double* d, int64_t n, int32_t k, double* out);
+
+/* Diagnostics (test support; not used by the compute path).
+ * Re/Im of the Faddeeva function the line tables are fitted from (host, long double). */
+int gpdla_diag_faddeeva_w(double x, double y, double* re, double* im);
+/* Max relative error of the fitted profile table of `line` against its long-double source. */
+int gpdla_diag_line_table_error(int32_t line, double* max_rel_err);
+
+/* Device buffers for callers without a GPU array library (the benchmark, tests, C callers).
+ * Callers that already hold device memory (e.g. PyTorch tensors) pass those pointers instead. */
+int gpdla_device_malloc(int32_t device, int64_t bytes, void** ptr);
+int gpdla_device_free(int32_t device, void* ptr);
+int gpdla_memcpy_htod(int32_t device, void* dst, const void* src, int64_t bytes);
+int gpdla_memcpy_dtoh(int32_t device, void* dst, const void* src, int64_t bytes);
+
+const char* gpdla_last_error(void);
+int32_t gpdla_version(void);
+int32_t gpdla_device_count(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GPDLA_H */

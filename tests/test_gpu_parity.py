@@ -1,0 +1,254 @@
+"""GPU parity: the HIP path (through the C ABI) against the oracle's committed golden fixtures,
+plus size-independent properties at the BASELINE configuration sizes.
+
+Tolerance (north star, BASELINE.json): per-spectrum log evidences within 1e-6 relative, written
+as |got - ref| <= 1e-6 * max(|ref|, 1).  The measured agreement is ~1e-10 or better; the tests
+also assert a tighter 1e-9 bar so a precision regression is caught long before the contract."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+from conftest import tol_ok  # noqa: E402
+from gp_dla_detection_amd import _lib as L  # noqa: E402
+from gp_dla_detection_amd import synthetic as syn  # noqa: E402
+from gp_dla_detection_amd.engine import Engine, log_mvnpdf_low_rank, voigt, voigt_batch  # noqa: E402
+from gp_dla_detection_amd.parameters import set_parameters  # noqa: E402
+
+
+@pytest.fixture(scope="module", autouse=True)
+def require_device():
+    lib = L.load()
+    assert lib.gpdla_device_count() > 0, "no HIP device: GPU tests must run on the MI355X box"
+
+
+@pytest.fixture(scope="module")
+def golden(golden_dir):
+    g = np.load(golden_dir / "process.npz")
+    model = {k: g[k] for k in ("rest_wavelengths", "mu", "M", "log_omega", "log_c_0", "log_tau_0", "log_beta")}
+    samples = dict(offset_samples=g["offset_samples"], nhi_samples=g["nhi_samples"])
+    packed = {k: g[k] for k in ("offsets", "wavelengths", "flux", "noise_variance", "pixel_mask", "z_qsos")}
+    return g, model, samples, packed
+
+
+def _rel_err(got, ref):
+    got, ref = np.asarray(got, float), np.asarray(ref, float)
+    return np.max(np.abs(got - ref) / np.maximum(np.abs(ref), 1.0))
+
+
+# ------------------------------------------------------------------------------ voigt MEX
+def test_voigt_matches_golden(golden_dir):
+    g = np.load(golden_dir / "voigt.npz")
+    for i in range(g["z"].size):
+        ref = g[f"out_{i}"]
+        got = voigt(g[f"lam_{i}"], g["z"][i], g["N"][i], int(g["num_lines"][i]))
+        assert got.shape == ref.shape
+        # absorption in [0,1]; absolute agreement + relative where the value is not underflowed
+        assert np.max(np.abs(got - ref)) < 1e-12
+        big = ref > 1e-200
+        assert np.max(np.abs(got[big] - ref[big]) / ref[big]) < 1e-9
+
+
+def test_voigt_batch_equals_single(golden_dir):
+    g = np.load(golden_dir / "voigt.npz")
+    lam = g["lam_0"]
+    zs, Ns = g["z"][:4], g["N"][:4]
+    batch = voigt_batch(lam, zs, Ns, 3)
+    for i in range(4):
+        np.testing.assert_array_equal(batch[i], voigt(lam, zs[i], Ns[i], 3))
+
+
+# ------------------------------------------------------------------------ log_mvnpdf
+def test_log_mvnpdf_matches_golden(golden_dir):
+    g = np.load(golden_dir / "mvn.npz")
+    for i in range(4):
+        got = log_mvnpdf_low_rank(g[f"y_{i}"], g[f"mu_{i}"], g[f"M_{i}"], g[f"d_{i}"])
+        ref = float(g[f"out_{i}"])
+        assert abs(got - ref) <= 1e-10 * max(1, abs(ref))
+
+
+def test_log_mvnpdf_non_pd_raises():
+    with pytest.raises(L.GpdlaNumericError):
+        log_mvnpdf_low_rank(np.ones(4), np.zeros(4), np.ones((4, 2)), -np.ones(4) * 10)
+
+
+# ------------------------------------------------------------------------ engine
+@pytest.mark.parametrize("mode", ["reference", "unmasked"])
+def test_engine_matches_golden(golden, mode):
+    g, model, samples, packed = golden
+    params = set_parameters(k=20, absorption_mode=mode)
+    with Engine(model, samples, params) as eng:
+        out = eng.process(packed)
+    pre = f"{mode}_"
+    for key, gkey in (("log_likelihoods_no_dla", "log_likelihood_no_dla"),
+                      ("sample_log_likelihoods_dla", "sample_log_likelihoods_dla"),
+                      ("log_likelihoods_dla", "log_likelihood_dla")):
+        ref = g[pre + gkey]
+        assert np.all(tol_ok(out[key], ref)), (key, _rel_err(out[key], ref))
+        assert _rel_err(out[key], ref) < 1e-9, (key, _rel_err(out[key], ref))
+    np.testing.assert_allclose(out["min_z_dlas"], g[pre + "min_z_dla"], rtol=1e-14)
+    np.testing.assert_allclose(out["max_z_dlas"], g[pre + "max_z_dla"], rtol=1e-14)
+    np.testing.assert_array_equal(out["num_pixels"], g[pre + "n"])
+
+
+def test_engine_batching_and_sharding_bitwise(golden):
+    g, model, samples, packed = golden
+    params = set_parameters(k=20)
+    with Engine(model, samples, params) as eng:
+        full = eng.process(packed)
+    with Engine(model, samples, params, max_batch_spectra=3) as eng:
+        batched = eng.process(packed)
+        # shard: spectra 0..3 and 4..7 processed separately
+        parts = []
+        for lo, hi in ((0, 4), (4, 8)):
+            sub = syn.pack_spectra([_unpack(packed, q) for q in range(lo, hi)])
+            parts.append(eng.process(sub))
+    for key in ("log_likelihoods_no_dla", "sample_log_likelihoods_dla", "log_likelihoods_dla"):
+        np.testing.assert_array_equal(batched[key], full[key])
+        np.testing.assert_array_equal(np.concatenate([p[key] for p in parts]), full[key])
+
+
+def _unpack(packed, q):
+    a, b = packed["offsets"][q], packed["offsets"][q + 1]
+    return dict(wavelengths=packed["wavelengths"][a:b], flux=packed["flux"][a:b],
+                noise_variance=packed["noise_variance"][a:b], pixel_mask=packed["pixel_mask"][a:b],
+                z_qso=packed["z_qsos"][q])
+
+
+def test_edge_cases_small_and_empty():
+    """Tiny spectra (J not a multiple of 4, n < 4), an unusable spectrum (no in-range pixel),
+    S not a multiple of the 64-sample block, and one / 31 Lyman lines."""
+    from oracle import gpdla_oracle as O
+    model = syn.make_model(k=8, seed=3)
+    samples = syn.make_samples(67)
+    base = syn.make_spectrum(model, 0, z_qso=2.8, n_target=None, mask_fraction=0.1)
+    spectra = []
+    for npx in (1, 2, 3, 5, 9, 33):
+        s = dict(base)
+        sl = slice(100, 100 + npx)
+        spectra.append({k: (v[sl] if isinstance(v, np.ndarray) else v) for k, v in s.items()})
+        spectra[-1]["pixel_mask"] = np.zeros(npx, dtype=bool)
+    empty = dict(base)
+    empty["z_qso"] = 9.5  # nothing in range
+    spectra.append(empty)
+    packed = syn.pack_spectra(spectra)
+    for nl in (1, 31):
+        params = set_parameters(k=8, num_lines=nl)
+        with Engine(model, samples, params) as eng:
+            out = eng.process(packed)
+        for q, s in enumerate(spectra[:-1]):
+            ref = O.process_spectrum(s["wavelengths"], s["flux"], s["noise_variance"], s["pixel_mask"],
+                                     s["z_qso"], model, samples["offset_samples"], samples["nhi_samples"],
+                                     num_lines=nl)
+            assert _rel_err(out["sample_log_likelihoods_dla"][q], ref["sample_log_likelihoods_dla"]) < 1e-9
+            assert _rel_err(out["log_likelihoods_no_dla"][q], ref["log_likelihood_no_dla"]) < 1e-9
+            assert _rel_err(out["log_likelihoods_dla"][q], ref["log_likelihood_dla"]) < 1e-9
+        assert np.isnan(out["log_likelihoods_dla"][-1]) and np.isnan(out["log_likelihoods_no_dla"][-1])
+        assert np.all(np.isnan(out["sample_log_likelihoods_dla"][-1]))
+
+
+@pytest.mark.parametrize("k", [4, 10, 16, 24])
+def test_other_ranks(k):
+    from oracle import gpdla_oracle as O
+    model = syn.make_model(k=k, seed=k)
+    samples = syn.make_samples(40)
+    spectra = syn.make_dr12q_like_spectra(model, 2, seed=k, mask_fraction=0.05)
+    with Engine(model, samples, set_parameters(k=k)) as eng:
+        out = eng.process(syn.pack_spectra(spectra))
+    for q, s in enumerate(spectra):
+        ref = O.process_spectrum(s["wavelengths"], s["flux"], s["noise_variance"], s["pixel_mask"],
+                                 s["z_qso"], model, samples["offset_samples"], samples["nhi_samples"])
+        assert _rel_err(out["sample_log_likelihoods_dla"][q], ref["sample_log_likelihoods_dla"]) < 1e-9
+        assert _rel_err(out["log_likelihoods_no_dla"][q], ref["log_likelihood_no_dla"]) < 1e-9
+
+
+# ------------------------------------------------------------------ full-size properties
+def test_full_size_config_properties():
+    """BASELINE configs[1] shape (n = 800, k = 20, S = 10^4): oracle spot checks on a sample subset,
+    the calc_cddf.py:246 normalisation invariant, determinism and host/device-path equality."""
+    from oracle import gpdla_oracle as O
+    model = syn.make_model(k=20)
+    samples = syn.make_samples(10000)
+    spectra = syn.make_spectra(model, 3)
+    packed = syn.pack_spectra(spectra)
+    with Engine(model, samples, set_parameters(k=20)) as eng:
+        out1 = eng.process(packed)
+        out2 = eng.process(packed)
+    for key in ("log_likelihoods_no_dla", "sample_log_likelihoods_dla", "log_likelihoods_dla"):
+        np.testing.assert_array_equal(out1[key], out2[key])
+    assert np.all(out1["num_pixels"] == 800)
+    sll, lld = out1["sample_log_likelihoods_dla"], out1["log_likelihoods_dla"]
+    tot = np.exp(sll - (lld[:, None] + np.log(sll.shape[1]))).sum(axis=1)
+    np.testing.assert_allclose(tot, 1.0, atol=1e-12)
+    rng = np.random.default_rng(0)
+    idx = np.sort(rng.choice(10000, 24, replace=False))
+    idx[:2] = [0, 9999]
+    s = spectra[0]
+    prep = O.prepare_spectrum(s["wavelengths"], s["flux"], s["noise_variance"], s["pixel_mask"], s["z_qso"], model)
+    zs = prep["zmin"] + (prep["zmax"] - prep["zmin"]) * samples["offset_samples"][idx]
+    ref = np.array([O.sample_log_likelihood(prep, z, N, 3) for z, N in zip(zs, samples["nhi_samples"][idx])])
+    assert _rel_err(sll[0, idx], ref) < 1e-9
+    assert _rel_err(out1["log_likelihoods_no_dla"][0], O.null_log_likelihood(prep)) < 1e-9
+
+
+def test_device_path_equals_host_path():
+    model = syn.make_model(k=20)
+    samples = syn.make_samples(1000)
+    packed = syn.pack_spectra(syn.make_spectra(model, 4))
+    D = L.DeviceArray.from_numpy
+    t = {k: D(packed[k]) for k in ("wavelengths", "flux", "noise_variance", "pixel_mask", "z_qsos")}
+    Q = packed["z_qsos"].size
+    o_null, o_dla = L.DeviceArray(0, Q, np.float64), L.DeviceArray(0, Q, np.float64)
+    o_s = L.DeviceArray(0, (Q, 1000), np.float64)
+    with Engine(model, samples, set_parameters(k=20)) as eng:
+        host = eng.process(packed)
+        eng.process_device(packed["offsets"], t["wavelengths"].ptr, t["flux"].ptr, t["noise_variance"].ptr,
+                           t["pixel_mask"].ptr, t["z_qsos"].ptr, o_null.ptr, o_dla.ptr, o_s.ptr, 1000)
+        eng.synchronize()
+        st = eng.stats()
+    np.testing.assert_array_equal(o_null.numpy(), host["log_likelihoods_no_dla"])
+    np.testing.assert_array_equal(o_dla.numpy(), host["log_likelihoods_dla"])
+    np.testing.assert_array_equal(o_s.numpy(), host["sample_log_likelihoods_dla"])
+    assert st["likelihood_launches"] == 2 and st["likelihood_ms"] > 0
+
+
+TORCH_INTEROP = r"""
+import sys, numpy as np
+sys.path.insert(0, sys.argv[1])
+import torch                                   # first: its HIP runtime is the one libgpdla binds to
+from gp_dla_detection_amd import synthetic as syn, _lib as L
+from gp_dla_detection_amd.engine import Engine
+from gp_dla_detection_amd.parameters import set_parameters
+maps = open('/proc/self/maps').read()
+dev = torch.device('cuda:0')
+model = syn.make_model(k=20); samples = syn.make_samples(200)
+packed = syn.pack_spectra(syn.make_spectra(model, 3))
+t = {k: torch.from_numpy(np.ascontiguousarray(packed[k])).to(dev)
+     for k in ('wavelengths', 'flux', 'noise_variance', 'pixel_mask', 'z_qsos')}
+o_null = torch.empty(3, dtype=torch.float64, device=dev); o_dla = torch.empty_like(o_null)
+o_s = torch.empty((3, 200), dtype=torch.float64, device=dev)
+with Engine(model, samples, set_parameters(k=20)) as eng:
+    host = eng.process(packed)
+    eng.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    eng.process_device(packed['offsets'], t['wavelengths'].data_ptr(), t['flux'].data_ptr(),
+                       t['noise_variance'].data_ptr(), t['pixel_mask'].data_ptr(), t['z_qsos'].data_ptr(),
+                       o_null.data_ptr(), o_dla.data_ptr(), o_s.data_ptr(), 200)
+    eng.synchronize()
+assert np.array_equal(o_s.cpu().numpy(), host['sample_log_likelihoods_dla'])
+assert np.array_equal(o_dla.cpu().numpy(), host['log_likelihoods_dla'])
+libs = {l.split()[-1] for l in open('/proc/self/maps') if 'libamdhip64' in l}
+assert len(libs) == 1, libs
+print('torch interop ok', libs)
+"""
+
+
+def test_torch_tensor_interop():
+    """PyTorch tensors as engine buffers: torch imported first so the process holds ONE HIP runtime
+    (torch ships its own libamdhip64 with the same SONAME)."""
+    import subprocess
+    import sys
+    from pathlib import Path
+    root = str(Path(__file__).resolve().parents[1])
+    r = subprocess.run([sys.executable, "-c", TORCH_INTEROP, root], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "torch interop ok" in r.stdout
