@@ -39,22 +39,41 @@ int set_error(int code, const char* fmt, ...) {
                        __LINE__);                                                           \
   } while (0)
 
-// ---- line-profile tables (fitted once per process on the host) + per-line x factors
-// layout: [kMaxLines][kLineTableStride] tables, then [kMaxLines] factors
-//   factor_j = c / (lambda_j 1e8) / (sigma sqrt 2)  so that  x_j = lambda * factor_j / (1+z) - c/(sigma sqrt 2)
-const std::vector<double>& host_line_data() {
-  static std::vector<double> data;
+// ---- line-profile data (fitted once per process on the host; layout in internal.h)
+struct HostLineData {
+  std::vector<double> buf;
+  WingPoly wing;
+};
+
+const HostLineData& host_line_data() {
+  static HostLineData d;
   static std::once_flag once;
   std::call_once(once, [] {
-    data.assign((size_t)kMaxLines * kLineTableStride + kMaxLines, 0.0);
-    for (int j = 0; j < kMaxLines; ++j) fit_line_table(j, data.data() + (size_t)j * kLineTableStride);
+    d.buf.assign(kLineBufDoubles, 0.0);
+    for (int j = 0; j < kMaxLines; ++j) fit_core_table(j, d.buf.data() + (size_t)j * kCoreTable);
     for (int j = 0; j < kMaxLines; ++j) {
+      // fac_j = c / (lambda_j 1e8) / (sigma sqrt 2): x_j = lambda fac_j / (1+z) - c / (sigma sqrt 2)
       const long double f = (long double)kCcgs / ((long double)kTransitionWavelengths[j] * 1e8L) /
                             ((long double)kSigma * std::sqrt(2.0L));
-      data[(size_t)kMaxLines * kLineTableStride + j] = (double)f;
+      d.buf[kLineBufFac + j] = (double)f;
+      line_wing_constants(j, &d.buf[kLineBufA + j], &d.buf[kLineBufB + j]);
     }
+    fit_wing(&d.wing);
   });
-  return data;
+  return d;
+}
+
+LineArgs make_line_args(const double* d_buf) {
+  const HostLineData& h = host_line_data();
+  LineArgs l{};
+  l.buf = d_buf;
+  l.wing = h.wing;
+  for (int j = 0; j < 3; ++j) {
+    l.fac3[j] = h.buf[kLineBufFac + j];
+    l.A3[j] = h.buf[kLineBufA + j];
+    l.B3[j] = h.buf[kLineBufB + j];
+  }
+  return l;
 }
 
 int check_device(int32_t device) {
@@ -82,7 +101,7 @@ int grow(T** p, size_t* cap, size_t count) {
 
 struct TimedLaunch {
   hipEvent_t start, stop;
-  int kind;  // 0 prep, 1 likelihood, 2 reduce
+  int kind;  // 0 prep, 1 likelihood, 2 reduce, 3 solve
 };
 
 }  // namespace
@@ -146,6 +165,7 @@ int resolve_events(gpdla_engine* e) {
     if (t.kind == 0) { e->stats.prep_ms += ms; e->stats.prep_launches++; }
     if (t.kind == 1) { e->stats.likelihood_ms += ms; e->stats.likelihood_launches++; }
     if (t.kind == 2) { e->stats.reduce_ms += ms; e->stats.reduce_launches++; }
+    if (t.kind == 3) { e->stats.solve_ms += ms; e->stats.solve_launches++; }
     (void)hipEventDestroy(t.start);
     (void)hipEventDestroy(t.stop);
   }
@@ -190,8 +210,7 @@ int gpdla_diag_faddeeva_w(double x, double y, double* re, double* im);  // fadde
 
 int gpdla_diag_line_table_error(int32_t line, double* max_rel_err) {
   if (line < 0 || line >= kMaxLines || !max_rel_err) return set_error(GPDLA_EINVAL, "bad line");
-  std::vector<double> tab(kLineTableStride);
-  *max_rel_err = fit_line_table(line, tab.data());
+  *max_rel_err = line_profile_error(line);
   return GPDLA_OK;
 }
 
@@ -258,7 +277,7 @@ int gpdla_engine_create(int32_t device, const gpdla_model* model, const gpdla_sa
   TRY_E(grow(&e->d_logom, &dummy, G)); dummy = 0;
   TRY_E(grow(&e->d_off, &dummy, (size_t)e->S)); dummy = 0;
   TRY_E(grow(&e->d_nhi, &dummy, (size_t)e->S)); dummy = 0;
-  const std::vector<double>& lines = host_line_data();
+  const std::vector<double>& lines = host_line_data().buf;
   TRY_E(grow(&e->d_lines, &dummy, lines.size())); dummy = 0;
   TRY_E(grow(&e->d_status, &dummy, 1));
   TRY_E(upload(e->d_rest, model->rest_wavelengths, G * 8, e->stream));
@@ -424,10 +443,13 @@ int gpdla_engine_process(gpdla_engine* e, const gpdla_spectra* sp, const gpdla_r
     la.info = e->d_info; la.panel = e->d_panel; la.lam_pad = e->d_lam;
     la.offsets = e->d_off; la.nhi = e->d_nhi; la.S = e->S;
     la.num_lines = e->params.num_lines;
-    la.line_tabs = e->d_lines;
-    la.line_mult = e->d_lines + (size_t)kMaxLines * kLineTableStride;
+    la.lines = make_line_args(e->d_lines);
     la.scratch = e->d_scratch;
-    la.sample_ll = o_sll; la.ld = ld; la.ll_null = o_null; la.status = e->d_status;
+    la.status = e->d_status;
+
+    SolveArgs sa{};
+    sa.q_count = (int32_t)nq; sa.info = e->d_info; sa.scratch = e->d_scratch; sa.S = e->S;
+    sa.sample_ll = o_sll; sa.ld = ld; sa.ll_null = o_null; sa.status = e->d_status;
 
     ReduceArgs ra{};
     ra.q_count = (int32_t)nq; ra.info = e->d_info; ra.sample_ll = o_sll; ra.ld = ld; ra.S = e->S;
@@ -442,6 +464,11 @@ int gpdla_engine_process(gpdla_engine* e, const gpdla_spectra* sp, const gpdla_r
     HIP_TRY(launch_likelihood(e->K, la, st));
     HIP_TRY(hipEventRecord(t1.stop, st));
     e->pending.push_back(t1);
+    TimedLaunch t3{};
+    if ((rc = record_start(e, &t3, 3))) return rc;
+    HIP_TRY(launch_solve(e->K, sa, blocks_x, st));
+    HIP_TRY(hipEventRecord(t3.stop, st));
+    e->pending.push_back(t3);
     if ((rc = record_start(e, &t2, 2))) return rc;
     HIP_TRY(launch_reduce(ra, st));
     HIP_TRY(hipEventRecord(t2.stop, st));
@@ -555,7 +582,7 @@ static int lines_on_device(double** d_lines) {
   std::lock_guard<std::mutex> lock(mu);
   if ((int)per_dev.size() <= dev) per_dev.resize(dev + 1, nullptr);
   if (!per_dev[dev]) {
-    const std::vector<double>& lines = host_line_data();
+    const std::vector<double>& lines = host_line_data().buf;
     double* p = nullptr;
     HIP_TRY(hipMalloc((void**)&p, lines.size() * 8));
     HIP_TRY(hipMemcpy(p, lines.data(), lines.size() * 8, hipMemcpyHostToDevice));
@@ -585,7 +612,7 @@ int gpdla_voigt_batch_f64(const double* lambdas, int64_t n_padded, const double*
   if (err == hipSuccess) err = hipMemcpy(d_lam, lambdas, n_padded * 8, hipMemcpyHostToDevice);
   if (err == hipSuccess) err = hipMemcpy(d_z, z, count * 8, hipMemcpyHostToDevice);
   if (err == hipSuccess) err = hipMemcpy(d_N, N, count * 8, hipMemcpyHostToDevice);
-  if (err == hipSuccess) err = launch_voigt_batch(d_lam, n_padded, d_z, d_N, count, num_lines, d_lines, d_out, nullptr);
+  if (err == hipSuccess) err = launch_voigt_batch(d_lam, n_padded, d_z, d_N, count, num_lines, make_line_args(d_lines), d_out, nullptr);
   if (err == hipSuccess) err = hipMemcpy(out, d_out, count * n_out * 8, hipMemcpyDeviceToHost);
   cleanup();
   if (err != hipSuccess) return set_error(GPDLA_EDEVICE, "voigt: %s", hipGetErrorString(err));

@@ -134,58 +134,95 @@ std::vector<long double> cheb_fit_monomial(const std::vector<long double>& fvals
 
 }  // namespace
 
-// Fit the table of line j (layout: line_profile.h).  Returns the max relative error of the
-// double-precision evaluation against the long-double function on a dense check grid.
-double fit_line_table(int j, double* tab) {
+// Per-line wing constants: f_j = A_j T (g + B_j T h) for |x| >= kCoreX.
+void line_wing_constants(int j, double* A, double* B) {
   const long double sig = (long double)kSigma;
   const long double y = (long double)kLorentzGammas[j] / (sig * std::sqrt(2.0L));
   const long double scale = (long double)kLeadingConstants[j] / (sig * std::sqrt(2.0L * kPiL));
-  auto f = [&](long double x) { return scale * faddeeva_w(x, y).real(); };
+  *A = (double)(scale * y);
+  *B = (double)(y * y);
+}
 
-  // core pieces: polynomial in u = x - centre, |u| <= kPieceW / 2
+namespace {
+
+// (a T + b)^n expansion of a polynomial given in s = a T + b (monomials), -> powers of T
+std::vector<long double> shift_to_T(const std::vector<long double>& mono_s, long double a, long double b) {
+  const int N = (int)mono_s.size();
+  std::vector<long double> t(N, 0.0L);
+  for (int n = 0; n < N; ++n) {
+    long double binom = 1.0L;
+    for (int r = 0; r <= n; ++r) {
+      t[r] += mono_s[n] * binom * std::pow(a, (long double)r) * std::pow(b, (long double)(n - r));
+      binom = binom * (n - r) / (r + 1);
+    }
+  }
+  return t;
+}
+
+// G(T; y) = Re w(1/sqrt(T) + i y) / (y T)
+long double wing_G(long double T, long double y) {
+  const long double x = 1.0L / std::sqrt(T);
+  return faddeeva_w(x, y).real() / (y * T);
+}
+
+}  // namespace
+
+// Universal damping-wing polynomials g, h on T in (0, 1/kCoreX^2]:  G(T; y) = g(T) + y^2 T h(T) + O(y^4 T^2).
+// Richardson in y^2 at y1, y2 = 2 y1 separates g and h.
+void fit_wing(WingPoly* w) {
+  const long double Tmax = 1.0L / ((long double)kCoreX * kCoreX);
+  const long double y1 = 1e-3L, y2 = 2e-3L;
+  for (int pass = 0; pass < 2; ++pass) {
+    const int NW = pass == 0 ? kWingG : kWingH;
+    std::vector<long double> v(NW);
+    for (int k = 0; k < NW; ++k) {
+      const long double s = std::cos(kPiL * (k + 0.5L) / NW);
+      const long double T = Tmax * (s + 1.0L) / 2.0L;
+      const long double G1 = wing_G(T, y1), G2 = wing_G(T, y2);
+      v[k] = pass == 0 ? (4.0L * G1 - G2) / 3.0L : (G2 - G1) / (3.0L * y1 * y1 * T);
+    }
+    std::vector<long double> t = shift_to_T(cheb_fit_monomial(v), 2.0L / Tmax, -1.0L);
+    for (int n = 0; n < NW; ++n) (pass == 0 ? w->g : w->h)[n] = (double)t[n];
+  }
+}
+
+// Core table of line j (kPieces x kCoreStride, polynomial in u = |x| - centre).
+void fit_core_table(int j, double* core) {
+  const long double sig = (long double)kSigma;
+  const long double y = (long double)kLorentzGammas[j] / (sig * std::sqrt(2.0L));
+  const long double scale = (long double)kLeadingConstants[j] / (sig * std::sqrt(2.0L * kPiL));
   const int N = kCoreDeg + 1;
   for (int p = 0; p < kPieces; ++p) {
     const long double centre = (p + 0.5L) * kPieceW, half = 0.5L * kPieceW;
     std::vector<long double> fv(N);
-    for (int k = 0; k < N; ++k) fv[k] = f(centre + half * std::cos(kPiL * (k + 0.5L) / N));
+    for (int k = 0; k < N; ++k)
+      fv[k] = scale * faddeeva_w(centre + half * std::cos(kPiL * (k + 0.5L) / N), y).real();
     std::vector<long double> mono = cheb_fit_monomial(fv);  // in s = u / half
     long double sc = 1.0L;
     for (int n = 0; n < N; ++n) {
-      tab[p * kCoreStride + n] = (double)(mono[n] * sc);
+      core[p * kCoreStride + n] = (double)(mono[n] * sc);
       sc /= half;
     }
   }
-  // damping wing: G(T) = f(x) x^2, T = 1/x^2 in (0, 1/kCoreX^2]
-  const int NW = kWingDeg + 1;
-  const long double Tmax = 1.0L / ((long double)kCoreX * kCoreX);
-  std::vector<long double> gv(NW);
-  for (int k = 0; k < NW; ++k) {
-    const long double s = std::cos(kPiL * (k + 0.5L) / NW);  // s in (-1,1) -> T = Tmax (s+1)/2
-    const long double T = Tmax * (s + 1.0L) / 2.0L;
-    const long double x = 1.0L / std::sqrt(T);
-    gv[k] = f(x) * x * x;
-  }
-  std::vector<long double> mono = cheb_fit_monomial(gv);  // in s
-  // s = 2T/Tmax - 1 -> expand sum_n m_n (2T/Tmax - 1)^n into powers of T
-  std::vector<long double> tcoef(NW, 0.0L);
-  for (int n = 0; n < NW; ++n) {
-    // (a T + b)^n, a = 2/Tmax, b = -1
-    long double binom = 1.0L;
-    for (int r = 0; r <= n; ++r) {
-      // C(n, r) a^r b^(n-r)
-      tcoef[r] += mono[n] * binom * std::pow(2.0L / Tmax, (long double)r) * ((n - r) % 2 ? -1.0L : 1.0L);
-      binom = binom * (n - r) / (r + 1);
-    }
-  }
-  double* wing = tab + kPieces * kCoreStride;
-  for (int n = 0; n < kWingStride; ++n) wing[n] = n < NW ? (double)tcoef[n] : 0.0;
+}
 
-  // self-check
+// Max relative error of the double-precision line profile of line j against the long-double
+// source on a dense grid (core: 36k points, wing: geometric out to |x| = 2e6).
+double line_profile_error(int j) {
+  std::vector<double> core(kCoreTable);
+  fit_core_table(j, core.data());
+  WingPoly w;
+  fit_wing(&w);
+  double A, B;
+  line_wing_constants(j, &A, &B);
+  const long double sig = (long double)kSigma;
+  const long double y = (long double)kLorentzGammas[j] / (sig * std::sqrt(2.0L));
+  const long double scale = (long double)kLeadingConstants[j] / (sig * std::sqrt(2.0L * kPiL));
   double maxrel = 0;
-  for (int i = 0; i <= 40000; ++i) {
-    const double x = (i < 28000) ? i * (kCoreX / 28000.0) * 1.0 : kCoreX * std::pow(1.0005, i - 28000);
-    const double got = line_profile_eval(tab, x);
-    const long double ref = f((long double)x);
+  for (int i = 0; i <= 48000; ++i) {
+    const double x = (i < 36000) ? i * (kCoreX / 36000.0) : kCoreX * std::pow(1.0004, i - 36000);
+    const double got = line_profile_eval(core.data(), w, A, B, x);
+    const long double ref = scale * faddeeva_w((long double)x, y).real();
     const double rel = (double)std::fabs((got - ref) / ref);
     if (rel > maxrel) maxrel = rel;
   }

@@ -91,6 +91,21 @@ struct PrepArgs {
   int32_t* slot_pixel;           // scratch map slot -> pixel (size = total slot capacity)
 };
 
+// Line-profile data.  Device buffer layout (doubles):
+//   [kMaxLines][kCoreTable] core tables | fac[kMaxLines] | A[kMaxLines] | B[kMaxLines]
+// fac_j = c / (lambda_j 1e8) / (sigma sqrt 2), so x_j = lambda * fac_j / (1 + z) - c / (sigma sqrt 2)
+// (voigt.c:278-279,287 divided by sigma sqrt 2).
+constexpr size_t kLineBufFac = (size_t)kMaxLines * kCoreTable;
+constexpr size_t kLineBufA = kLineBufFac + kMaxLines;
+constexpr size_t kLineBufB = kLineBufA + kMaxLines;
+constexpr size_t kLineBufDoubles = kLineBufB + kMaxLines;
+
+struct LineArgs {
+  const double* buf;   // device line buffer (layout above)
+  WingPoly wing;       // universal damping-wing polynomials (SGPR-resident)
+  double fac3[3], A3[3], B3[3];  // Lyman alpha, beta, gamma: the 3-line fast path
+};
+
 struct LikelihoodArgs {
   int32_t q_count;
   const SpecInfo* info;
@@ -100,9 +115,16 @@ struct LikelihoodArgs {
   const double* nhi;             // [S]
   int64_t S;
   int32_t num_lines;
-  const double* line_tabs;       // [num_lines][kLineTableStride]
-  const double* line_mult;       // [num_lines] c / lambda_j (host-precomputed pieces), see kernel
+  LineArgs lines;
   double* scratch;               // [grid blocks][64][kES]
+  int32_t* status;
+};
+
+struct SolveArgs {
+  int32_t q_count;
+  const SpecInfo* info;
+  const double* scratch;
+  int64_t S;
   double* sample_ll;             // [q_count][ld] or nullptr
   int64_t ld;
   double* ll_null;               // [q_count]
@@ -123,10 +145,11 @@ struct ReduceArgs {
 
 hipError_t launch_prep(int K, const PrepArgs& a, hipStream_t s);
 hipError_t launch_likelihood(int K, const LikelihoodArgs& a, hipStream_t s);
+hipError_t launch_solve(int K, const SolveArgs& a, int64_t blocks_x, hipStream_t s);
 hipError_t launch_reduce(const ReduceArgs& a, hipStream_t s);
 hipError_t launch_voigt_batch(const double* lambdas, int64_t n_padded, const double* z,
                               const double* N, int64_t count, int32_t num_lines,
-                              const double* line_tabs, double* out, hipStream_t s);
+                              const LineArgs& lines, double* out, hipStream_t s);
 hipError_t launch_mvn_single(const double* y, const double* mu, const double* M_colmajor,
                              const double* d, int64_t n, int32_t k, double* out,
                              int32_t* status, hipStream_t s);
@@ -135,6 +158,9 @@ int panel_row_doubles(int K);
 int scratch_doubles(int K);
 
 // host-side table fitting (faddeeva_host.cpp)
-double fit_line_table(int line, double* tab);
+void fit_core_table(int line, double* core);
+void fit_wing(WingPoly* w);
+void line_wing_constants(int line, double* A, double* B);
+double line_profile_error(int line);
 
 }  // namespace gpdla

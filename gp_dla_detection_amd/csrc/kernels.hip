@@ -144,18 +144,35 @@ __device__ inline double interp_eval(const double* xp, const double* fp, int G, 
 
 // ---------------------------------------------------------------------------------------------
 // Voigt raw profile at one padded wavelength: exp(N * total), total = -sum_j lc_j V_j(v_j)
-// (voigt.c:282-292).  `a_j` = c/(lambda_j 1e8) / (1+z) / (sigma sqrt 2) per line is formed from
-// the host-computed line factor and the lane's 1/(1+z).
+// (voigt.c:282-292).  x_j = lambda * fac_j / (1+z) - c/(sigma sqrt 2) (voigt.c:278-279,287).
 // ---------------------------------------------------------------------------------------------
+constexpr double kC2 = kCcgs / (kSigma * 1.41421356237309504880);  // c / (sigma sqrt 2)
+
+// generic: any number of lines, core tables in global memory
 __device__ inline double raw_profile(double lam, double zfac, double N, int num_lines,
-                                     const double* __restrict__ line_tabs,
-                                     const double* __restrict__ line_mult) {
-  constexpr double kC2 = kCcgs / (kSigma * 1.41421356237309504880);  // c / (sigma sqrt 2)
+                                     const LineArgs& L) {
   double total = 0.0;
   for (int j = 0; j < num_lines; ++j) {
-    const double aj = line_mult[j] * zfac;
-    const double x = fma(lam, aj, -kC2);
-    total -= line_profile_eval(line_tabs + j * kLineTableStride, x);
+    const double x = fma(lam, L.buf[kLineBufFac + j] * zfac, -kC2);
+    total -= line_profile_eval(L.buf + (size_t)j * kCoreTable, L.wing, L.buf[kLineBufA + j],
+                               L.buf[kLineBufB + j], x);
+  }
+  return exp(N * total);
+}
+
+// 3-line fast path (Lyman alpha, beta, gamma; set_parameters.m:63): the damping wing is
+// evaluated branch-free for every lane, the core polynomial (LDS tables) only by the rare
+// lanes with |x| < kCoreX.
+__device__ inline double raw_profile3(double lam, const double (&afac)[3], double N,
+                                      const double* __restrict__ core_lds, const LineArgs& L) {
+  double total = 0.0;
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const double x = fma(lam, afac[j], -kC2);
+    const double ax = fabs(x);
+    double f = wing_eval(L.wing, L.A3[j], L.B3[j], x);
+    if (ax < kCoreX) f = core_eval(core_lds + j * kCoreTable, ax);
+    total -= f;
   }
   return exp(N * total);
 }
@@ -330,30 +347,60 @@ __global__ __launch_bounds__(256) void prep_kernel(PrepArgs a) {
 // likelihood: for one spectrum (blockIdx.y) and 64 samples (4 waves x 16), sweep all slots:
 //   per lane (sample s = lane & 15, segment g = lane >> 4): Voigt raw profile at the leading
 //   padded wavelength, 7-tap convolution from a register window, DLA-modulated pixel terms
-//   a^2/d and a r/d (process_qsos.m:189-197), then v_mfma_f64_4x4x4_4b over the 58 Khatri-Rao
-//   tiles (Gram + u).  Epilogue: per-sample augmented LDL^T (quad of lanes per sample) ->
-//   log N(y; a mu, diag(a) M M' diag(a) + diag(a^2 w^2 + sigma^2)) (log_mvnpdf_low_rank.m).
+//   a^2/d and a r/d (process_qsos.m:189-197), then v_mfma_f64_4x4x4_4b over the Khatri-Rao
+//   tiles (Gram + u).  Panel rows are staged chunk by chunk into a double-buffered LDS ring by
+//   global_load_lds (the next chunk's DMA overlaps this chunk's compute).  The epilogue writes the
+//   per-sample Gram / u / scalars to `scratch` for solve_kernel.
 // ---------------------------------------------------------------------------------------------
 template <int K>
-__global__ __launch_bounds__(256) void likelihood_kernel(LikelihoodArgs a) {
+__device__ inline void stage_chunk(const double* __restrict__ panel, int L, int c, double* buf,
+                                   int wave, int lane) {
+  using Lay = Layout<K>;
+  constexpr int kGran = Lay::kRow / 2;                 // 16-byte granules per row
+  constexpr int kTot = 4 * kChunkSteps * kGran;        // granules per chunk
+  constexpr int kInstr = (kTot + 63) / 64;             // 1 KiB wave instructions per chunk
+  for (int i = wave; i < kInstr; i += kWavesPerBlock) {
+    const int gi = i * 64 + lane;
+    if (gi < kTot) {
+      const int r = gi / kGran, o = gi - r * kGran;
+      const int tt = r >> 2, gg = r & 3;
+      const double* src = panel + ((int64_t)gg * L + c * kChunkSteps + tt) * Lay::kRow + 2 * o;
+      // global_load_lds_dwordx4: 64 lanes x 16 B land at M0 + lane*16.  Issued from inline asm so
+      // hipcc does not make the other buffer's ds_reads wait on it; the consumer side waits with
+      // an explicit s_waitcnt vmcnt(0) + barrier at the end of the chunk.
+      const uint32_t dst = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)(buf + i * 128);
+      asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, off"
+                   :: "s"(__builtin_amdgcn_readfirstlane(dst)), "v"(src) : "memory", "m0");
+    }
+  }
+}
+
+template <int K, int NL>
+__global__ __launch_bounds__(256, 2) void likelihood_kernel(LikelihoodArgs a) {
   using Lay = Layout<K>;
   constexpr int kTiles = Lay::kTiles;
   constexpr int kGT = Lay::kGT;
   constexpr int kRow = Lay::kRow;
   constexpr int kJS = Lay::kJS;
-  __shared__ __attribute__((aligned(16))) double lds[4 * kChunkSteps * kRow];
+  constexpr int kBuf = 4 * kChunkSteps * kRow;
+  constexpr int kCoreLds = NL == 3 ? 3 * kCoreTable : 1;
+  __shared__ __attribute__((aligned(16))) double lds[2 * kBuf + kCoreLds];
+  double* core_lds = lds + 2 * kBuf;
 
   const int q = blockIdx.y;
   const SpecInfo inf = a.info[q];
+  if (inf.J == 0) return;  // unusable spectrum: solve_kernel writes NaN
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int64_t block_lin = (int64_t)blockIdx.y * gridDim.x + blockIdx.x;
   const int64_t s_base = (int64_t)blockIdx.x * kSamplesPerBlock + wave * kSamplesPerWave;
+  const int L = inf.L;
+  const int nchunks = (L + kChunkSteps - 1) / kChunkSteps;
+  const double* panel = a.panel + inf.slot_base * kRow;
 
-  if (inf.J == 0) {  // unusable spectrum: NaN outputs (MATLAB would have errored)
-    const int64_t s = s_base + (lane & 15);
-    if (lane < 16 && s < a.S && a.sample_ll) a.sample_ll[q * a.ld + s] = NAN;
-    if (lane < 16 && s == a.S) a.ll_null[q] = NAN;
-    return;
+  // prologue: first chunk's DMA, then the core tables (plain loads) while it flies
+  stage_chunk<K>(panel, L, 0, lds, wave, lane);
+  if constexpr (NL == 3) {
+    for (int i = threadIdx.x; i < 3 * kCoreTable; i += 256) core_lds[i] = a.lines.buf[i];
   }
 
   // ---- per-lane sample constants (MFMA A-operand layout: sample = lane & 15, segment = lane >> 4)
@@ -365,70 +412,69 @@ __global__ __launch_bounds__(256) void likelihood_kernel(LikelihoodArgs a) {
   const double N = (s < a.S) ? a.nhi[s] : 0.0;
   const double zdla = inf.zmin + (inf.zmax - inf.zmin) * off;  // process_qsos.m:163-165
   const double zfac = 1.0 / (1 + zdla);
-  const int L = inf.L;
-
-  // ---- sliding window: raw profile at padded positions gL + 0..5
+  double afac[3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) afac[j] = a.lines.fac3[j] * zfac;
   const double* lamp = a.lam_pad + inf.lam_base + (int64_t)g * L;
-  double w0 = raw_profile(lamp[0], zfac, N, a.num_lines, a.line_tabs, a.line_mult);
-  double w1 = raw_profile(lamp[1], zfac, N, a.num_lines, a.line_tabs, a.line_mult);
-  double w2 = raw_profile(lamp[2], zfac, N, a.num_lines, a.line_tabs, a.line_mult);
-  double w3 = raw_profile(lamp[3], zfac, N, a.num_lines, a.line_tabs, a.line_mult);
-  double w4 = raw_profile(lamp[4], zfac, N, a.num_lines, a.line_tabs, a.line_mult);
-  double w5 = raw_profile(lamp[5], zfac, N, a.num_lines, a.line_tabs, a.line_mult);
+  double lw[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) lw[i] = lamp[i];
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  auto raw = [&](double lam) {
+    if constexpr (NL == 3) return raw_profile3(lam, afac, N, core_lds, a.lines);
+    else return raw_profile(lam, zfac, N, a.num_lines, a.lines);
+  };
+  // sliding window: raw profile at padded positions gL + 0..5
+  double w0 = raw(lw[0]), w1 = raw(lw[1]), w2 = raw(lw[2]);
+  double w3 = raw(lw[3]), w4 = raw(lw[4]), w5 = raw(lw[5]);
 
   double acc[kTiles];
 #pragma unroll
   for (int t = 0; t < kTiles; ++t) acc[t] = 0.0;
-  double q1 = 0.0;       // sum r^2 / d
-  double pm = 1.0;       // prod d = pm * 2^pe
+  double q1 = 0.0;  // sum r^2 / d
+  double pm = 1.0;  // prod d = pm * 2^pe
   int pe = 0;
 
-  const int nchunks = (L + kChunkSteps - 1) / kChunkSteps;
-  const double* panel = a.panel + inf.slot_base * kRow;
   for (int c = 0; c < nchunks; ++c) {
-    __syncthreads();
-    {  // stage 4 segments x kChunkSteps rows (double2 granules)
-      constexpr int kHalfRow = kRow / 2;
-      constexpr int kTotal = 4 * kChunkSteps * kHalfRow;
-      for (int idx = threadIdx.x; idx < kTotal; idx += 256) {
-        const int r = idx / kHalfRow, o = idx - r * kHalfRow;
-        const int tt = r >> 2, gg = r & 3;
-        const int64_t slot = (int64_t)gg * L + c * kChunkSteps + tt;
-        reinterpret_cast<double2*>(lds)[idx] = reinterpret_cast<const double2*>(panel + slot * kRow)[o];
-      }
-    }
-    __syncthreads();
+    double* cur = lds + (c & 1) * kBuf;
+    if (c + 1 < nchunks) stage_chunk<K>(panel, L, c + 1, lds + ((c + 1) & 1) * kBuf, wave, lane);
 #pragma unroll
     for (int tt = 0; tt < kChunkSteps; ++tt) {
       const int t = c * kChunkSteps + tt;
-      const double* row = lds + (tt * 4 + g) * kRow;
-      const double lam = row[Lay::kLam];
-      const double y = row[Lay::kY];
-      const double noise = row[Lay::kNoise];
-      const double mu = row[Lay::kMu];
-      const double om2 = row[Lay::kOmega2];
-      const bool valid = row[Lay::kValid] != 0.0;
-      const double w6 = raw_profile(lam, zfac, N, a.num_lines, a.line_tabs, a.line_mult);
+      const double* row = cur + (tt * 4 + g) * kRow;
+      double lam, y, noise, mu, om2, vld;
+      if constexpr ((kTiles & 1) == 0) {
+        const double2 s0 = *reinterpret_cast<const double2*>(row + Lay::kLam);
+        const double2 s1 = *reinterpret_cast<const double2*>(row + Lay::kNoise);
+        const double2 s2 = *reinterpret_cast<const double2*>(row + Lay::kOmega2);
+        lam = s0.x; y = s0.y; noise = s1.x; mu = s1.y; om2 = s2.x; vld = s2.y;
+      } else {
+        lam = row[Lay::kLam]; y = row[Lay::kY]; noise = row[Lay::kNoise];
+        mu = row[Lay::kMu]; om2 = row[Lay::kOmega2]; vld = row[Lay::kValid];
+      }
+      const double w6 = raw(lam);
       // instrumental broadening, voigt.c:297-299 (zero-initialised accumulator, taps in order)
-      double ab = 0.0;
-      ab += w0 * kInstrumentProfile[0];
-      ab += w1 * kInstrumentProfile[1];
-      ab += w2 * kInstrumentProfile[2];
-      ab += w3 * kInstrumentProfile[3];
-      ab += w4 * kInstrumentProfile[4];
-      ab += w5 * kInstrumentProfile[5];
-      ab += w6 * kInstrumentProfile[6];
+      double ab = w0 * kInstrumentProfile[0];
+      ab = fma(w1, kInstrumentProfile[1], ab);
+      ab = fma(w2, kInstrumentProfile[2], ab);
+      ab = fma(w3, kInstrumentProfile[3], ab);
+      ab = fma(w4, kInstrumentProfile[4], ab);
+      ab = fma(w5, kInstrumentProfile[5], ab);
+      ab = fma(w6, kInstrumentProfile[6], ab);
       w0 = w1; w1 = w2; w2 = w3; w3 = w4; w4 = w5; w5 = w6;
       if (is_null) ab = 1.0;  // null model: no absorption (process_qsos.m:150-152)
       // process_qsos.m:191-197 and log_mvnpdf_low_rank.m:11-15
-      const double r = y - mu * ab;
+      const double r = fma(-mu, ab, y);
       const double a2 = ab * ab;
-      const double d = om2 * a2 + noise;
+      const double d = fma(om2, a2, noise);
       const double dinv = rcp_nr(d);
-      const bool use = active && valid && (t < L);
+      const bool use = active && (vld != 0.0) && (t < L);
+      const double rd = r * dinv;
       const double wg = use ? a2 * dinv : 0.0;
-      const double wu = use ? ab * r * dinv : 0.0;
-      q1 += use ? r * r * dinv : 0.0;
+      const double wu = use ? ab * rd : 0.0;
+      q1 = use ? fma(r, rd, q1) : q1;
       pm *= use ? d : 1.0;
       // B operands: tile t, entry 4t + (lane & 3) of this lane's segment row
       const double* brow = row + (lane & 3) * kJS;
@@ -448,6 +494,8 @@ __global__ __launch_bounds__(256) void likelihood_kernel(LikelihoodArgs a) {
       pm = frexp(pm, &ex);
       pe += ex;
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA for chunk c+1 landed
+    __syncthreads();                                   // ... and everyone's; buffer c free again
   }
 
   // ---- combine the 4 segments of each sample (lanes l, l^16, l^32, l^48)
@@ -462,28 +510,46 @@ __global__ __launch_bounds__(256) void likelihood_kernel(LikelihoodArgs a) {
     pe += pe2 + ex;
   }
 
-  // ---- epilogue 1: accumulators -> scratch (sample-major); D lane map of 4x4x4_4b:
+  // ---- epilogue: accumulators -> scratch (sample-major); D lane map of 4x4x4_4b:
   //      sample 4*((lane>>2)&3) + (lane>>4), entry 4t + (lane&3)
   double* scr = a.scratch + (block_lin * kSamplesPerBlock + wave * kSamplesPerWave) * Lay::kES;
-  {
-    const int sd = 4 * ((lane >> 2) & 3) + (lane >> 4);
-    double* dst = scr + sd * Lay::kES + (lane & 3);
+  const int sd = 4 * ((lane >> 2) & 3) + (lane >> 4);
+  double* dst = scr + sd * Lay::kES + (lane & 3);
 #pragma unroll
-    for (int t = 0; t < kTiles; ++t) dst[4 * t] = acc[t];
-    if (lane < 16) {
-      double* sc = scr + lane * Lay::kES + 4 * kTiles;
-      sc[0] = q1;
-      sc[1] = pm;
-      sc[2] = (double)pe;
-    }
+  for (int t = 0; t < kTiles; ++t) dst[4 * t] = acc[t];
+  if (lane < 16) {
+    double* sc = scr + lane * Lay::kES + 4 * kTiles;
+    sc[0] = q1;
+    sc[1] = pm;
+    sc[2] = (double)pe;
   }
-  __syncthreads();
+}
 
-  // ---- epilogue 2: augmented LDL^T per sample, one quad of lanes per sample.
-  //      Lane jq owns Gram columns c = 4jj + jq (rows 0..4jj+3) and u rows i = 4m + jq.
+// ---------------------------------------------------------------------------------------------
+// solve: per-sample augmented LDL^T, one quad of lanes per sample (the wave's 16 samples).
+//   Lane jq owns Gram columns c = 4jj + jq (rows 0..4jj+3) and u rows i = 4m + jq; pivot rows
+//   are broadcast inside the quad with DPP.  B = I + M'D^-1 M (log_mvnpdf_low_rank.m:22-24),
+//   [B u; u' q1] = L D L' gives log det B = sum log D_p and r'K^-1 r = the last pivot
+//   (log_mvnpdf_low_rank.m:26-32).
+// ---------------------------------------------------------------------------------------------
+template <int K>
+__global__ __launch_bounds__(256) void solve_kernel(SolveArgs a) {
+  using Lay = Layout<K>;
+  constexpr int kTiles = Lay::kTiles;
+  constexpr int kGT = Lay::kGT;
   constexpr int NJJ = (K + 3) / 4;
+  const int q = blockIdx.y;
+  const SpecInfo inf = a.info[q];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int jq = lane & 3, sq = lane >> 2;
-  const double* srow = scr + sq * Lay::kES;
+  const int64_t block_lin = (int64_t)blockIdx.y * gridDim.x + blockIdx.x;
+  const int64_t s2 = (int64_t)blockIdx.x * kSamplesPerBlock + wave * kSamplesPerWave + sq;
+  if (inf.J == 0) {
+    if (jq == 0 && s2 < a.S && a.sample_ll) a.sample_ll[q * a.ld + s2] = NAN;
+    if (jq == 0 && s2 == a.S) a.ll_null[q] = NAN;
+    return;
+  }
+  const double* srow = a.scratch + ((block_lin * kSamplesPerBlock) + wave * kSamplesPerWave + sq) * Lay::kES;
   double A[NJJ][4 * NJJ];
   double U[NJJ];
 #pragma unroll
@@ -537,7 +603,6 @@ __global__ __launch_bounds__(256) void likelihood_kernel(LikelihoodArgs a) {
     }
     quad = fma(-up, upinv, quad);
   }
-  const int64_t s2 = s_base + sq;
   if (jq == 0 && s2 <= a.S) {
     const double logdet_b = log(pb) + eb * kLn2;
     const double logdet_d = log(dm) + de * kLn2;
@@ -588,9 +653,7 @@ __global__ __launch_bounds__(256) void voigt_batch_kernel(const double* __restri
                                                           int64_t n_padded,
                                                           const double* __restrict__ zs,
                                                           const double* __restrict__ Ns,
-                                                          int32_t num_lines,
-                                                          const double* __restrict__ line_tabs,
-                                                          const double* __restrict__ line_mult,
+                                                          int32_t num_lines, LineArgs lines,
                                                           double* __restrict__ out) {
   __shared__ double raw[256 + 2 * kWidth];
   const int64_t sidx = blockIdx.x;
@@ -602,7 +665,7 @@ __global__ __launch_bounds__(256) void voigt_batch_kernel(const double* __restri
     __syncthreads();
     for (int i = threadIdx.x; i < 256 + 2 * kWidth; i += 256) {
       const int64_t p = base + i;
-      raw[i] = (p < n_padded) ? raw_profile(lambdas[p], zfac, N, num_lines, line_tabs, line_mult) : 0.0;
+      raw[i] = (p < n_padded) ? raw_profile(lambdas[p], zfac, N, num_lines, lines) : 0.0;
     }
     __syncthreads();
     const int64_t i = base + threadIdx.x;
@@ -696,7 +759,16 @@ hipError_t launch_prep_k(const PrepArgs& a, hipStream_t s) {
 template <int K>
 hipError_t launch_likelihood_k(const LikelihoodArgs& a, hipStream_t s) {
   const int64_t blocks_x = (a.S + 1 + kSamplesPerBlock - 1) / kSamplesPerBlock;
-  hipLaunchKernelGGL(likelihood_kernel<K>, dim3((unsigned)blocks_x, a.q_count), dim3(256), 0, s, a);
+  if (a.num_lines == 3)
+    hipLaunchKernelGGL((likelihood_kernel<K, 3>), dim3((unsigned)blocks_x, a.q_count), dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL((likelihood_kernel<K, 0>), dim3((unsigned)blocks_x, a.q_count), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+template <int K>
+hipError_t launch_solve_k(const SolveArgs& a, int64_t blocks_x, hipStream_t s) {
+  hipLaunchKernelGGL(solve_kernel<K>, dim3((unsigned)blocks_x, a.q_count), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 
@@ -739,6 +811,13 @@ hipError_t launch_likelihood(int K, const LikelihoodArgs& a, hipStream_t s) {
   return hipErrorInvalidValue;
 }
 
+hipError_t launch_solve(int K, const SolveArgs& a, int64_t blocks_x, hipStream_t s) {
+#define X(k) if (K == k) return launch_solve_k<k>(a, blocks_x, s);
+  GPDLA_FOR_EACH_RANK(X)
+#undef X
+  return hipErrorInvalidValue;
+}
+
 hipError_t launch_reduce(const ReduceArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(reduce_kernel, dim3(a.q_count), dim3(256), 0, s, a);
   return hipGetLastError();
@@ -746,11 +825,9 @@ hipError_t launch_reduce(const ReduceArgs& a, hipStream_t s) {
 
 hipError_t launch_voigt_batch(const double* lambdas, int64_t n_padded, const double* z,
                               const double* N, int64_t count, int32_t num_lines,
-                              const double* line_tabs_and_mult, double* out, hipStream_t s) {
-  const double* tabs = line_tabs_and_mult;
-  const double* mult = line_tabs_and_mult + (int64_t)kMaxLines * kLineTableStride;
+                              const LineArgs& lines, double* out, hipStream_t s) {
   hipLaunchKernelGGL(voigt_batch_kernel, dim3((unsigned)count), dim3(256), 0, s, lambdas,
-                     n_padded, z, N, num_lines, tabs, mult, out);
+                     n_padded, z, N, num_lines, lines, out);
   return hipGetLastError();
 }
 
