@@ -1,0 +1,71 @@
+#!/usr/bin/env python3
+"""Summarise a tools/profile.sh run (rocprofv3 CSVs) into profiles/<tag>_summary.json + .md.
+
+Traffic accounting follows /opt/skills/guides/MI355X_MICROARCH.md (HBM section): FETCH_SIZE and
+WRITE_SIZE are in KiB, collected in separate passes; on gfx950 FETCH_SIZE reports half the bytes
+of a wide (16 B/lane) coalesced streaming read, so the read side is doubled.  Counts include
+Infinity-Cache (MALL) hits.
+"""
+from __future__ import annotations
+
+import collections
+import csv
+import json
+import sys
+from pathlib import Path
+
+
+def load_counters(path):
+    agg = collections.defaultdict(list)
+    for r in csv.DictReader(open(path)):
+        agg[(r["Kernel_Name"], r["Counter_Name"])].append(float(r["Counter_Value"]))
+    return agg
+
+
+def main(src: str, tag: str, dst: str = "profiles"):
+    src, dst = Path(src), Path(dst)
+    dst.mkdir(exist_ok=True)
+    stats = list(csv.DictReader(open(src / "trace" / "trace_kernel_stats.csv")))
+    fetch = load_counters(src / "fetch" / "fetch_counter_collection.csv")
+    write = load_counters(src / "write" / "write_counter_collection.csv")
+    sq = load_counters(src / "sq" / "sq_counter_collection.csv")
+    bench = json.loads((src / "bench_trace.json").read_text().strip().splitlines()[-1])
+    out = {"tag": tag, "bench_under_trace": {k: bench[k] for k in ("value", "unit", "ms_per_step", "kernel_ms")},
+           "kernels": []}
+    for row in stats:
+        name = row["Name"]
+        short = name.replace("(anonymous namespace)::", "")
+        ent = {"kernel": short, "calls": int(row["Calls"]), "avg_ms": float(row["AverageNs"]) / 1e6,
+               "pct": float(row["Percentage"])}
+        key = next((k for k in fetch if k[0] == name and k[1] == "FETCH_SIZE"), None)
+        wkey = next((k for k in write if k[0] == name and k[1] == "WRITE_SIZE"), None)
+        if key and wkey:
+            f_kib = sum(fetch[key]) / len(fetch[key])
+            w_kib = sum(write[wkey]) / len(write[wkey])
+            ent["fetch_size_kib"] = f_kib
+            ent["write_size_kib"] = w_kib
+            ent["hbm_bytes_per_launch"] = (2 * f_kib + w_kib) * 1024
+            ent["hbm_gbs"] = ent["hbm_bytes_per_launch"] / (ent["avg_ms"] * 1e-3) / 1e9
+        for cn in ("SQ_INSTS_VALU", "SQ_INSTS_MFMA", "SQ_INSTS_LDS", "SQ_WAVES", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES"):
+            k = (name, cn)
+            if k in sq:
+                ent[cn] = sum(sq[k]) / len(sq[k])
+        out["kernels"].append(ent)
+    (dst / f"{tag}_summary.json").write_text(json.dumps(out, indent=1))
+    lines = [f"# rocprofv3 summary `{tag}`", "",
+             f"bench under trace: {bench['value']:.4g} {bench['unit']}, {bench['ms_per_step']:.2f} ms/step", "",
+             "| kernel | calls | avg ms | % | HBM GB/launch (2*FETCH+WRITE) | HBM GB/s | VALU/wave | MFMA/wave | LDS/wave |",
+             "|---|---|---|---|---|---|---|---|---|"]
+    for e in out["kernels"]:
+        w = e.get("SQ_WAVES") or 0
+        per = lambda c: f"{e[c] / w:.0f}" if w and c in e else "-"
+        gb = f"{e['hbm_bytes_per_launch'] / 1e9:.3f}" if "hbm_bytes_per_launch" in e else "-"
+        gbs = f"{e['hbm_gbs']:.0f}" if "hbm_gbs" in e else "-"
+        lines.append(f"| {e['kernel']} | {e['calls']} | {e['avg_ms']:.3f} | {e['pct']:.2f} | {gb} | {gbs} | "
+                     f"{per('SQ_INSTS_VALU')} | {per('SQ_INSTS_MFMA')} | {per('SQ_INSTS_LDS')} |")
+    (dst / f"{tag}_summary.md").write_text("\n".join(lines) + "\n")
+    print("\n".join(lines))
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:])
