@@ -177,7 +177,6 @@ def main():
                           "bytes_per_eval": effective_bytes_per_eval(n_mean, args.k),
                           "note": "north-star streamed-panel accounting (SURVEY.md 8d); compulsory DRAM bytes are ~24 B/eval"},
         "kernel_ms": {"prep": st["prep_ms"] / max(st["prep_launches"], 1), "likelihood": avg_ms,
-                      "solve": st["solve_ms"] / max(st["solve_launches"], 1),
                       "reduce": st["reduce_ms"] / max(st["reduce_launches"], 1)},
         "checks_ok": ok,
     }

@@ -61,9 +61,8 @@ class Results(C.Structure):
 
 
 class Stats(C.Structure):
-    _fields_ = [("prep_ms", C.c_double), ("likelihood_ms", C.c_double), ("solve_ms", C.c_double),
-                ("reduce_ms", C.c_double), ("prep_launches", C.c_int64),
-                ("likelihood_launches", C.c_int64), ("solve_launches", C.c_int64),
+    _fields_ = [("prep_ms", C.c_double), ("likelihood_ms", C.c_double), ("reduce_ms", C.c_double),
+                ("prep_launches", C.c_int64), ("likelihood_launches", C.c_int64),
                 ("reduce_launches", C.c_int64), ("spectra", C.c_int64), ("sample_evals", C.c_int64)]
 
 

@@ -101,7 +101,7 @@ int grow(T** p, size_t* cap, size_t count) {
 
 struct TimedLaunch {
   hipEvent_t start, stop;
-  int kind;  // 0 prep, 1 likelihood, 2 reduce, 3 solve
+  int kind;  // 0 prep, 1 likelihood, 2 reduce
 };
 
 }  // namespace
@@ -123,7 +123,7 @@ struct gpdla_engine {
   int32_t* d_status = nullptr;
 
   // batch workspaces
-  size_t cap_meta = 0, cap_q = 0, cap_slots = 0, cap_lam = 0, cap_scr = 0, cap_sll = 0;
+  size_t cap_meta = 0, cap_q = 0, cap_slots = 0, cap_lam = 0, cap_sll = 0, cap_scr = 0;
   size_t cap_smap = 0, cap_wl = 0, cap_flux = 0, cap_noise = 0, cap_mask = 0, cap_z = 0;
   int64_t* d_meta = nullptr;  // [offsets(Q+1) | slot_base | lam_base | slot_cap]
   double *d_wl = nullptr, *d_flux = nullptr, *d_noise = nullptr;
@@ -165,7 +165,6 @@ int resolve_events(gpdla_engine* e) {
     if (t.kind == 0) { e->stats.prep_ms += ms; e->stats.prep_launches++; }
     if (t.kind == 1) { e->stats.likelihood_ms += ms; e->stats.likelihood_launches++; }
     if (t.kind == 2) { e->stats.reduce_ms += ms; e->stats.reduce_launches++; }
-    if (t.kind == 3) { e->stats.solve_ms += ms; e->stats.solve_launches++; }
     (void)hipEventDestroy(t.start);
     (void)hipEventDestroy(t.stop);
   }
@@ -364,8 +363,8 @@ int gpdla_engine_process(gpdla_engine* e, const gpdla_spectra* sp, const gpdla_r
     if ((rc = grow(&e->d_info, &e->cap_q, (size_t)QB))) return rc;
     if ((rc = grow(&e->d_panel, &e->cap_slots, (size_t)slots * row))) return rc;
     if ((rc = grow(&e->d_lam, &e->cap_lam, (size_t)lams))) return rc;
-    if ((rc = grow(&e->d_smap, &e->cap_smap, (size_t)slots))) return rc;
     if ((rc = grow(&e->d_scratch, &e->cap_scr, (size_t)blocks_x * nq * kSamplesPerBlock * es))) return rc;
+    if ((rc = grow(&e->d_smap, &e->cap_smap, (size_t)slots))) return rc;
     HIP_TRY(hipMemcpyAsync(e->d_meta, hm, per_batch * sizeof(int64_t), hipMemcpyHostToDevice, st));
 
     const double *wl, *fl, *nv, *zq;
@@ -445,11 +444,7 @@ int gpdla_engine_process(gpdla_engine* e, const gpdla_spectra* sp, const gpdla_r
     la.num_lines = e->params.num_lines;
     la.lines = make_line_args(e->d_lines);
     la.scratch = e->d_scratch;
-    la.status = e->d_status;
-
-    SolveArgs sa{};
-    sa.q_count = (int32_t)nq; sa.info = e->d_info; sa.scratch = e->d_scratch; sa.S = e->S;
-    sa.sample_ll = o_sll; sa.ld = ld; sa.ll_null = o_null; sa.status = e->d_status;
+    la.sample_ll = o_sll; la.ld = ld; la.ll_null = o_null; la.status = e->d_status;
 
     ReduceArgs ra{};
     ra.q_count = (int32_t)nq; ra.info = e->d_info; ra.sample_ll = o_sll; ra.ld = ld; ra.S = e->S;
@@ -464,11 +459,7 @@ int gpdla_engine_process(gpdla_engine* e, const gpdla_spectra* sp, const gpdla_r
     HIP_TRY(launch_likelihood(e->K, la, st));
     HIP_TRY(hipEventRecord(t1.stop, st));
     e->pending.push_back(t1);
-    TimedLaunch t3{};
-    if ((rc = record_start(e, &t3, 3))) return rc;
-    HIP_TRY(launch_solve(e->K, sa, blocks_x, st));
-    HIP_TRY(hipEventRecord(t3.stop, st));
-    e->pending.push_back(t3);
+
     if ((rc = record_start(e, &t2, 2))) return rc;
     HIP_TRY(launch_reduce(ra, st));
     HIP_TRY(hipEventRecord(t2.stop, st));
@@ -492,7 +483,7 @@ int gpdla_engine_process(gpdla_engine* e, const gpdla_spectra* sp, const gpdla_r
       // host inputs were staged in reusable workspaces
       HIP_TRY(hipStreamSynchronize(st));
     }
-    // otherwise the next batch reuses panel / scratch workspaces in stream order
+    // otherwise the next batch reuses the panel workspace in stream order
   }
   HIP_TRY(hipEventRecord(e->meta_done, st));
   if (!out_dev) return gpdla_engine_synchronize(e);

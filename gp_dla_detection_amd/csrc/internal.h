@@ -36,7 +36,7 @@ struct Layout {
   static constexpr int kTiles = kGT + kUT;
   static constexpr int kJS = ((kTiles + 2) + 1) & ~1;  // per-j stride (doubles), even
   static constexpr int kRow = 4 * kJS;                 // doubles per slot row
-  static constexpr int kES = 4 * kTiles + 8;           // scratch doubles per sample
+  static constexpr int kES = 4 * kTiles + 8;           // epilogue doubles per sample (Gram, u, scalars)
   // slot scalars in the spare words
   static constexpr int kLam = 0 * kJS + kTiles;        // padded wavelength at slot + 6
   static constexpr int kY = 0 * kJS + kTiles + 1;
@@ -116,15 +116,7 @@ struct LikelihoodArgs {
   int64_t S;
   int32_t num_lines;
   LineArgs lines;
-  double* scratch;               // [grid blocks][64][kES]
-  int32_t* status;
-};
-
-struct SolveArgs {
-  int32_t q_count;
-  const SpecInfo* info;
-  const double* scratch;
-  int64_t S;
+  double* scratch;               // [grid blocks][64][kES]: epilogue transpose tiles
   double* sample_ll;             // [q_count][ld] or nullptr
   int64_t ld;
   double* ll_null;               // [q_count]
@@ -145,7 +137,6 @@ struct ReduceArgs {
 
 hipError_t launch_prep(int K, const PrepArgs& a, hipStream_t s);
 hipError_t launch_likelihood(int K, const LikelihoodArgs& a, hipStream_t s);
-hipError_t launch_solve(int K, const SolveArgs& a, int64_t blocks_x, hipStream_t s);
 hipError_t launch_reduce(const ReduceArgs& a, hipStream_t s);
 hipError_t launch_voigt_batch(const double* lambdas, int64_t n_padded, const double* z,
                               const double* N, int64_t count, int32_t num_lines,

@@ -344,13 +344,88 @@ __global__ __launch_bounds__(256) void prep_kernel(PrepArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------------
+// Per-sample augmented LDL^T in registers, one quad of lanes per sample.
+//   srow (Layout<K>::kES doubles): Gram entries (r, c), r <= c, at gram_index(r, c); u_i at
+//   4*kGT + i; sum r^2/d, prod-d mantissa and exponent at 4*kTiles + {0,1,2}.
+//   Lane jq owns Gram columns c = 4jj + jq (rows 0..4jj+3) and u rows i = 4m + jq; pivot rows are
+//   broadcast inside the quad with DPP.  [B u; u' q1] with B = I + M'D^-1 M
+//   (log_mvnpdf_low_rank.m:22-24) is factored as L D L': log det B = sum log D_p and
+//   r'K^-1 r = q1 - u'B^-1 u is the last pivot (log_mvnpdf_low_rank.m:26-32).
+// ---------------------------------------------------------------------------------------------
+template <int K>
+__device__ inline double ldl_log_likelihood(const double* srow, int jq, int n, bool& bad_out) {
+  using Lay = Layout<K>;
+  constexpr int kTiles = Lay::kTiles;
+  constexpr int kGT = Lay::kGT;
+  constexpr int NJJ = (K + 3) / 4;
+  double A[NJJ][4 * NJJ];
+  double U[NJJ];
+#pragma unroll
+  for (int jj = 0; jj < NJJ; ++jj) {
+    const int c = 4 * jj + jq;
+#pragma unroll
+    for (int i = 0; i < 4 * jj + 4; ++i) {
+      double v = 0.0;
+      if (i <= c && c < K) {
+        v = srow[gram_index<K>(i, c)];
+        if (i == c) v += 1.0;  // B = I + M' D^-1 M (log_mvnpdf_low_rank.m:23)
+      }
+      A[jj][i] = v;
+    }
+    U[jj] = (c < K) ? srow[4 * kGT + c] : 0.0;
+  }
+  double quad = srow[4 * kTiles];
+  const double dm = srow[4 * kTiles + 1];
+  const double de = srow[4 * kTiles + 2];
+  double pb = 1.0;
+  int eb = 0;
+  bool bad = false;
+#pragma unroll
+  for (int p = 0; p < K; ++p) {
+    const double Dp = quad_bcast(A[p >> 2][p], p & 3);
+    bad |= !(Dp > 0.0) || !(Dp < INFINITY);
+    const double invD = 1.0 / Dp;
+    pb *= Dp;
+    if ((p & 3) == 3) {
+      int ex;
+      pb = frexp(pb, &ex);
+      eb += ex;
+    }
+    const double up = quad_bcast(U[p >> 2], p & 3);
+    const double upinv = up * invD;
+    double rowp[K];
+#pragma unroll
+    for (int i = p + 1; i < K; ++i) rowp[i] = quad_bcast(A[i >> 2][p], i & 3);
+#pragma unroll
+    for (int jj = p >> 2; jj < NJJ; ++jj) {
+      const double sc = A[jj][p] * invD;
+#pragma unroll
+      for (int i = p + 1; i < 4 * jj + 4 && i < K; ++i) A[jj][i] = fma(-rowp[i], sc, A[jj][i]);
+    }
+#pragma unroll
+    for (int mm = 0; mm < NJJ; ++mm) {
+      if (4 * mm + 3 > p) {
+        const bool cnd = (4 * mm + jq) > p;
+        U[mm] = cnd ? fma(-A[mm][p], upinv, U[mm]) : U[mm];
+      }
+    }
+    quad = fma(-up, upinv, quad);
+  }
+  const double logdet_b = log(pb) + eb * kLn2;
+  const double logdet_d = log(dm) + de * kLn2;
+  const double ll = -0.5 * (quad + (logdet_d + logdet_b) + n * kLog2Pi);  // log_mvnpdf_low_rank.m:30-32
+  bad_out = bad || !(fabs(ll) < INFINITY);
+  return bad_out ? NAN : ll;
+}
+
+// ---------------------------------------------------------------------------------------------
 // likelihood: for one spectrum (blockIdx.y) and 64 samples (4 waves x 16), sweep all slots:
 //   per lane (sample s = lane & 15, segment g = lane >> 4): Voigt raw profile at the leading
 //   padded wavelength, 7-tap convolution from a register window, DLA-modulated pixel terms
 //   a^2/d and a r/d (process_qsos.m:189-197), then v_mfma_f64_4x4x4_4b over the Khatri-Rao
 //   tiles (Gram + u).  Panel rows are staged chunk by chunk into a double-buffered LDS ring by
-//   global_load_lds (the next chunk's DMA overlaps this chunk's compute).  The epilogue writes the
-//   per-sample Gram / u / scalars to `scratch` for solve_kernel.
+//   global_load_lds (the next chunk's DMA overlaps this chunk's compute).  The epilogue transposes
+//   the accumulators through a block-private scratch tile and runs the per-sample augmented LDL^T.
 // ---------------------------------------------------------------------------------------------
 template <int K>
 __device__ inline void stage_chunk(const double* __restrict__ panel, int L, int c, double* buf,
@@ -369,14 +444,17 @@ __device__ inline void stage_chunk(const double* __restrict__ panel, int L, int 
       // hipcc does not make the other buffer's ds_reads wait on it; the consumer side waits with
       // an explicit s_waitcnt vmcnt(0) + barrier at the end of the chunk.
       const uint32_t dst = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)(buf + i * 128);
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
       asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, off"
                    :: "s"(__builtin_amdgcn_readfirstlane(dst)), "v"(src) : "memory", "m0");
+#pragma clang diagnostic pop
     }
   }
 }
 
 template <int K, int NL>
-__global__ __launch_bounds__(256, 2) void likelihood_kernel(LikelihoodArgs a) {
+__global__ __launch_bounds__(256, (K <= 20 ? 2 : 1)) void likelihood_kernel(LikelihoodArgs a) {
   using Lay = Layout<K>;
   constexpr int kTiles = Lay::kTiles;
   constexpr int kGT = Lay::kGT;
@@ -389,10 +467,14 @@ __global__ __launch_bounds__(256, 2) void likelihood_kernel(LikelihoodArgs a) {
 
   const int q = blockIdx.y;
   const SpecInfo inf = a.info[q];
-  if (inf.J == 0) return;  // unusable spectrum: solve_kernel writes NaN
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int64_t block_lin = (int64_t)blockIdx.y * gridDim.x + blockIdx.x;
   const int64_t s_base = (int64_t)blockIdx.x * kSamplesPerBlock + wave * kSamplesPerWave;
+  if (inf.J == 0) {  // unusable spectrum (no unmasked in-range pixel): NaN outputs
+    const int64_t su = s_base + (lane >> 2);
+    if ((lane & 3) == 0 && su < a.S && a.sample_ll) a.sample_ll[q * a.ld + su] = NAN;
+    if ((lane & 3) == 0 && su == a.S) a.ll_null[q] = NAN;
+    return;
+  }
   const int L = inf.L;
   const int nchunks = (L + kChunkSteps - 1) / kChunkSteps;
   const double* panel = a.panel + inf.slot_base * kRow;
@@ -510,107 +592,31 @@ __global__ __launch_bounds__(256, 2) void likelihood_kernel(LikelihoodArgs a) {
     pe += pe2 + ex;
   }
 
-  // ---- epilogue: accumulators -> scratch (sample-major); D lane map of 4x4x4_4b:
-  //      sample 4*((lane>>2)&3) + (lane>>4), entry 4t + (lane&3)
-  double* scr = a.scratch + (block_lin * kSamplesPerBlock + wave * kSamplesPerWave) * Lay::kES;
-  const int sd = 4 * ((lane >> 2) & 3) + (lane >> 4);
-  double* dst = scr + sd * Lay::kES + (lane & 3);
+  // ---- epilogue: accumulators -> this block's private scratch tile (sample-major; read straight
+  //      back from L2 after the barrier, which frees the accumulator registers), then the
+  //      augmented LDL^T per sample in registers (a quad of lanes each).
+  //      D lane map of 4x4x4_4b: sample 4*((lane>>2)&3) + (lane>>4), entry 4t + (lane&3).
+  double* scr = a.scratch + (((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * kSamplesPerBlock +
+                             wave * kSamplesPerWave) * Lay::kES;
+  {
+    const int sd = 4 * ((lane >> 2) & 3) + (lane >> 4);
+    double* dst = scr + sd * Lay::kES + (lane & 3);
 #pragma unroll
-  for (int t = 0; t < kTiles; ++t) dst[4 * t] = acc[t];
-  if (lane < 16) {
-    double* sc = scr + lane * Lay::kES + 4 * kTiles;
-    sc[0] = q1;
-    sc[1] = pm;
-    sc[2] = (double)pe;
+    for (int t = 0; t < kTiles; ++t) dst[4 * t] = acc[t];
+    if (lane < 16) {
+      double* sc = scr + lane * Lay::kES + 4 * kTiles;
+      sc[0] = q1;
+      sc[1] = pm;
+      sc[2] = (double)pe;
+    }
   }
-}
-
-// ---------------------------------------------------------------------------------------------
-// solve: per-sample augmented LDL^T, one quad of lanes per sample (the wave's 16 samples).
-//   Lane jq owns Gram columns c = 4jj + jq (rows 0..4jj+3) and u rows i = 4m + jq; pivot rows
-//   are broadcast inside the quad with DPP.  B = I + M'D^-1 M (log_mvnpdf_low_rank.m:22-24),
-//   [B u; u' q1] = L D L' gives log det B = sum log D_p and r'K^-1 r = the last pivot
-//   (log_mvnpdf_low_rank.m:26-32).
-// ---------------------------------------------------------------------------------------------
-template <int K>
-__global__ __launch_bounds__(256) void solve_kernel(SolveArgs a) {
-  using Lay = Layout<K>;
-  constexpr int kTiles = Lay::kTiles;
-  constexpr int kGT = Lay::kGT;
-  constexpr int NJJ = (K + 3) / 4;
-  const int q = blockIdx.y;
-  const SpecInfo inf = a.info[q];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  __syncthreads();
   const int jq = lane & 3, sq = lane >> 2;
-  const int64_t block_lin = (int64_t)blockIdx.y * gridDim.x + blockIdx.x;
-  const int64_t s2 = (int64_t)blockIdx.x * kSamplesPerBlock + wave * kSamplesPerWave + sq;
-  if (inf.J == 0) {
-    if (jq == 0 && s2 < a.S && a.sample_ll) a.sample_ll[q * a.ld + s2] = NAN;
-    if (jq == 0 && s2 == a.S) a.ll_null[q] = NAN;
-    return;
-  }
-  const double* srow = a.scratch + ((block_lin * kSamplesPerBlock) + wave * kSamplesPerWave + sq) * Lay::kES;
-  double A[NJJ][4 * NJJ];
-  double U[NJJ];
-#pragma unroll
-  for (int jj = 0; jj < NJJ; ++jj) {
-    const int c = 4 * jj + jq;
-#pragma unroll
-    for (int i = 0; i < 4 * jj + 4; ++i) {
-      double v = 0.0;
-      if (i <= c && c < K) {
-        v = srow[gram_index<K>(i, c)];
-        if (i == c) v += 1.0;  // B = I + M' D^-1 M (log_mvnpdf_low_rank.m:23)
-      }
-      A[jj][i] = v;
-    }
-    U[jj] = (c < K) ? srow[4 * kGT + c] : 0.0;
-  }
-  double quad = srow[4 * kTiles];
-  const double dm = srow[4 * kTiles + 1];
-  const double de = srow[4 * kTiles + 2];
-  double pb = 1.0;
-  int eb = 0;
-  bool bad = false;
-#pragma unroll
-  for (int p = 0; p < K; ++p) {
-    const double Dp = quad_bcast(A[p >> 2][p], p & 3);
-    bad |= !(Dp > 0.0) || !(Dp < INFINITY);
-    const double invD = 1.0 / Dp;
-    pb *= Dp;
-    if ((p & 3) == 3) {
-      int ex;
-      pb = frexp(pb, &ex);
-      eb += ex;
-    }
-    const double up = quad_bcast(U[p >> 2], p & 3);
-    const double upinv = up * invD;
-    double rowp[K];
-#pragma unroll
-    for (int i = p + 1; i < K; ++i) rowp[i] = quad_bcast(A[i >> 2][p], i & 3);
-#pragma unroll
-    for (int jj = p >> 2; jj < NJJ; ++jj) {
-      const double sc = A[jj][p] * invD;
-#pragma unroll
-      for (int i = p + 1; i < 4 * jj + 4 && i < K; ++i) A[jj][i] = fma(-rowp[i], sc, A[jj][i]);
-    }
-#pragma unroll
-    for (int mm = 0; mm < NJJ; ++mm) {
-      if (4 * mm + 3 > p) {
-        const bool cnd = (4 * mm + jq) > p;
-        U[mm] = cnd ? fma(-A[mm][p], upinv, U[mm]) : U[mm];
-      }
-    }
-    quad = fma(-up, upinv, quad);
-  }
+  const int64_t s2 = s_base + sq;
+  bool bad;
+  const double ll = ldl_log_likelihood<K>(scr + sq * Lay::kES, jq, inf.n, bad);
   if (jq == 0 && s2 <= a.S) {
-    const double logdet_b = log(pb) + eb * kLn2;
-    const double logdet_d = log(dm) + de * kLn2;
-    double ll = -0.5 * (quad + (logdet_d + logdet_b) + inf.n * kLog2Pi);  // log_mvnpdf_low_rank.m:30-32
-    if (bad || !(fabs(ll) < INFINITY)) {
-      ll = NAN;
-      atomicOr(a.status, 1);
-    }
+    if (bad) atomicOr(a.status, 1);
     if (s2 == a.S) a.ll_null[q] = ll;
     else if (a.sample_ll) a.sample_ll[q * a.ld + s2] = ll;
   }
@@ -766,11 +772,7 @@ hipError_t launch_likelihood_k(const LikelihoodArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-template <int K>
-hipError_t launch_solve_k(const SolveArgs& a, int64_t blocks_x, hipStream_t s) {
-  hipLaunchKernelGGL(solve_kernel<K>, dim3((unsigned)blocks_x, a.q_count), dim3(256), 0, s, a);
-  return hipGetLastError();
-}
+
 
 }  // namespace
 
@@ -783,15 +785,15 @@ bool rank_supported(int K) {
   return false;
 }
 
-int panel_row_doubles(int K) {
-#define X(k) if (K == k) return Layout<k>::kRow;
+int scratch_doubles(int K) {
+#define X(k) if (K == k) return Layout<k>::kES;
   GPDLA_FOR_EACH_RANK(X)
 #undef X
   return 0;
 }
 
-int scratch_doubles(int K) {
-#define X(k) if (K == k) return Layout<k>::kES;
+int panel_row_doubles(int K) {
+#define X(k) if (K == k) return Layout<k>::kRow;
   GPDLA_FOR_EACH_RANK(X)
 #undef X
   return 0;
@@ -806,13 +808,6 @@ hipError_t launch_prep(int K, const PrepArgs& a, hipStream_t s) {
 
 hipError_t launch_likelihood(int K, const LikelihoodArgs& a, hipStream_t s) {
 #define X(k) if (K == k) return launch_likelihood_k<k>(a, s);
-  GPDLA_FOR_EACH_RANK(X)
-#undef X
-  return hipErrorInvalidValue;
-}
-
-hipError_t launch_solve(int K, const SolveArgs& a, int64_t blocks_x, hipStream_t s) {
-#define X(k) if (K == k) return launch_solve_k<k>(a, blocks_x, s);
   GPDLA_FOR_EACH_RANK(X)
 #undef X
   return hipErrorInvalidValue;

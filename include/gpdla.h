@@ -106,8 +106,8 @@ typedef struct gpdla_results {
 
 /* Kernel-time accounting (HIP events on the engine's stream), cumulative since create/reset. */
 typedef struct gpdla_stats {
-  double prep_ms, likelihood_ms, solve_ms, reduce_ms;
-  int64_t prep_launches, likelihood_launches, solve_launches, reduce_launches;
+  double prep_ms, likelihood_ms, reduce_ms;
+  int64_t prep_launches, likelihood_launches, reduce_launches;
   int64_t spectra, sample_evals;       /* sample_evals = sum over spectra of S (null evals excluded) */
 } gpdla_stats;
 

@@ -209,7 +209,7 @@ def test_device_path_equals_host_path():
     np.testing.assert_array_equal(o_null.numpy(), host["log_likelihoods_no_dla"])
     np.testing.assert_array_equal(o_dla.numpy(), host["log_likelihoods_dla"])
     np.testing.assert_array_equal(o_s.numpy(), host["sample_log_likelihoods_dla"])
-    assert st["likelihood_launches"] == 2 and st["likelihood_ms"] > 0 and st["solve_launches"] == 2
+    assert st["likelihood_launches"] == 2 and st["likelihood_ms"] > 0
 
 
 TORCH_INTEROP = r"""
