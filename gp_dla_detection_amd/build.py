@@ -12,21 +12,25 @@ SOURCES = ["kernels.hip", "engine.hip", "faddeeva_host.cpp"]
 OUT = PKG / "libgpdla.so"
 
 
-def build(verbose: bool = False, force: bool = False) -> Path:
+def build(verbose: bool = False, force: bool = False, out: Path | None = None,
+          defines: dict | None = None) -> Path:
+    """Compile libgpdla.so (or a variant with -D``defines`` into ``out``, for A/B experiments)."""
+    OUT_ = Path(out) if out else OUT
     srcs = [CSRC / s for s in SOURCES]
     deps = srcs + list(CSRC.glob("*.h")) + [PKG.parent / "include" / "gpdla.h"]
-    if OUT.exists() and not force and all(OUT.stat().st_mtime >= d.stat().st_mtime for d in deps):
-        return OUT
+    if OUT_.exists() and not force and not defines and all(OUT_.stat().st_mtime >= d.stat().st_mtime for d in deps):
+        return OUT_
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     cmd = [hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-Wno-unused-result", "-o", str(OUT)] + [str(s) for s in srcs]
+           "-Wno-unused-result", "-o", str(OUT_)] + [f"-D{k}={v}" for k, v in (defines or {}).items()] \
+        + [str(s) for s in srcs]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
-    tmp = OUT.with_suffix(".so.tmp")
+    tmp = OUT_.with_suffix(".so.tmp")
     cmd[cmd.index("-o") + 1] = str(tmp)
     subprocess.run(cmd, check=True, cwd=CSRC)
-    tmp.replace(OUT)
-    return OUT
+    tmp.replace(OUT_)
+    return OUT_
 
 
 if __name__ == "__main__":

@@ -42,7 +42,6 @@ int set_error(int code, const char* fmt, ...) {
 // ---- line-profile data (fitted once per process on the host; layout in internal.h)
 struct HostLineData {
   std::vector<double> buf;
-  WingPoly wing;
 };
 
 const HostLineData& host_line_data() {
@@ -50,29 +49,24 @@ const HostLineData& host_line_data() {
   static std::once_flag once;
   std::call_once(once, [] {
     d.buf.assign(kLineBufDoubles, 0.0);
-    for (int j = 0; j < kMaxLines; ++j) fit_core_table(j, d.buf.data() + (size_t)j * kCoreTable);
+    for (int j = 0; j < kMaxLines; ++j) {
+      fit_core_table(j, d.buf.data() + (size_t)j * kCoreTable);
+      fit_wing_line(j, d.buf.data() + kLineBufWing + (size_t)j * kWingStride);
+    }
     for (int j = 0; j < kMaxLines; ++j) {
       // fac_j = c / (lambda_j 1e8) / (sigma sqrt 2): x_j = lambda fac_j / (1+z) - c / (sigma sqrt 2)
       const long double f = (long double)kCcgs / ((long double)kTransitionWavelengths[j] * 1e8L) /
                             ((long double)kSigma * std::sqrt(2.0L));
       d.buf[kLineBufFac + j] = (double)f;
-      line_wing_constants(j, &d.buf[kLineBufA + j], &d.buf[kLineBufB + j]);
     }
-    fit_wing(&d.wing);
+    for (int j = 0; j < 64; ++j) d.buf[kLineBufExp2 + j] = (double)std::exp2((long double)j / 64.0L);
   });
   return d;
 }
 
 LineArgs make_line_args(const double* d_buf) {
-  const HostLineData& h = host_line_data();
   LineArgs l{};
   l.buf = d_buf;
-  l.wing = h.wing;
-  for (int j = 0; j < 3; ++j) {
-    l.fac3[j] = h.buf[kLineBufFac + j];
-    l.A3[j] = h.buf[kLineBufA + j];
-    l.B3[j] = h.buf[kLineBufB + j];
-  }
   return l;
 }
 

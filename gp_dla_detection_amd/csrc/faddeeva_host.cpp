@@ -134,15 +134,6 @@ std::vector<long double> cheb_fit_monomial(const std::vector<long double>& fvals
 
 }  // namespace
 
-// Per-line wing constants: f_j = A_j T (g + B_j T h) for |x| >= kCoreX.
-void line_wing_constants(int j, double* A, double* B) {
-  const long double sig = (long double)kSigma;
-  const long double y = (long double)kLorentzGammas[j] / (sig * std::sqrt(2.0L));
-  const long double scale = (long double)kLeadingConstants[j] / (sig * std::sqrt(2.0L * kPiL));
-  *A = (double)(scale * y);
-  *B = (double)(y * y);
-}
-
 namespace {
 
 // (a T + b)^n expansion of a polynomial given in s = a T + b (monomials), -> powers of T
@@ -159,38 +150,35 @@ std::vector<long double> shift_to_T(const std::vector<long double>& mono_s, long
   return t;
 }
 
-// G(T; y) = Re w(1/sqrt(T) + i y) / (y T)
-long double wing_G(long double T, long double y) {
-  const long double x = 1.0L / std::sqrt(T);
-  return faddeeva_w(x, y).real() / (y * T);
+// Line j's profile scale lc_j / (sigma sqrt(2 pi)) and damping y_j = gamma_j / (sigma sqrt 2).
+void line_scale(int j, long double* scale, long double* y) {
+  const long double sig = (long double)kSigma;
+  *y = (long double)kLorentzGammas[j] / (sig * std::sqrt(2.0L));
+  *scale = (long double)kLeadingConstants[j] / (sig * std::sqrt(2.0L * kPiL));
 }
 
 }  // namespace
 
-// Universal damping-wing polynomials g, h on T in (0, 1/kCoreX^2]:  G(T; y) = g(T) + y^2 T h(T) + O(y^4 T^2).
-// Richardson in y^2 at y1, y2 = 2 y1 separates g and h.
-void fit_wing(WingPoly* w) {
+// Wing polynomial of line j: f_j(x) x^2 = sum_n wing[n] T^n on T = 1/x^2 in (0, 1/kCoreX^2]
+// (Chebyshev interpolation at kWingDeg + 1 first-kind nodes, then monomials in T).
+void fit_wing_line(int j, double* wing) {
+  long double scale, y;
+  line_scale(j, &scale, &y);
   const long double Tmax = 1.0L / ((long double)kCoreX * kCoreX);
-  const long double y1 = 1e-3L, y2 = 2e-3L;
-  for (int pass = 0; pass < 2; ++pass) {
-    const int NW = pass == 0 ? kWingG : kWingH;
-    std::vector<long double> v(NW);
-    for (int k = 0; k < NW; ++k) {
-      const long double s = std::cos(kPiL * (k + 0.5L) / NW);
-      const long double T = Tmax * (s + 1.0L) / 2.0L;
-      const long double G1 = wing_G(T, y1), G2 = wing_G(T, y2);
-      v[k] = pass == 0 ? (4.0L * G1 - G2) / 3.0L : (G2 - G1) / (3.0L * y1 * y1 * T);
-    }
-    std::vector<long double> t = shift_to_T(cheb_fit_monomial(v), 2.0L / Tmax, -1.0L);
-    for (int n = 0; n < NW; ++n) (pass == 0 ? w->g : w->h)[n] = (double)t[n];
+  const int N = kWingDeg + 1;
+  std::vector<long double> fv(N);
+  for (int k = 0; k < N; ++k) {
+    const long double T = Tmax * (std::cos(kPiL * (k + 0.5L) / N) + 1.0L) / 2.0L;
+    fv[k] = scale * faddeeva_w(1.0L / std::sqrt(T), y).real() / T;
   }
+  const std::vector<long double> t = shift_to_T(cheb_fit_monomial(fv), 2.0L / Tmax, -1.0L);
+  for (int n = 0; n < kWingStride; ++n) wing[n] = n < N ? (double)t[n] : 0.0;
 }
 
 // Core table of line j (kPieces x kCoreStride, polynomial in u = |x| - centre).
 void fit_core_table(int j, double* core) {
-  const long double sig = (long double)kSigma;
-  const long double y = (long double)kLorentzGammas[j] / (sig * std::sqrt(2.0L));
-  const long double scale = (long double)kLeadingConstants[j] / (sig * std::sqrt(2.0L * kPiL));
+  long double scale, y;
+  line_scale(j, &scale, &y);
   const int N = kCoreDeg + 1;
   for (int p = 0; p < kPieces; ++p) {
     const long double centre = (p + 0.5L) * kPieceW, half = 0.5L * kPieceW;
@@ -209,19 +197,15 @@ void fit_core_table(int j, double* core) {
 // Max relative error of the double-precision line profile of line j against the long-double
 // source on a dense grid (core: 36k points, wing: geometric out to |x| = 2e6).
 double line_profile_error(int j) {
-  std::vector<double> core(kCoreTable);
+  std::vector<double> core(kCoreTable), wing(kWingStride);
   fit_core_table(j, core.data());
-  WingPoly w;
-  fit_wing(&w);
-  double A, B;
-  line_wing_constants(j, &A, &B);
-  const long double sig = (long double)kSigma;
-  const long double y = (long double)kLorentzGammas[j] / (sig * std::sqrt(2.0L));
-  const long double scale = (long double)kLeadingConstants[j] / (sig * std::sqrt(2.0L * kPiL));
+  fit_wing_line(j, wing.data());
+  long double scale, y;
+  line_scale(j, &scale, &y);
   double maxrel = 0;
   for (int i = 0; i <= 48000; ++i) {
     const double x = (i < 36000) ? i * (kCoreX / 36000.0) : kCoreX * std::pow(1.0004, i - 36000);
-    const double got = line_profile_eval(core.data(), w, A, B, x);
+    const double got = line_profile_eval(core.data(), wing.data(), x);
     const long double ref = scale * faddeeva_w((long double)x, y).real();
     const double rel = (double)std::fabs((got - ref) / ref);
     if (rel > maxrel) maxrel = rel;

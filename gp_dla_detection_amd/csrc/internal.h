@@ -92,18 +92,17 @@ struct PrepArgs {
 };
 
 // Line-profile data.  Device buffer layout (doubles):
-//   [kMaxLines][kCoreTable] core tables | fac[kMaxLines] | A[kMaxLines] | B[kMaxLines]
+//   [kMaxLines][kCoreTable] core tables | [kMaxLines][kWingStride] wing polynomials |
+//   fac[kMaxLines] | 2^(j/64)[64]
 // fac_j = c / (lambda_j 1e8) / (sigma sqrt 2), so x_j = lambda * fac_j / (1 + z) - c / (sigma sqrt 2)
 // (voigt.c:278-279,287 divided by sigma sqrt 2).
-constexpr size_t kLineBufFac = (size_t)kMaxLines * kCoreTable;
-constexpr size_t kLineBufA = kLineBufFac + kMaxLines;
-constexpr size_t kLineBufB = kLineBufA + kMaxLines;
-constexpr size_t kLineBufDoubles = kLineBufB + kMaxLines;
+constexpr size_t kLineBufWing = (size_t)kMaxLines * kCoreTable;
+constexpr size_t kLineBufFac = kLineBufWing + (size_t)kMaxLines * kWingStride;
+constexpr size_t kLineBufExp2 = kLineBufFac + kMaxLines;  // 2^(j/64), j = 0..63 (exp_tab64)
+constexpr size_t kLineBufDoubles = kLineBufExp2 + 64;
 
 struct LineArgs {
   const double* buf;   // device line buffer (layout above)
-  WingPoly wing;       // universal damping-wing polynomials (SGPR-resident)
-  double fac3[3], A3[3], B3[3];  // Lyman alpha, beta, gamma: the 3-line fast path
 };
 
 struct LikelihoodArgs {
@@ -150,8 +149,7 @@ int scratch_doubles(int K);
 
 // host-side table fitting (faddeeva_host.cpp)
 void fit_core_table(int line, double* core);
-void fit_wing(WingPoly* w);
-void line_wing_constants(int line, double* A, double* B);
+void fit_wing_line(int line, double* wing);
 double line_profile_error(int line);
 
 }  // namespace gpdla

@@ -10,6 +10,17 @@
 
 #include "internal.h"
 
+// Build-time variant switches (A/B experiments; defaults are the shipped configuration).
+#ifndef GPDLA_WAVES_PER_EU
+#define GPDLA_WAVES_PER_EU 2
+#endif
+#ifndef GPDLA_SCHED_FENCE
+#define GPDLA_SCHED_FENCE 1
+#endif
+#ifndef GPDLA_FAST_EXP
+#define GPDLA_FAST_EXP 1
+#endif
+
 namespace gpdla {
 
 namespace {
@@ -27,6 +38,26 @@ __device__ inline double rcp_nr(double d) {
   r = fma(r, e, r);
   e = fma(-d, r, 1.0);
   return fma(r, e, r);
+}
+
+// exp(v) for v <= 0 (v = N * total, voigt.c:291): v = (64 m + j) ln2/64 + r, |r| <= ln2/128,
+// exp(v) = 2^m * 2^(j/64) * e^r with 2^(j/64) from a 64-entry LDS table (host-rounded from long
+// double) and e^r a degree-5 Taylor polynomial (truncation < 4e-17).  Underflows to +0 like exp.
+__device__ inline double exp_tab64(double v, const double* __restrict__ tab) {
+  constexpr double kInvL = 92.33248261689366;              // 64 / ln 2
+  constexpr double kLhi = 0.010830424695086549;           // ln2/64 to 33 bits (k*kLhi exact)
+  constexpr double kLlo = 1.162596423439437e-12;           // ln2/64 - kLhi
+  v = fmax(v, -1100.0);                                    // keeps k in int range; exp(-1100) = 0
+  const double k = __builtin_rint(v * kInvL);
+  double r = fma(-k, kLhi, v);
+  r = fma(-k, kLlo, r);
+  double p = fma(r, 1.0 / 120.0, 1.0 / 24.0);
+  p = fma(p, r, 1.0 / 6.0);
+  p = fma(p, r, 0.5);
+  p = fma(p, r, 1.0);
+  p = fma(p, r, 1.0);
+  const int ki = (int)k;
+  return __builtin_ldexp(p * tab[ki & 63], ki >> 6);
 }
 
 template <int SRC>
@@ -154,27 +185,33 @@ __device__ inline double raw_profile(double lam, double zfac, double N, int num_
   double total = 0.0;
   for (int j = 0; j < num_lines; ++j) {
     const double x = fma(lam, L.buf[kLineBufFac + j] * zfac, -kC2);
-    total -= line_profile_eval(L.buf + (size_t)j * kCoreTable, L.wing, L.buf[kLineBufA + j],
-                               L.buf[kLineBufB + j], x);
+    total -= line_profile_eval(L.buf + (size_t)j * kCoreTable,
+                               L.buf + kLineBufWing + (size_t)j * kWingStride, x);
   }
   return exp(N * total);
 }
 
 // 3-line fast path (Lyman alpha, beta, gamma; set_parameters.m:63): the damping wing is
-// evaluated branch-free for every lane, the core polynomial (LDS tables) only by the rare
-// lanes with |x| < kCoreX.
+// evaluated branch-free for every lane with its coefficients read from LDS by broadcast
+// (wing_lds), the core polynomial (LDS tables) only by the lanes with |x| < kCoreX.
 __device__ inline double raw_profile3(double lam, const double (&afac)[3], double N,
-                                      const double* __restrict__ core_lds, const LineArgs& L) {
+                                      const double* __restrict__ core_lds,
+                                      const double* __restrict__ wing_lds,
+                                      const double* __restrict__ exp_lds) {
   double total = 0.0;
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
     const double x = fma(lam, afac[j], -kC2);
     const double ax = fabs(x);
-    double f = wing_eval(L.wing, L.A3[j], L.B3[j], x);
+    double f = wing_eval(wing_lds + j * kWingStride, x);
     if (ax < kCoreX) f = core_eval(core_lds + j * kCoreTable, ax);
     total -= f;
   }
+#if GPDLA_FAST_EXP
+  return exp_tab64(N * total, exp_lds);
+#else
   return exp(N * total);
+#endif
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -282,10 +319,15 @@ __global__ __launch_bounds__(256) void prep_kernel(PrepArgs a) {
   const int lane = tid & 63, wave = tid >> 6;
   const double* rest_g = a.rest;
   const int G = a.num_rest;
+  // Slot j holds segment gg = j / Ls, step t = j % Ls, i.e. pixel-order position gg L + t; the
+  // steps t >= L that round each segment up to whole chunks are neutral rows (like masked pixels).
+  const int Ls = L > 0 ? ((L + kChunkSteps - 1) / kChunkSteps) * kChunkSteps : kChunkSteps;
   for (int64_t j = wave; j < cap; j += 4) {
     double* row = a.panel + (sb + j) * Lay::kRow;
-    const int pix = (j < J) ? smap[j] : -1;
-    const double lam_lead = lam_pad[j + 2 * kWidth];
+    const int gg = (int)(j / Ls), t = (int)(j - (int64_t)gg * Ls);
+    const int pos = (gg < 4 && t < L) ? gg * L + t : -1;
+    const int pix = (pos >= 0 && pos < J) ? smap[pos] : -1;
+    const double lam_lead = lam_pad[(pos >= 0 ? pos : j) + 2 * kWidth];  // any finite value if neutral
     if (pix >= 0) {
       const double lam = wl[pix];
       const double rest = lam / (1 + z);
@@ -454,16 +496,19 @@ __device__ inline void stage_chunk(const double* __restrict__ panel, int L, int 
 }
 
 template <int K, int NL>
-__global__ __launch_bounds__(256, (K <= 20 ? 2 : 1)) void likelihood_kernel(LikelihoodArgs a) {
+__global__ __launch_bounds__(256, (K <= 20 ? GPDLA_WAVES_PER_EU : 1)) void likelihood_kernel(LikelihoodArgs a) {
   using Lay = Layout<K>;
   constexpr int kTiles = Lay::kTiles;
   constexpr int kGT = Lay::kGT;
   constexpr int kRow = Lay::kRow;
   constexpr int kJS = Lay::kJS;
   constexpr int kBuf = 4 * kChunkSteps * kRow;
-  constexpr int kCoreLds = NL == 3 ? 3 * kCoreTable : 1;
+  constexpr int kWingLds = 4 * ((3 * kWingStride + 3) / 4);
+  constexpr int kCoreLds = NL == 3 ? 3 * kCoreTable + kWingLds + 64 : 1;
   __shared__ __attribute__((aligned(16))) double lds[2 * kBuf + kCoreLds];
   double* core_lds = lds + 2 * kBuf;
+  double* wing_lds = core_lds + 3 * kCoreTable;
+  double* exp_lds = wing_lds + kWingLds;
 
   const int q = blockIdx.y;
   const SpecInfo inf = a.info[q];
@@ -477,26 +522,30 @@ __global__ __launch_bounds__(256, (K <= 20 ? 2 : 1)) void likelihood_kernel(Like
   }
   const int L = inf.L;
   const int nchunks = (L + kChunkSteps - 1) / kChunkSteps;
+  const int Ls = nchunks * kChunkSteps;  // segment stride in the panel; rows L..Ls-1 are neutral
   const double* panel = a.panel + inf.slot_base * kRow;
 
   // prologue: first chunk's DMA, then the core tables (plain loads) while it flies
-  stage_chunk<K>(panel, L, 0, lds, wave, lane);
+  stage_chunk<K>(panel, Ls, 0, lds, wave, lane);
   if constexpr (NL == 3) {
     for (int i = threadIdx.x; i < 3 * kCoreTable; i += 256) core_lds[i] = a.lines.buf[i];
+    if (threadIdx.x < 64) exp_lds[threadIdx.x] = a.lines.buf[kLineBufExp2 + threadIdx.x];
+    if (threadIdx.x < 3 * kWingStride) wing_lds[threadIdx.x] = a.lines.buf[kLineBufWing + threadIdx.x];
   }
 
   // ---- per-lane sample constants (MFMA A-operand layout: sample = lane & 15, segment = lane >> 4)
   const int g = lane >> 4;
   const int64_t s = s_base + (lane & 15);
-  const bool active = s <= a.S;
-  const bool is_null = s == a.S;
+  // The null model (s == S) and the idle lanes past it (s > S, outputs discarded) run with N = 0:
+  // every raw profile is then exp(0) = 1 exactly and the 7 taps sum to exactly 1.0 in the order
+  // below, i.e. absorption 1 (process_qsos.m:150-152) with no select in the sweep.
   const double off = (s < a.S) ? a.offsets[s] : 0.5;
   const double N = (s < a.S) ? a.nhi[s] : 0.0;
   const double zdla = inf.zmin + (inf.zmax - inf.zmin) * off;  // process_qsos.m:163-165
   const double zfac = 1.0 / (1 + zdla);
   double afac[3];
 #pragma unroll
-  for (int j = 0; j < 3; ++j) afac[j] = a.lines.fac3[j] * zfac;
+  for (int j = 0; j < 3; ++j) afac[j] = a.lines.buf[kLineBufFac + j] * zfac;
   const double* lamp = a.lam_pad + inf.lam_base + (int64_t)g * L;
   double lw[6];
 #pragma unroll
@@ -504,13 +553,13 @@ __global__ __launch_bounds__(256, (K <= 20 ? 2 : 1)) void likelihood_kernel(Like
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
-  auto raw = [&](double lam) {
-    if constexpr (NL == 3) return raw_profile3(lam, afac, N, core_lds, a.lines);
+  auto raw = [&](double lam, const double* wing) {
+    if constexpr (NL == 3) return raw_profile3(lam, afac, N, core_lds, wing, exp_lds);
     else return raw_profile(lam, zfac, N, a.num_lines, a.lines);
   };
   // sliding window: raw profile at padded positions gL + 0..5
-  double w0 = raw(lw[0]), w1 = raw(lw[1]), w2 = raw(lw[2]);
-  double w3 = raw(lw[3]), w4 = raw(lw[4]), w5 = raw(lw[5]);
+  double w0 = raw(lw[0], wing_lds), w1 = raw(lw[1], wing_lds), w2 = raw(lw[2], wing_lds);
+  double w3 = raw(lw[3], wing_lds), w4 = raw(lw[4], wing_lds), w5 = raw(lw[5], wing_lds);
 
   double acc[kTiles];
 #pragma unroll
@@ -521,22 +570,24 @@ __global__ __launch_bounds__(256, (K <= 20 ? 2 : 1)) void likelihood_kernel(Like
 
   for (int c = 0; c < nchunks; ++c) {
     double* cur = lds + (c & 1) * kBuf;
-    if (c + 1 < nchunks) stage_chunk<K>(panel, L, c + 1, lds + ((c + 1) & 1) * kBuf, wave, lane);
+    if (c + 1 < nchunks) stage_chunk<K>(panel, Ls, c + 1, lds + ((c + 1) & 1) * kBuf, wave, lane);
 #pragma unroll
     for (int tt = 0; tt < kChunkSteps; ++tt) {
-      const int t = c * kChunkSteps + tt;
       const double* row = cur + (tt * 4 + g) * kRow;
-      double lam, y, noise, mu, om2, vld;
+      double lam, y, noise, mu, om2;
       if constexpr ((kTiles & 1) == 0) {
         const double2 s0 = *reinterpret_cast<const double2*>(row + Lay::kLam);
         const double2 s1 = *reinterpret_cast<const double2*>(row + Lay::kNoise);
-        const double2 s2 = *reinterpret_cast<const double2*>(row + Lay::kOmega2);
-        lam = s0.x; y = s0.y; noise = s1.x; mu = s1.y; om2 = s2.x; vld = s2.y;
+        lam = s0.x; y = s0.y; noise = s1.x; mu = s1.y; om2 = row[Lay::kOmega2];
       } else {
         lam = row[Lay::kLam]; y = row[Lay::kY]; noise = row[Lay::kNoise];
-        mu = row[Lay::kMu]; om2 = row[Lay::kOmega2]; vld = row[Lay::kValid];
+        mu = row[Lay::kMu]; om2 = row[Lay::kOmega2];
       }
-      const double w6 = raw(lam);
+      // Per-step opaque zero: the wing coefficients are re-read from LDS (broadcast) every step
+      // instead of being hoisted into registers for the whole chunk.
+      int zoff;
+      asm volatile("s_mov_b32 %0, 0" : "=s"(zoff));
+      const double w6 = raw(lam, wing_lds + zoff);
       // instrumental broadening, voigt.c:297-299 (zero-initialised accumulator, taps in order)
       double ab = w0 * kInstrumentProfile[0];
       ab = fma(w1, kInstrumentProfile[1], ab);
@@ -546,18 +597,21 @@ __global__ __launch_bounds__(256, (K <= 20 ? 2 : 1)) void likelihood_kernel(Like
       ab = fma(w5, kInstrumentProfile[5], ab);
       ab = fma(w6, kInstrumentProfile[6], ab);
       w0 = w1; w1 = w2; w2 = w3; w3 = w4; w4 = w5; w5 = w6;
-      if (is_null) ab = 1.0;  // null model: no absorption (process_qsos.m:150-152)
-      // process_qsos.m:191-197 and log_mvnpdf_low_rank.m:11-15
+      // process_qsos.m:191-197 and log_mvnpdf_low_rank.m:11-15.  Masked / padding rows carry
+      // y = mu = om2 = 0, noise = 1 and an all-zero Khatri-Rao row, so they add exactly nothing
+      // (r = 0, d = 1, zero B operands) without a per-pixel select.
       const double r = fma(-mu, ab, y);
       const double a2 = ab * ab;
       const double d = fma(om2, a2, noise);
       const double dinv = rcp_nr(d);
-      const bool use = active && (vld != 0.0) && (t < L);
       const double rd = r * dinv;
-      const double wg = use ? a2 * dinv : 0.0;
-      const double wu = use ? ab * rd : 0.0;
-      q1 = use ? fma(r, rd, q1) : q1;
-      pm *= use ? d : 1.0;
+      const double wg = a2 * dinv;
+      const double wu = ab * rd;
+      q1 = fma(r, rd, q1);
+      pm *= d;
+#if GPDLA_SCHED_FENCE
+      __builtin_amdgcn_sched_barrier(0);
+#endif
       // B operands: tile t, entry 4t + (lane & 3) of this lane's segment row
       const double* brow = row + (lane & 3) * kJS;
 #pragma unroll

@@ -41,11 +41,11 @@ def test_faddeeva_host_matches_scipy():
             assert abs(im_.value - ref.imag) <= 2e-14 * abs(ref.imag) + 1e-300, (x, y)
 
 
-@pytest.mark.parametrize("line", [0, 1, 2, 5, 12, 30])
+@pytest.mark.parametrize("line", list(range(31)))
 def test_line_tables_accurate(line):
     err = C.c_double()
     assert L.load().gpdla_diag_line_table_error(line, C.byref(err)) == 0
-    assert err.value < 1e-14
+    assert err.value < 2e-15  # measured max over all 31 lines: 5.5e-16
 
 
 def test_no_cpu_fallback_without_device():

@@ -1,0 +1,17 @@
+"""Build A/B variants of libgpdla into tools/variants/<name>.so (experiments only)."""
+import sys
+from pathlib import Path
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+from gp_dla_detection_amd.build import build
+
+VARIANTS = {
+    "f1_e1": dict(GPDLA_SCHED_FENCE=1, GPDLA_FAST_EXP=1),
+    "f1_e0": dict(GPDLA_SCHED_FENCE=1, GPDLA_FAST_EXP=0),
+    "f0_e1": dict(GPDLA_SCHED_FENCE=0, GPDLA_FAST_EXP=1),
+}
+if __name__ == "__main__":
+    names = sys.argv[1:] or list(VARIANTS)
+    out = Path(__file__).resolve().parent / "variants"
+    out.mkdir(exist_ok=True)
+    for n in names:
+        print(n, build(out=out / f"{n}.so", defines=VARIANTS[n], force=True))
