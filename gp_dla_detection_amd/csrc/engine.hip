@@ -112,7 +112,8 @@ struct gpdla_engine {
   double *d_rest = nullptr, *d_mu = nullptr, *d_M = nullptr, *d_logom = nullptr;
   int32_t num_rest = 0;
   double c0 = 0, tau0 = 0, beta = 0;
-  double *d_off = nullptr, *d_nhi = nullptr;
+  double *d_off = nullptr, *d_nhi = nullptr;  // samples in ascending-offset (z_DLA) order
+  int32_t* d_perm = nullptr;                   // sorted sample index -> caller's sample index
   double* d_lines = nullptr;
   int32_t* d_status = nullptr;
 
@@ -212,7 +213,7 @@ void gpdla_engine_destroy(gpdla_engine* e) {
   (void)hipSetDevice(e->device);
   if (e->stream) (void)hipStreamSynchronize(e->stream);
   for (auto& t : e->pending) { (void)hipEventDestroy(t.start); (void)hipEventDestroy(t.stop); }
-  void* bufs[] = {e->d_rest, e->d_mu, e->d_M, e->d_logom, e->d_off, e->d_nhi, e->d_lines,
+  void* bufs[] = {e->d_rest, e->d_mu, e->d_M, e->d_logom, e->d_off, e->d_nhi, e->d_perm, e->d_lines,
                   e->d_status, e->d_meta, e->d_wl, e->d_flux, e->d_noise, e->d_mask, e->d_z,
                   e->d_info, e->d_panel, e->d_lam, e->d_smap, e->d_scratch, e->d_sll,
                   e->d_llnull, e->d_lldla, e->d_zmin, e->d_zmax, e->d_npix};
@@ -270,6 +271,7 @@ int gpdla_engine_create(int32_t device, const gpdla_model* model, const gpdla_sa
   TRY_E(grow(&e->d_logom, &dummy, G)); dummy = 0;
   TRY_E(grow(&e->d_off, &dummy, (size_t)e->S)); dummy = 0;
   TRY_E(grow(&e->d_nhi, &dummy, (size_t)e->S)); dummy = 0;
+  TRY_E(grow(&e->d_perm, &dummy, (size_t)e->S)); dummy = 0;
   const std::vector<double>& lines = host_line_data().buf;
   TRY_E(grow(&e->d_lines, &dummy, lines.size())); dummy = 0;
   TRY_E(grow(&e->d_status, &dummy, 1));
@@ -277,8 +279,23 @@ int gpdla_engine_create(int32_t device, const gpdla_model* model, const gpdla_sa
   TRY_E(upload(e->d_mu, model->mu, G * 8, e->stream));
   TRY_E(upload(e->d_M, Mrow.data(), G * K * 8, e->stream));
   TRY_E(upload(e->d_logom, model->log_omega, G * 8, e->stream));
-  TRY_E(upload(e->d_off, samples->offset_samples, (size_t)e->S * 8, e->stream));
-  TRY_E(upload(e->d_nhi, samples->nhi_samples, (size_t)e->S * 8, e->stream));
+  // Samples are swept in ascending offset order: z_DLA = zmin + (zmax - zmin) offset is then
+  // ascending for every spectrum, so the 16 samples of a wave put their line centres on nearly
+  // the same pixels and the divergent |x| < kCoreX branch is taken in few steps.  Each sample's
+  // arithmetic is lane-independent, so results are unchanged; outputs scatter back via d_perm.
+  std::vector<int32_t> perm((size_t)e->S);
+  for (int64_t i = 0; i < e->S; ++i) perm[i] = (int32_t)i;
+  std::stable_sort(perm.begin(), perm.end(), [&](int32_t a, int32_t b) {
+    return samples->offset_samples[a] < samples->offset_samples[b];
+  });
+  std::vector<double> off_sorted((size_t)e->S), nhi_sorted((size_t)e->S);
+  for (int64_t i = 0; i < e->S; ++i) {
+    off_sorted[i] = samples->offset_samples[perm[i]];
+    nhi_sorted[i] = samples->nhi_samples[perm[i]];
+  }
+  TRY_E(upload(e->d_off, off_sorted.data(), (size_t)e->S * 8, e->stream));
+  TRY_E(upload(e->d_nhi, nhi_sorted.data(), (size_t)e->S * 8, e->stream));
+  TRY_E(upload(e->d_perm, perm.data(), (size_t)e->S * 4, e->stream));
   TRY_E(upload(e->d_lines, lines.data(), lines.size() * 8, e->stream));
   if (hipMemsetAsync(e->d_status, 0, 4, e->stream) != hipSuccess ||
       hipStreamSynchronize(e->stream) != hipSuccess)
@@ -355,7 +372,8 @@ int gpdla_engine_process(gpdla_engine* e, const gpdla_spectra* sp, const gpdla_r
     int rc;
     if ((rc = grow(&e->d_meta, &e->cap_meta, per_batch))) return rc;
     if ((rc = grow(&e->d_info, &e->cap_q, (size_t)QB))) return rc;
-    if ((rc = grow(&e->d_panel, &e->cap_slots, (size_t)slots * row))) return rc;
+    // + one LDS row of slack: the staging DMA reads whole 1 KiB pieces (kernels.hip stage_chunk)
+    if ((rc = grow(&e->d_panel, &e->cap_slots, (size_t)slots * row + panel_lds_row_doubles(e->K)))) return rc;
     if ((rc = grow(&e->d_lam, &e->cap_lam, (size_t)lams))) return rc;
     if ((rc = grow(&e->d_scratch, &e->cap_scr, (size_t)blocks_x * nq * kSamplesPerBlock * es))) return rc;
     if ((rc = grow(&e->d_smap, &e->cap_smap, (size_t)slots))) return rc;
@@ -434,7 +452,7 @@ int gpdla_engine_process(gpdla_engine* e, const gpdla_spectra* sp, const gpdla_r
     LikelihoodArgs la{};
     la.q_count = (int32_t)nq;
     la.info = e->d_info; la.panel = e->d_panel; la.lam_pad = e->d_lam;
-    la.offsets = e->d_off; la.nhi = e->d_nhi; la.S = e->S;
+    la.offsets = e->d_off; la.nhi = e->d_nhi; la.perm = e->d_perm; la.S = e->S;
     la.num_lines = e->params.num_lines;
     la.lines = make_line_args(e->d_lines);
     la.scratch = e->d_scratch;

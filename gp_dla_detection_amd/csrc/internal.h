@@ -35,7 +35,9 @@ struct Layout {
   static constexpr int kUT = (K + 3) / 4;       // u tiles
   static constexpr int kTiles = kGT + kUT;
   static constexpr int kJS = ((kTiles + 2) + 1) & ~1;  // per-j stride (doubles), even
-  static constexpr int kRow = 4 * kJS;                 // doubles per slot row
+  static constexpr int kRow = 4 * kJS;                 // doubles per slot row (HBM panel stride)
+  static constexpr int kRowL = (kRow + 127) & ~127;    // LDS row stride: whole 1 KiB DMA pieces
+  static constexpr int kPieces = kRowL / 128;          // global_load_lds_dwordx4 per staged row
   static constexpr int kES = 4 * kTiles + 8;           // epilogue doubles per sample (Gram, u, scalars)
   // slot scalars in the spare words
   static constexpr int kLam = 0 * kJS + kTiles;        // padded wavelength at slot + 6
@@ -110,8 +112,9 @@ struct LikelihoodArgs {
   const SpecInfo* info;
   const double* panel;
   const double* lam_pad;
-  const double* offsets;         // [S] offset samples
+  const double* offsets;         // [S] offset samples (ascending; see engine.hip)
   const double* nhi;             // [S]
+  const int32_t* perm;           // [S] sorted sample index -> output sample index
   int64_t S;
   int32_t num_lines;
   LineArgs lines;
@@ -145,6 +148,7 @@ hipError_t launch_mvn_single(const double* y, const double* mu, const double* M_
                              int32_t* status, hipStream_t s);
 bool rank_supported(int K);
 int panel_row_doubles(int K);
+int panel_lds_row_doubles(int K);
 int scratch_doubles(int K);
 
 // host-side table fitting (faddeeva_host.cpp)

@@ -469,27 +469,29 @@ __device__ inline double ldl_log_likelihood(const double* srow, int jq, int n, b
 //   global_load_lds (the next chunk's DMA overlaps this chunk's compute).  The epilogue transposes
 //   the accumulators through a block-private scratch tile and runs the per-sample augmented LDL^T.
 // ---------------------------------------------------------------------------------------------
+// Stage chunk c (4 steps x 4 segments = 16 rows) into an LDS ring buffer.  Wave w copies the 4
+// rows of segment w, which are contiguous in the panel (rows w Ls + 4c .. +3), to LDS rows
+// 4 tt + w, each as kPieces 1 KiB global_load_lds_dwordx4 pieces (the last piece over-reads up to
+// kRowL - kRow doubles into the next row; the panel has that much slack at its end).  The row base
+// is wave-uniform (SGPRs, saddr form), the per-lane byte offsets are fixed VGPRs, so a piece
+// costs no VALU.  Issued from inline asm so hipcc does not make the other buffer's ds_reads wait
+// on it; the consumer waits with an explicit s_waitcnt vmcnt(0) + barrier at the end of the chunk.
+// Hazards inside the string: s_nop 4 for a fresh SGPR base read by a global_* op, s_nop 0 between
+// the M0 write and the LDS-DMA that reads it.
 template <int K>
-__device__ inline void stage_chunk(const double* __restrict__ panel, int L, int c, double* buf,
-                                   int wave, int lane) {
+__device__ inline void stage_chunk(const double* __restrict__ panel, int Ls, int c, uint32_t buf,
+                                   int wave_s, const uint32_t (&voff)[Layout<K>::kPieces]) {
   using Lay = Layout<K>;
-  constexpr int kGran = Lay::kRow / 2;                 // 16-byte granules per row
-  constexpr int kTot = 4 * kChunkSteps * kGran;        // granules per chunk
-  constexpr int kInstr = (kTot + 63) / 64;             // 1 KiB wave instructions per chunk
-  for (int i = wave; i < kInstr; i += kWavesPerBlock) {
-    const int gi = i * 64 + lane;
-    if (gi < kTot) {
-      const int r = gi / kGran, o = gi - r * kGran;
-      const int tt = r >> 2, gg = r & 3;
-      const double* src = panel + ((int64_t)gg * L + c * kChunkSteps + tt) * Lay::kRow + 2 * o;
-      // global_load_lds_dwordx4: 64 lanes x 16 B land at M0 + lane*16.  Issued from inline asm so
-      // hipcc does not make the other buffer's ds_reads wait on it; the consumer side waits with
-      // an explicit s_waitcnt vmcnt(0) + barrier at the end of the chunk.
-      const uint32_t dst = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)(buf + i * 128);
+#pragma unroll
+  for (int tt = 0; tt < kChunkSteps; ++tt) {
+    const double* src = panel + ((int64_t)wave_s * Ls + c * kChunkSteps + tt) * Lay::kRow;
+    const uint32_t dst = buf + (uint32_t)((tt * 4 + wave_s) * Lay::kRowL * 8);
+#pragma unroll
+    for (int h = 0; h < Lay::kPieces; ++h) {
 #pragma clang diagnostic push
 #pragma clang diagnostic ignored "-Winline-asm"
-      asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, off"
-                   :: "s"(__builtin_amdgcn_readfirstlane(dst)), "v"(src) : "memory", "m0");
+      asm volatile("s_nop 4\n\ts_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2"
+                   :: "s"(dst + h * 1024), "v"(voff[h]), "s"(src) : "memory", "m0");
 #pragma clang diagnostic pop
     }
   }
@@ -500,9 +502,10 @@ __global__ __launch_bounds__(256, (K <= 20 ? GPDLA_WAVES_PER_EU : 1)) void likel
   using Lay = Layout<K>;
   constexpr int kTiles = Lay::kTiles;
   constexpr int kGT = Lay::kGT;
-  constexpr int kRow = Lay::kRow;
+  constexpr int kRowL = Lay::kRowL;
   constexpr int kJS = Lay::kJS;
-  constexpr int kBuf = 4 * kChunkSteps * kRow;
+  constexpr int kBuf = 4 * kChunkSteps * kRowL;
+  static_assert(kWavesPerBlock == 4, "stage_chunk: one wave per segment");
   constexpr int kWingLds = 4 * ((3 * kWingStride + 3) / 4);
   constexpr int kCoreLds = NL == 3 ? 3 * kCoreTable + kWingLds + 64 : 1;
   __shared__ __attribute__((aligned(16))) double lds[2 * kBuf + kCoreLds];
@@ -523,10 +526,15 @@ __global__ __launch_bounds__(256, (K <= 20 ? GPDLA_WAVES_PER_EU : 1)) void likel
   const int L = inf.L;
   const int nchunks = (L + kChunkSteps - 1) / kChunkSteps;
   const int Ls = nchunks * kChunkSteps;  // segment stride in the panel; rows L..Ls-1 are neutral
-  const double* panel = a.panel + inf.slot_base * kRow;
+  const double* panel = a.panel + inf.slot_base * Lay::kRow;
+  const int wave_s = __builtin_amdgcn_readfirstlane(wave);
+  const uint32_t lds_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)lds;
+  uint32_t voff[Lay::kPieces];
+#pragma unroll
+  for (int h = 0; h < Lay::kPieces; ++h) voff[h] = (uint32_t)(lane * 16 + h * 1024);
 
   // prologue: first chunk's DMA, then the core tables (plain loads) while it flies
-  stage_chunk<K>(panel, Ls, 0, lds, wave, lane);
+  stage_chunk<K>(panel, Ls, 0, lds_base, wave_s, voff);
   if constexpr (NL == 3) {
     for (int i = threadIdx.x; i < 3 * kCoreTable; i += 256) core_lds[i] = a.lines.buf[i];
     if (threadIdx.x < 64) exp_lds[threadIdx.x] = a.lines.buf[kLineBufExp2 + threadIdx.x];
@@ -570,10 +578,11 @@ __global__ __launch_bounds__(256, (K <= 20 ? GPDLA_WAVES_PER_EU : 1)) void likel
 
   for (int c = 0; c < nchunks; ++c) {
     double* cur = lds + (c & 1) * kBuf;
-    if (c + 1 < nchunks) stage_chunk<K>(panel, Ls, c + 1, lds + ((c + 1) & 1) * kBuf, wave, lane);
+    if (c + 1 < nchunks)
+      stage_chunk<K>(panel, Ls, c + 1, lds_base + (uint32_t)(((c + 1) & 1) * kBuf * 8), wave_s, voff);
 #pragma unroll
     for (int tt = 0; tt < kChunkSteps; ++tt) {
-      const double* row = cur + (tt * 4 + g) * kRow;
+      const double* row = cur + (tt * 4 + g) * kRowL;
       double lam, y, noise, mu, om2;
       if constexpr ((kTiles & 1) == 0) {
         const double2 s0 = *reinterpret_cast<const double2*>(row + Lay::kLam);
@@ -672,7 +681,7 @@ __global__ __launch_bounds__(256, (K <= 20 ? GPDLA_WAVES_PER_EU : 1)) void likel
   if (jq == 0 && s2 <= a.S) {
     if (bad) atomicOr(a.status, 1);
     if (s2 == a.S) a.ll_null[q] = ll;
-    else if (a.sample_ll) a.sample_ll[q * a.ld + s2] = ll;
+    else if (a.sample_ll) a.sample_ll[q * a.ld + a.perm[s2]] = ll;
   }
 }
 
@@ -848,6 +857,12 @@ int scratch_doubles(int K) {
 
 int panel_row_doubles(int K) {
 #define X(k) if (K == k) return Layout<k>::kRow;
+  GPDLA_FOR_EACH_RANK(X)
+#undef X
+  return 0;
+}
+int panel_lds_row_doubles(int K) {
+#define X(k) if (K == k) return Layout<k>::kRowL;
   GPDLA_FOR_EACH_RANK(X)
 #undef X
   return 0;
