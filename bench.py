@@ -41,31 +41,73 @@ def effective_bytes_per_eval(n: int, k: int, w: int = 8) -> float:
     return w * (n * (k + 5) + 8) + w
 
 
-def cpu_baseline(model, samples, spectra, budget_s: float) -> dict:
-    """The numpy oracle (MATLAB-order restatement) on one host core, on a bounded sample of the
-    same workload: spectra 0, 1, ... with all their DLA samples, until the time budget is spent."""
+def _cpu_worker(task):
+    """One host process: the oracle over one spectrum's DLA samples until the deadline."""
+    model, spec, offsets, nhis, budget_s = task
     from threadpoolctl import threadpool_limits
     from oracle import gpdla_oracle as O
-    done, nspec = 0, 0
+    done = 0
     with threadpool_limits(limits=1):
         t0 = time.perf_counter()
-        for s in spectra:
-            prep = O.prepare_spectrum(s["wavelengths"], s["flux"], s["noise_variance"], s["pixel_mask"],
-                                      s["z_qso"], model)
-            zs = prep["zmin"] + (prep["zmax"] - prep["zmin"]) * samples["offset_samples"]
-            nspec += 1
-            for z, N in zip(zs, samples["nhi_samples"]):
-                O.sample_log_likelihood(prep, z, N, 3)
-                done += 1
-                if time.perf_counter() - t0 >= budget_s:
-                    break
+        prep = O.prepare_spectrum(spec["wavelengths"], spec["flux"], spec["noise_variance"],
+                                  spec["pixel_mask"], spec["z_qso"], model)
+        zs = prep["zmin"] + (prep["zmax"] - prep["zmin"]) * offsets
+        for z, N in zip(zs, nhis):
+            O.sample_log_likelihood(prep, z, N, 3)
+            done += 1
             if time.perf_counter() - t0 >= budget_s:
                 break
         el = time.perf_counter() - t0
-    return {"value": done / el, "unit": "evals/s", "cores": 1, "kind": "port",
-            "sample": f"{done} (spectrum, DLA-sample) evaluations over the first {nspec} spectra of the bench "
-                      f"workload (n=800, k=20, 3 lines) in {el:.1f} s on 1 host core; numpy/scipy restatement "
-                      "of process_qsos.m:186-197 (MATLAB is not available)"}
+    return done, el
+
+
+def host_cores() -> int:
+    """Cores this process may use, capped at the GPU box's per-GPU CPU share (16)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(16, n))
+
+
+def cpu_baseline(model, samples, spectra, budget_s: float) -> dict:
+    """The numpy oracle (MATLAB-order restatement of process_qsos.m:186-197) on the host cores,
+    parallel over spectra like the reference's per-worker parfor (one process per core, one BLAS
+    thread each), on a bounded sample of the bench workload: worker c sweeps the DLA samples of
+    spectrum c in order until the time budget is spent.  Runs before the GPU is initialised
+    (spawned workers)."""
+    import multiprocessing as mp
+    cores = host_cores()
+    tasks = [(model, spectra[c % len(spectra)], samples["offset_samples"], samples["nhi_samples"], budget_s)
+             for c in range(cores)]
+    t0 = time.perf_counter()
+    with mp.get_context("spawn").Pool(cores) as pool:
+        res = pool.map(_cpu_worker, tasks)
+    wall = time.perf_counter() - t0
+    done = sum(r[0] for r in res)
+    el = max(r[1] for r in res)
+    return {"value": done / el, "unit": "evals/s", "cores": cores, "kind": "port",
+            "sample": f"{done} (spectrum, DLA-sample) evaluations: {cores} host processes x 1 thread, "
+                      f"process c sweeping the samples of bench spectrum c for {el:.1f} s (wall incl. start-up "
+                      f"{wall:.1f} s); numpy/scipy restatement of process_qsos.m:186-197 (MATLAB is not "
+                      "available); n=800, k=20, 3 lines"}
+
+
+# rocprofv3 summary of this workload (tools/profile.sh + tools/summarize_profile.py), committed
+PROFILE_SUMMARY = ROOT / "profiles" / "r1c_summary.json"
+
+
+def profiled_traffic(Q: int, S: int, k: int):
+    """HBM bytes per likelihood launch from the committed PMC profile of the default workload
+    (2 x FETCH_SIZE + WRITE_SIZE, gfx950 correction per MI355X_MICROARCH.md; includes
+    Infinity-Cache hits).  None for other workloads or if no summary is present."""
+    if (Q, S, k) != (1024, 10000, 20) or not PROFILE_SUMMARY.exists():
+        return None, None
+    d = json.loads(PROFILE_SUMMARY.read_text())
+    for ent in d["kernels"]:
+        if ent["kernel"].startswith("void gpdla::likelihood_kernel<20") and "hbm_bytes_per_launch" in ent:
+            return ent["hbm_bytes_per_launch"], f"{PROFILE_SUMMARY.relative_to(ROOT)} (rocprofv3 PMC)"
+    return None, None
 
 
 def main():
@@ -99,6 +141,10 @@ def main():
     Q = args.spectra
     spectra = [syn.make_spectrum(model, rank * Q + q) for q in range(Q)]
     packed = syn.pack_spectra(spectra)
+    # CPU baseline first, while no process has touched the GPU (its workers are spawned)
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_budget > 0:
+        cpu = cpu_baseline(model, samples, spectra, args.cpu_budget)
     D = lambda a: L.DeviceArray.from_numpy(a, device=local_rank)
     t = {key: D(packed[key]) for key in ("wavelengths", "flux", "noise_variance", "pixel_mask", "z_qsos")}
     S = args.samples
@@ -151,6 +197,7 @@ def main():
     achieved_tf = flops_launch / (avg_ms * 1e-3) / 1e12
     eff_gbs = effective_bytes_per_eval(n_mean, args.k) * evals_per_launch / (avg_ms * 1e-3) / 1e9
 
+    traffic, traffic_src = profiled_traffic(Q, S, args.k)
     result = {
         "metric": "(spectrum x DLA-sample) log-evidence evals/sec",
         "value": value,
@@ -168,7 +215,8 @@ def main():
                                f"3 Lyman lines, fp64", "spectra_per_gpu": Q, "num_samples": S,
                    "k": args.k, "n_pixels": n_mean, "parallelism": f"spectrum-shard x{world}"},
         "roofline": {"bound": "mfma", "achieved": achieved_tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": achieved_tf / FP64_PEAK_TFLOPS, "traffic": None,
+                     "frac": achieved_tf / FP64_PEAK_TFLOPS, "traffic": traffic,
+                     "traffic_source": traffic_src,
                      "kernel": "likelihood_kernel<20>", "avg_launch_ms": avg_ms,
                      "flops_per_eval": algorithmic_flops_per_eval(n_mean, args.k),
                      "evals_per_launch": evals_per_launch},
@@ -180,8 +228,8 @@ def main():
                       "reduce": st["reduce_ms"] / max(st["reduce_launches"], 1)},
         "checks_ok": ok,
     }
-    if rank == 0 and world == 1 and args.cpu_budget > 0:
-        result["cpu_baseline"] = cpu_baseline(model, samples, spectra, args.cpu_budget)
+    if cpu is not None:
+        result["cpu_baseline"] = cpu
     if rank == 0:
         print(json.dumps(result), flush=True)
     eng.close()

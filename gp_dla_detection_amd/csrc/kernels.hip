@@ -461,7 +461,7 @@ __device__ inline double ldl_log_likelihood(const double* srow, int jq, int n, b
 }
 
 // ---------------------------------------------------------------------------------------------
-// likelihood: for one spectrum (blockIdx.y) and 64 samples (4 waves x 16), sweep all slots:
+// likelihood: for one spectrum and 64 samples (4 waves x 16), sweep all slots:
 //   per lane (sample s = lane & 15, segment g = lane >> 4): Voigt raw profile at the leading
 //   padded wavelength, 7-tap convolution from a register window, DLA-modulated pixel terms
 //   a^2/d and a r/d (process_qsos.m:189-197), then v_mfma_f64_4x4x4_4b over the Khatri-Rao
@@ -513,10 +513,18 @@ __global__ __launch_bounds__(256, (K <= 20 ? GPDLA_WAVES_PER_EU : 1)) void likel
   double* wing_lds = core_lds + 3 * kCoreTable;
   double* exp_lds = wing_lds + kWingLds;
 
-  const int q = blockIdx.y;
+  // XCD-aware block order: the dispatcher deals consecutive blocks round-robin over the 8 XCDs,
+  // so block b runs on XCD b % 8.  Virtual index v gives each XCD one contiguous eighth of the
+  // (spectrum, sample-block) space: the blocks sharing a spectrum's panel share one XCD's L2.
+  const int64_t blocks_x = (a.S + 1 + kSamplesPerBlock - 1) / kSamplesPerBlock;
+  const int64_t per_xcd = gridDim.x / 8;  // grid is padded to a multiple of 8
+  const int64_t v = (int64_t)(blockIdx.x % 8) * per_xcd + blockIdx.x / 8;
+  if (v >= blocks_x * a.q_count) return;
+  const int q = (int)(v / blocks_x);
+  const int64_t bx = v - (int64_t)q * blocks_x;
   const SpecInfo inf = a.info[q];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int64_t s_base = (int64_t)blockIdx.x * kSamplesPerBlock + wave * kSamplesPerWave;
+  const int64_t s_base = bx * kSamplesPerBlock + wave * kSamplesPerWave;
   if (inf.J == 0) {  // unusable spectrum (no unmasked in-range pixel): NaN outputs
     const int64_t su = s_base + (lane >> 2);
     if ((lane & 3) == 0 && su < a.S && a.sample_ll) a.sample_ll[q * a.ld + su] = NAN;
@@ -659,7 +667,7 @@ __global__ __launch_bounds__(256, (K <= 20 ? GPDLA_WAVES_PER_EU : 1)) void likel
   //      back from L2 after the barrier, which frees the accumulator registers), then the
   //      augmented LDL^T per sample in registers (a quad of lanes each).
   //      D lane map of 4x4x4_4b: sample 4*((lane>>2)&3) + (lane>>4), entry 4t + (lane&3).
-  double* scr = a.scratch + (((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * kSamplesPerBlock +
+  double* scr = a.scratch + (v * kSamplesPerBlock +
                              wave * kSamplesPerWave) * Lay::kES;
   {
     const int sd = 4 * ((lane >> 2) & 3) + (lane >> 4);
@@ -828,10 +836,12 @@ hipError_t launch_prep_k(const PrepArgs& a, hipStream_t s) {
 template <int K>
 hipError_t launch_likelihood_k(const LikelihoodArgs& a, hipStream_t s) {
   const int64_t blocks_x = (a.S + 1 + kSamplesPerBlock - 1) / kSamplesPerBlock;
+  const int64_t nb = (blocks_x * a.q_count + 7) / 8 * 8;  // 1-D, padded for the XCD remap
+  if (nb > INT32_MAX) return hipErrorInvalidValue;
   if (a.num_lines == 3)
-    hipLaunchKernelGGL((likelihood_kernel<K, 3>), dim3((unsigned)blocks_x, a.q_count), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((likelihood_kernel<K, 3>), dim3((unsigned)nb), dim3(256), 0, s, a);
   else
-    hipLaunchKernelGGL((likelihood_kernel<K, 0>), dim3((unsigned)blocks_x, a.q_count), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((likelihood_kernel<K, 0>), dim3((unsigned)nb), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 
