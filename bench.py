@@ -94,7 +94,7 @@ def cpu_baseline(model, samples, spectra, budget_s: float) -> dict:
 
 
 # rocprofv3 summary of this workload (tools/profile.sh + tools/summarize_profile.py), committed
-PROFILE_SUMMARY = ROOT / "profiles" / "r1c_summary.json"
+PROFILE_SUMMARY = ROOT / "profiles" / "r1d_summary.json"
 
 
 def profiled_traffic(Q: int, S: int, k: int):
