@@ -22,6 +22,9 @@ MEM_HOST = 0
 MEM_DEVICE = 1
 ABSORPTION_REFERENCE = 0
 ABSORPTION_UNMASKED = 1
+PATH_AUTO = 0
+PATH_FUSED = 1
+PATH_PANEL_GEMM = 2
 
 dp = C.POINTER(C.c_double)
 i64p = C.POINTER(C.c_int64)
@@ -44,7 +47,8 @@ class Params(C.Structure):
                 ("min_lambda", C.c_double), ("max_lambda", C.c_double),
                 ("lya_wavelength", C.c_double), ("lyman_limit", C.c_double),
                 ("min_z_cut", C.c_double), ("max_z_cut", C.c_double),
-                ("absorption_mode", C.c_int32), ("max_batch_spectra", C.c_int32)]
+                ("absorption_mode", C.c_int32), ("max_batch_spectra", C.c_int32),
+                ("path", C.c_int32)]
 
 
 class Spectra(C.Structure):

@@ -1,0 +1,219 @@
+// Device helpers shared by the fused path (kernels.hip) and the panel-GEMM path (gemm_path.hip):
+// constants, block scans/reductions, model interpolation, the Voigt raw profile (voigt.c:282-292)
+// and the table exp.  Header-only, internal linkage per translation unit.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+
+#include "internal.h"
+
+// Build-time variant switches (A/B experiments; defaults are the shipped configuration).
+#ifndef GPDLA_WAVES_PER_EU
+#define GPDLA_WAVES_PER_EU 2
+#endif
+#ifndef GPDLA_SCHED_FENCE
+#define GPDLA_SCHED_FENCE 1
+#endif
+#ifndef GPDLA_FAST_EXP
+#define GPDLA_FAST_EXP 1
+#endif
+
+namespace gpdla {
+
+namespace {
+
+constexpr double kLog2Pi = 1.83787706640934534;  // log_mvnpdf_low_rank.m:7
+constexpr double kLn2 = 0.693147180559945309417;
+
+// ---------------------------------------------------------------------------------------------
+// small device helpers
+// ---------------------------------------------------------------------------------------------
+__device__ inline double rcp_nr(double d) {
+  // v_rcp_f64 (~2^-26) refined by two Newton steps -> within 1 ulp of 1/d
+  double r = __builtin_amdgcn_rcp(d);
+  double e = fma(-d, r, 1.0);
+  r = fma(r, e, r);
+  e = fma(-d, r, 1.0);
+  return fma(r, e, r);
+}
+
+// exp(v) for v <= 0 (v = N * total, voigt.c:291): v = (64 m + j) ln2/64 + r, |r| <= ln2/128,
+// exp(v) = 2^m * 2^(j/64) * e^r with 2^(j/64) from a 64-entry LDS table (host-rounded from long
+// double) and e^r a degree-5 Taylor polynomial (truncation < 4e-17).  Underflows to +0 like exp.
+__device__ inline double exp_tab64(double v, const double* __restrict__ tab) {
+  constexpr double kInvL = 92.33248261689366;              // 64 / ln 2
+  constexpr double kLhi = 0.010830424695086549;           // ln2/64 to 33 bits (k*kLhi exact)
+  constexpr double kLlo = 1.162596423439437e-12;           // ln2/64 - kLhi
+  v = fmax(v, -1100.0);                                    // keeps k in int range; exp(-1100) = 0
+  const double k = __builtin_rint(v * kInvL);
+  double r = fma(-k, kLhi, v);
+  r = fma(-k, kLlo, r);
+  double p = fma(r, 1.0 / 120.0, 1.0 / 24.0);
+  p = fma(p, r, 1.0 / 6.0);
+  p = fma(p, r, 0.5);
+  p = fma(p, r, 1.0);
+  p = fma(p, r, 1.0);
+  const int ki = (int)k;
+  return __builtin_ldexp(p * tab[ki & 63], ki >> 6);
+}
+
+template <int SRC>
+__device__ inline double quad_bcast_c(double v) {
+  int lo = __double2loint(v), hi = __double2hiint(v);
+  lo = __builtin_amdgcn_mov_dpp(lo, SRC * 0x55, 0xF, 0xF, false);
+  hi = __builtin_amdgcn_mov_dpp(hi, SRC * 0x55, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+
+// value of lane (quad_base + src) broadcast to the 4 lanes of each quad; src folds to a
+// constant after unrolling
+__device__ inline double quad_bcast(double v, int src) {
+  switch (src & 3) {
+    case 0: return quad_bcast_c<0>(v);
+    case 1: return quad_bcast_c<1>(v);
+    case 2: return quad_bcast_c<2>(v);
+    default: return quad_bcast_c<3>(v);
+  }
+}
+
+__device__ inline int wave_incl_scan(int v) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    int t = __shfl_up(v, off);
+    if (lane >= off) v += t;
+  }
+  return v;
+}
+
+// exclusive block scan over 256 threads; returns exclusive prefix, total via *total
+__device__ inline int block_excl_scan(int v, int* lds4, int* total) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  int inc = wave_incl_scan(v);
+  if (lane == 63) lds4[wave] = inc;
+  __syncthreads();
+  int woff = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    int c = lds4[w];
+    if (w < wave) woff += c;
+    tot += c;
+  }
+  __syncthreads();
+  *total = tot;
+  return woff + inc - v;
+}
+
+__device__ inline double block_reduce_min(double v, double* lds4) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = fmin(v, __shfl_xor(v, off));
+  if (lane == 0) lds4[wave] = v;
+  __syncthreads();
+  double r = fmin(fmin(lds4[0], lds4[1]), fmin(lds4[2], lds4[3]));
+  __syncthreads();
+  return r;
+}
+
+__device__ inline double block_reduce_max(double v, double* lds4) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = fmax(v, __shfl_xor(v, off));
+  if (lane == 0) lds4[wave] = v;
+  __syncthreads();
+  double r = fmax(fmax(lds4[0], lds4[1]), fmax(lds4[2], lds4[3]));
+  __syncthreads();
+  return r;
+}
+
+__device__ inline double block_reduce_sum(double v, double* lds4) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+  if (lane == 0) lds4[wave] = v;
+  __syncthreads();
+  double r = (lds4[0] + lds4[1]) + (lds4[2] + lds4[3]);
+  __syncthreads();
+  return r;
+}
+
+// Gram pair e -> (r, c), row-major upper triangle (r <= c)
+template <int K>
+__device__ inline void gram_pair(int e, int& r, int& c) {
+  int rr = 0, start = 0;
+  while (rr < K - 1 && e >= start + (K - rr)) {
+    start += K - rr;
+    ++rr;
+  }
+  r = rr;
+  c = rr + (e - start);
+}
+
+template <int K>
+__device__ __host__ constexpr int gram_index(int r, int c) {
+  return r * K - r * (r - 1) / 2 + (c - r);
+}
+
+// numpy.interp-style linear interpolation index on a strictly increasing grid
+__device__ inline int interp_index(const double* xp, int G, double x) {
+  int lo = 0, hi = G - 1;  // invariant xp[lo] <= x < xp[hi] (x inside the grid)
+  while (hi - lo > 1) {
+    int mid = (lo + hi) >> 1;
+    if (xp[mid] <= x) lo = mid; else hi = mid;
+  }
+  return lo;
+}
+
+__device__ inline double interp_eval(const double* xp, const double* fp, int G, int j, double x) {
+  if (x >= xp[G - 1]) return fp[G - 1];
+  const double slope = (fp[j + 1] - fp[j]) / (xp[j + 1] - xp[j]);
+  return slope * (x - xp[j]) + fp[j];
+}
+
+// ---------------------------------------------------------------------------------------------
+// Voigt raw profile at one padded wavelength: exp(N * total), total = -sum_j lc_j V_j(v_j)
+// (voigt.c:282-292).  x_j = lambda * fac_j / (1+z) - c/(sigma sqrt 2) (voigt.c:278-279,287).
+// ---------------------------------------------------------------------------------------------
+constexpr double kC2 = kCcgs / (kSigma * 1.41421356237309504880);  // c / (sigma sqrt 2)
+
+// generic: any number of lines, core tables in global memory
+__device__ inline double raw_profile(double lam, double zfac, double N, int num_lines,
+                                     const LineArgs& L) {
+  double total = 0.0;
+  for (int j = 0; j < num_lines; ++j) {
+    const double x = fma(lam, L.buf[kLineBufFac + j] * zfac, -kC2);
+    total -= line_profile_eval(L.buf + (size_t)j * kCoreTable,
+                               L.buf + kLineBufWing + (size_t)j * kWingStride, x);
+  }
+  return exp(N * total);
+}
+
+// 3-line fast path (Lyman alpha, beta, gamma; set_parameters.m:63): the damping wing is
+// evaluated branch-free for every lane with its coefficients read from LDS by broadcast
+// (wing_lds), the core polynomial (LDS tables) only by the lanes with |x| < kCoreX.
+__device__ inline double raw_profile3(double lam, const double (&afac)[3], double N,
+                                      const double* __restrict__ core_lds,
+                                      const double* __restrict__ wing_lds,
+                                      const double* __restrict__ exp_lds) {
+  double total = 0.0;
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const double x = fma(lam, afac[j], -kC2);
+    const double ax = fabs(x);
+    double f = wing_eval(wing_lds + j * kWingStride, x);
+    if (ax < kCoreX) f = core_eval(core_lds + j * kCoreTable, ax);
+    total -= f;
+  }
+#if GPDLA_FAST_EXP
+  return exp_tab64(N * total, exp_lds);
+#else
+  return exp(N * total);
+#endif
+}
+
+}  // namespace
+
+}  // namespace gpdla

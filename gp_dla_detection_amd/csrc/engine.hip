@@ -1,6 +1,7 @@
 // C-ABI of libgpdla.so (include/gpdla.h): engine lifecycle, device workspaces, batching,
 // kernel-time accounting and the standalone voigt / log_mvnpdf_low_rank entry points.
 #include <hip/hip_runtime.h>
+#include <rocblas/rocblas.h>
 
 #include <algorithm>
 #include <cmath>
@@ -104,6 +105,8 @@ struct gpdla_engine {
   int device = 0;
   int K = 0;
   int64_t S = 0;
+  bool gemm = false;                 // panel-GEMM path (gemm_path.hip + rocBLAS) instead of fused
+  rocblas_handle blas = nullptr;
   gpdla_params params{};
   hipStream_t own_stream = nullptr;
   hipStream_t stream = nullptr;
@@ -132,6 +135,11 @@ struct gpdla_engine {
          *d_zmax = nullptr;
   int32_t* d_npix = nullptr;
   size_t cap_qout = 0;
+  // panel-GEMM path workspaces
+  double *d_pm = nullptr, *d_srow = nullptr, *d_wg = nullptr, *d_wu = nullptr, *d_G = nullptr,
+         *d_U = nullptr, *d_q1p = nullptr, *d_ldp = nullptr;
+  size_t cap_pm = 0, cap_srow = 0, cap_wg = 0, cap_wu = 0, cap_G = 0, cap_U = 0, cap_q1p = 0,
+         cap_ldp = 0;
 
   // pinned host metadata (reused after meta_ready completes)
   int64_t* h_meta = nullptr;
@@ -178,6 +186,8 @@ int validate_params(const gpdla_params* p) {
   if (!(p->max_lambda > p->min_lambda) || !(p->pixel_spacing > 0) || !(p->lya_wavelength > 0))
     return set_error(GPDLA_EINVAL, "invalid wavelength parameters");
   if (p->max_batch_spectra < 0) return set_error(GPDLA_EINVAL, "max_batch_spectra < 0");
+  if (p->path != GPDLA_PATH_AUTO && p->path != GPDLA_PATH_FUSED && p->path != GPDLA_PATH_PANEL_GEMM)
+    return set_error(GPDLA_EINVAL, "path=%d", p->path);
   return GPDLA_OK;
 }
 
@@ -216,10 +226,12 @@ void gpdla_engine_destroy(gpdla_engine* e) {
   void* bufs[] = {e->d_rest, e->d_mu, e->d_M, e->d_logom, e->d_off, e->d_nhi, e->d_perm, e->d_lines,
                   e->d_status, e->d_meta, e->d_wl, e->d_flux, e->d_noise, e->d_mask, e->d_z,
                   e->d_info, e->d_panel, e->d_lam, e->d_smap, e->d_scratch, e->d_sll,
-                  e->d_llnull, e->d_lldla, e->d_zmin, e->d_zmax, e->d_npix};
+                  e->d_llnull, e->d_lldla, e->d_zmin, e->d_zmax, e->d_npix, e->d_pm, e->d_srow,
+                  e->d_wg, e->d_wu, e->d_G, e->d_U, e->d_q1p, e->d_ldp};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (e->h_meta) (void)hipHostFree(e->h_meta);
+  if (e->blas) (void)rocblas_destroy_handle(e->blas);
   if (e->meta_done) (void)hipEventDestroy(e->meta_done);
   if (e->own_stream) (void)hipStreamDestroy(e->own_stream);
   delete e;
@@ -232,8 +244,12 @@ int gpdla_engine_create(int32_t device, const gpdla_model* model, const gpdla_sa
   int rc = check_device(device);
   if (rc) return rc;
   if ((rc = validate_params(params))) return rc;
-  if (!rank_supported(model->k))
-    return set_error(GPDLA_EUNSUPPORTED, "rank k=%d not compiled (supported: 4 8 10 12 16 20 24)", model->k);
+  const bool fused_ok = rank_supported(model->k);
+  const bool use_gemm = params->path == GPDLA_PATH_PANEL_GEMM || (params->path == GPDLA_PATH_AUTO && !fused_ok);
+  if (!use_gemm && !fused_ok)
+    return set_error(GPDLA_EUNSUPPORTED, "rank k=%d not compiled for the fused path (4 8 10 12 16 20 24)", model->k);
+  if (use_gemm && (model->k < 1 || model->k > kGemmMaxK))
+    return set_error(GPDLA_EUNSUPPORTED, "rank k=%d outside the panel-GEMM path's 1..%d", model->k, kGemmMaxK);
   if (model->num_rest < 2 || !model->rest_wavelengths || !model->mu || !model->M || !model->log_omega)
     return set_error(GPDLA_EINVAL, "invalid model");
   for (int i = 1; i < model->num_rest; ++i)
@@ -247,6 +263,7 @@ int gpdla_engine_create(int32_t device, const gpdla_model* model, const gpdla_sa
   e->device = device;
   e->K = model->k;
   e->S = samples->num_samples;
+  e->gemm = use_gemm;
   e->params = *params;
   e->num_rest = model->num_rest;
   e->c0 = std::exp(model->log_c_0);     // process_qsos.m:84-86
@@ -259,6 +276,8 @@ int gpdla_engine_create(int32_t device, const gpdla_model* model, const gpdla_sa
   e->stream = e->own_stream;
   if (hipEventCreateWithFlags(&e->meta_done, hipEventDisableTiming) != hipSuccess)
     return fail(set_error(GPDLA_EDEVICE, "hipEventCreate failed"));
+  if (e->gemm && rocblas_create_handle(&e->blas) != rocblas_status_success)
+    return fail(set_error(GPDLA_EDEVICE, "rocblas_create_handle failed"));
 
   const size_t G = model->num_rest, K = model->k;
   std::vector<double> Mrow(G * K);
@@ -313,6 +332,48 @@ int gpdla_engine_set_stream(gpdla_engine* e, void* hip_stream) {
   return GPDLA_OK;
 }
 
+// Panel-GEMM path for one batch: per spectrum and chunk of samples, weights -> two dgemm ->
+// batched LDL^T (gemm_path.hip).  All on stream st, in order.
+static int run_panel_gemm(gpdla_engine* e, int64_t nq, const int64_t* h_sb, const int64_t* h_lb,
+                          const int64_t* h_cap, int64_t sc_max, double* o_sll, int64_t ld,
+                          double* o_null, hipStream_t st) {
+  const int K = e->K;
+  const int64_t E = (int64_t)K * (K + 1) / 2;
+  if (rocblas_set_stream(e->blas, st) != rocblas_status_success)
+    return set_error(GPDLA_EDEVICE, "rocblas_set_stream failed");
+  const double one = 1.0, zero = 0.0;
+  for (int64_t q = 0; q < nq; ++q) {
+    for (int64_t s0 = 0; s0 <= e->S; s0 += sc_max) {
+      const int32_t sc = (int32_t)std::min<int64_t>(sc_max, e->S + 1 - s0);
+      WeightsArgs wa{};
+      wa.info = e->d_info; wa.q = (int32_t)q;
+      wa.srow = e->d_srow + h_sb[q] * 8; wa.lam_pad = e->d_lam + h_lb[q]; wa.cap = h_cap[q];
+      wa.offsets = e->d_off; wa.nhi = e->d_nhi; wa.S = e->S; wa.s0 = s0; wa.sc = sc;
+      wa.num_lines = e->params.num_lines; wa.lines = make_line_args(e->d_lines);
+      wa.wg = e->d_wg; wa.wu = e->d_wu; wa.q1p = e->d_q1p; wa.ldp = e->d_ldp;
+      HIP_TRY(launch_weights(wa, st));
+      // Gram (E x sc) = PG (E x cap, the slot-major Khatri-Rao rows) * Wg^T (Wg stored [cap][sc])
+      rocblas_status bs = rocblas_dgemm(e->blas, rocblas_operation_none, rocblas_operation_transpose,
+                                        (rocblas_int)E, sc, (rocblas_int)h_cap[q], &one,
+                                        e->d_panel + h_sb[q] * E, (rocblas_int)E, e->d_wg, sc, &zero,
+                                        e->d_G, (rocblas_int)E);
+      if (bs == rocblas_status_success)
+        bs = rocblas_dgemm(e->blas, rocblas_operation_none, rocblas_operation_transpose, K, sc,
+                           (rocblas_int)h_cap[q], &one, e->d_pm + h_sb[q] * K, K, e->d_wu, sc, &zero,
+                           e->d_U, K);
+      if (bs != rocblas_status_success)
+        return set_error(GPDLA_EDEVICE, "rocblas_dgemm failed: %s", rocblas_status_to_string(bs));
+      LdlArgs da{};
+      da.info = e->d_info; da.q = (int32_t)q; da.k = K;
+      da.G = e->d_G; da.U = e->d_U; da.q1p = e->d_q1p; da.ldp = e->d_ldp;
+      da.S = e->S; da.s0 = s0; da.sc = sc; da.perm = e->d_perm;
+      da.sample_ll = o_sll ? o_sll + q * ld : nullptr; da.ll_null = o_null + q; da.status = e->d_status;
+      HIP_TRY(launch_ldl_batch(da, st));
+    }
+  }
+  return GPDLA_OK;
+}
+
 int gpdla_engine_process(gpdla_engine* e, const gpdla_spectra* sp, const gpdla_results* res) {
   if (!e || !sp || !res) return set_error(GPDLA_EINVAL, "null argument");
   const int64_t Q = sp->num_spectra;
@@ -332,8 +393,12 @@ int gpdla_engine_process(gpdla_engine* e, const gpdla_spectra* sp, const gpdla_r
   HIP_TRY(hipSetDevice(e->device));
   hipStream_t st = e->stream;
 
-  const int64_t QB = e->params.max_batch_spectra > 0 ? e->params.max_batch_spectra : 1024;
-  const int row = panel_row_doubles(e->K), es = scratch_doubles(e->K);
+  const int64_t QB = e->params.max_batch_spectra > 0 ? e->params.max_batch_spectra : (e->gemm ? 64 : 1024);
+  // panel doubles per slot: fused layout row, or the Khatri-Rao row of the panel-GEMM layout
+  const int64_t E = (int64_t)e->K * (e->K + 1) / 2;
+  const int64_t row = e->gemm ? E : panel_row_doubles(e->K);
+  const int es = e->gemm ? 0 : scratch_doubles(e->K);
+  const int64_t sc_max = std::min<int64_t>(e->S + 1, 16384);  // panel-GEMM sample chunk
   const int64_t blocks_x = (e->S + 1 + kSamplesPerBlock - 1) / kSamplesPerBlock;
 
   // pinned metadata for every batch of this call: per batch (QB+1) + 3*QB int64
@@ -355,7 +420,7 @@ int gpdla_engine_process(gpdla_engine* e, const gpdla_spectra* sp, const gpdla_r
     int64_t* h_sb = hm + (QB + 1);
     int64_t* h_lb = h_sb + QB;
     int64_t* h_cap = h_lb + QB;
-    int64_t slots = 0, lams = 0;
+    int64_t slots = 0, lams = 0, cap_max = 0;
     for (int64_t q = 0; q < nq; ++q) {
       h_off[q] = sp->offsets[q0 + q] - sp->offsets[q0];
       const int64_t lpix = sp->offsets[q0 + q + 1] - sp->offsets[q0 + q];
@@ -363,6 +428,7 @@ int gpdla_engine_process(gpdla_engine* e, const gpdla_spectra* sp, const gpdla_r
       h_sb[q] = slots;
       h_lb[q] = lams;
       h_cap[q] = cap;
+      cap_max = std::max(cap_max, cap);
       slots += cap;
       lams += cap + 8;
     }
@@ -373,9 +439,21 @@ int gpdla_engine_process(gpdla_engine* e, const gpdla_spectra* sp, const gpdla_r
     if ((rc = grow(&e->d_meta, &e->cap_meta, per_batch))) return rc;
     if ((rc = grow(&e->d_info, &e->cap_q, (size_t)QB))) return rc;
     // + one LDS row of slack: the staging DMA reads whole 1 KiB pieces (kernels.hip stage_chunk)
-    if ((rc = grow(&e->d_panel, &e->cap_slots, (size_t)slots * row + panel_lds_row_doubles(e->K)))) return rc;
+    if ((rc = grow(&e->d_panel, &e->cap_slots,
+                   (size_t)(slots * row + (e->gemm ? 0 : panel_lds_row_doubles(e->K)))))) return rc;
     if ((rc = grow(&e->d_lam, &e->cap_lam, (size_t)lams))) return rc;
-    if ((rc = grow(&e->d_scratch, &e->cap_scr, (size_t)blocks_x * nq * kSamplesPerBlock * es))) return rc;
+    if (e->gemm) {
+      if ((rc = grow(&e->d_pm, &e->cap_pm, (size_t)slots * e->K))) return rc;
+      if ((rc = grow(&e->d_srow, &e->cap_srow, (size_t)slots * 8))) return rc;
+      if ((rc = grow(&e->d_wg, &e->cap_wg, (size_t)(cap_max * sc_max)))) return rc;
+      if ((rc = grow(&e->d_wu, &e->cap_wu, (size_t)(cap_max * sc_max)))) return rc;
+      if ((rc = grow(&e->d_G, &e->cap_G, (size_t)(E * sc_max)))) return rc;
+      if ((rc = grow(&e->d_U, &e->cap_U, (size_t)(e->K * sc_max)))) return rc;
+      if ((rc = grow(&e->d_q1p, &e->cap_q1p, (size_t)(4 * sc_max)))) return rc;
+      if ((rc = grow(&e->d_ldp, &e->cap_ldp, (size_t)(4 * sc_max)))) return rc;
+    } else {
+      if ((rc = grow(&e->d_scratch, &e->cap_scr, (size_t)blocks_x * nq * kSamplesPerBlock * es))) return rc;
+    }
     if ((rc = grow(&e->d_smap, &e->cap_smap, (size_t)slots))) return rc;
     HIP_TRY(hipMemcpyAsync(e->d_meta, hm, per_batch * sizeof(int64_t), hipMemcpyHostToDevice, st));
 
@@ -448,6 +526,7 @@ int gpdla_engine_process(gpdla_engine* e, const gpdla_spectra* sp, const gpdla_r
     pa.pixel_spacing = e->params.pixel_spacing;
     pa.absorption_mode = e->params.absorption_mode;
     pa.info = e->d_info; pa.panel = e->d_panel; pa.lam_pad = e->d_lam; pa.slot_pixel = e->d_smap;
+    pa.k = e->K; pa.panel_m = e->d_pm; pa.srow = e->d_srow;
 
     LikelihoodArgs la{};
     la.q_count = (int32_t)nq;
@@ -464,11 +543,15 @@ int gpdla_engine_process(gpdla_engine* e, const gpdla_spectra* sp, const gpdla_r
 
     TimedLaunch t0{}, t1{}, t2{};
     if ((rc = record_start(e, &t0, 0))) return rc;
-    HIP_TRY(launch_prep(e->K, pa, st));
+    HIP_TRY(launch_prep(e->gemm ? 0 : e->K, pa, st));
     HIP_TRY(hipEventRecord(t0.stop, st));
     e->pending.push_back(t0);
     if ((rc = record_start(e, &t1, 1))) return rc;
-    HIP_TRY(launch_likelihood(e->K, la, st));
+    if (!e->gemm) {
+      HIP_TRY(launch_likelihood(e->K, la, st));
+    } else if ((rc = run_panel_gemm(e, nq, h_sb, h_lb, h_cap, sc_max, o_sll, ld, o_null, st))) {
+      return rc;
+    }
     HIP_TRY(hipEventRecord(t1.stop, st));
     e->pending.push_back(t1);
 

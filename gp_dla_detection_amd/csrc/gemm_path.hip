@@ -1,0 +1,203 @@
+// Panel-GEMM path for any rank k <= kGemmMaxK (BASELINE configs[4]: k = 50): the north star's
+// "MFMA for the n x k panel contraction" branch.  Per (spectrum, chunk of samples):
+//   weights_kernel    Voigt absorption x pixel terms (process_qsos.m:186-197) ->
+//                     Wg[slot][s] = a^2/d, Wu[slot][s] = a r/d, per-segment sum r^2/d, sum log d
+//   rocBLAS dgemm x2  Gram[s] = PG^T Wg[:, s] (Khatri-Rao panel, k(k+1)/2 columns) and
+//                     u[s] = M^T Wu[:, s]  (engine.hip)  -- log_mvnpdf_low_rank.m:13-23
+//   ldl_batch_kernel  augmented LDL^T of [[I + Gram, u], [u', sum r^2/d]] per sample -> logdet and
+//                     r'K^-1 r (log_mvnpdf_low_rank.m:24-32), one wave per sample.
+// Slot layout, neutral padding rows and sample order are those of the fused path (kernels.hip).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+
+#include "device_common.h"
+#include "internal.h"
+
+namespace gpdla {
+
+namespace {
+
+// One wave per segment (4 per block), lanes over 64 consecutive samples of the chunk; the wave
+// walks its segment's slots with the same register sliding window as the fused kernel.  Writes
+// are coalesced (sample-contiguous rows), slot scalars are wave-uniform loads.
+template <int NL>
+__global__ __launch_bounds__(256) void weights_kernel(WeightsArgs a) {
+  constexpr int kWingLds = 4 * ((3 * kWingStride + 3) / 4);
+  __shared__ __attribute__((aligned(16))) double tables[NL == 3 ? 3 * kCoreTable + kWingLds + 64 : 1];
+  const SpecInfo inf = a.info[a.q];
+  if (inf.J == 0) return;  // unusable spectrum: the LDL kernel writes NaN
+  const int lane = threadIdx.x & 63;
+  const int g = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int sl = blockIdx.x * 64 + lane;
+  const bool active = sl < a.sc;
+  const int64_t s = a.s0 + sl;
+  double* core_lds = tables;
+  double* wing_lds = tables + 3 * kCoreTable;
+  double* exp_lds = wing_lds + kWingLds;
+  if constexpr (NL == 3) {
+    for (int i = threadIdx.x; i < 3 * kCoreTable; i += 256) core_lds[i] = a.lines.buf[i];
+    if (threadIdx.x < 64) exp_lds[threadIdx.x] = a.lines.buf[kLineBufExp2 + threadIdx.x];
+    if (threadIdx.x < 3 * kWingStride) wing_lds[threadIdx.x] = a.lines.buf[kLineBufWing + threadIdx.x];
+    __syncthreads();
+  }
+  const int L = inf.L;
+  const int Ls = ((L + kChunkSteps - 1) / kChunkSteps) * kChunkSteps;
+  // null model (s == S) and idle lanes: N = 0, absorption exactly 1 (see kernels.hip)
+  const double off = (s < a.S) ? a.offsets[s] : 0.5;
+  const double N = (s < a.S) ? a.nhi[s] : 0.0;
+  const double zdla = inf.zmin + (inf.zmax - inf.zmin) * off;  // process_qsos.m:163-165
+  const double zfac = 1.0 / (1 + zdla);
+  double afac[3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) afac[j] = a.lines.buf[kLineBufFac + j] * zfac;
+  auto raw = [&](double lam) {
+    if constexpr (NL == 3) return raw_profile3(lam, afac, N, core_lds, wing_lds, exp_lds);
+    else return raw_profile(lam, zfac, N, a.num_lines, a.lines);
+  };
+  const double* lamp = a.lam_pad + (int64_t)g * L;
+  double w0 = raw(lamp[0]), w1 = raw(lamp[1]), w2 = raw(lamp[2]);
+  double w3 = raw(lamp[3]), w4 = raw(lamp[4]), w5 = raw(lamp[5]);
+  double q1 = 0.0, pm = 1.0;
+  int pe = 0;
+  const int64_t ldw = a.sc;
+  for (int t = 0; t < Ls; ++t) {
+    const int64_t slot = (int64_t)g * Ls + t;
+    const double* sr = a.srow + slot * 8;
+    const double lam = sr[0], y = sr[1], noise = sr[2], mu = sr[3], om2 = sr[4];
+    const double w6 = raw(lam);
+    double ab = w0 * kInstrumentProfile[0];  // voigt.c:297-299
+    ab = fma(w1, kInstrumentProfile[1], ab);
+    ab = fma(w2, kInstrumentProfile[2], ab);
+    ab = fma(w3, kInstrumentProfile[3], ab);
+    ab = fma(w4, kInstrumentProfile[4], ab);
+    ab = fma(w5, kInstrumentProfile[5], ab);
+    ab = fma(w6, kInstrumentProfile[6], ab);
+    w0 = w1; w1 = w2; w2 = w3; w3 = w4; w4 = w5; w5 = w6;
+    const double r = fma(-mu, ab, y);  // process_qsos.m:191-197, log_mvnpdf_low_rank.m:11-15
+    const double a2 = ab * ab;
+    const double d = fma(om2, a2, noise);
+    const double dinv = rcp_nr(d);
+    const double rd = r * dinv;
+    q1 = fma(r, rd, q1);
+    pm *= d;
+    if ((t & 3) == 3) {
+      int ex;
+      pm = frexp(pm, &ex);
+      pe += ex;
+    }
+    if (active) {
+      a.wg[slot * ldw + sl] = a2 * dinv;
+      a.wu[slot * ldw + sl] = ab * rd;
+    }
+  }
+  // slots past the 4 segments (capacity slack) are neutral rows of the panel: weight 0
+  for (int64_t slot = 4 * (int64_t)Ls + g; slot < a.cap; slot += 4) {
+    if (active) {
+      a.wg[slot * ldw + sl] = 0.0;
+      a.wu[slot * ldw + sl] = 0.0;
+    }
+  }
+  if (active) {
+    a.q1p[(int64_t)sl * 4 + g] = q1;
+    a.ldp[(int64_t)sl * 4 + g] = log(pm) + pe * kLn2;
+  }
+}
+
+// Augmented LDL^T per sample, one wave per sample (4 per block), matrix packed lower-triangular
+// in LDS: A(i, j), j <= i <= k, at i(i+1)/2 + j; row k is [u', sum r^2/d].  Right-looking: at
+// pivot p every lane updates a share of the trailing triangle (index table tri: element t ->
+// (row offset, column offset)); after the k pivots A(k, k) = r'D^-1 r - u'B^-1 u = r'K^-1 r.
+constexpr int kTriMax = kGemmMaxK * (kGemmMaxK + 1) / 2;
+constexpr int kPackedMax = (kGemmMaxK + 1) * (kGemmMaxK + 2) / 2;
+
+__device__ inline void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__global__ __launch_bounds__(256) void ldl_batch_kernel(LdlArgs a) {
+  __shared__ uint32_t tri[kTriMax];
+  __shared__ double mats[4][kPackedMax];
+  const int K = a.k;
+  const int T0 = K * (K + 1) / 2;
+  for (int t = threadIdx.x; t < T0; t += 256) {
+    int ai = (int)((sqrtf(8.0f * (float)t + 1.0f) - 1.0f) * 0.5f);
+    while ((ai + 1) * (ai + 2) / 2 <= t) ++ai;
+    while (ai * (ai + 1) / 2 > t) --ai;
+    tri[t] = ((uint32_t)ai << 16) | (uint32_t)(t - ai * (ai + 1) / 2);
+  }
+  __syncthreads();
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int sl = blockIdx.x * 4 + wave;
+  if (sl >= a.sc) return;  // wave-uniform; no block barrier below
+  const int64_t s = a.s0 + sl;
+  const SpecInfo inf = a.info[a.q];
+  auto emit = [&](double ll) {
+    if (lane != 0) return;
+    if (s == a.S) *a.ll_null = ll;
+    else if (a.sample_ll) a.sample_ll[a.perm[s]] = ll;
+  };
+  if (inf.J == 0) {  // no usable pixel: NaN outputs (as the fused path)
+    emit(NAN);
+    return;
+  }
+  double* A = mats[wave];
+  auto at = [&](int i, int j) -> double& { return A[i * (i + 1) / 2 + j]; };
+  const int64_t E = T0;
+  const double* Gs = a.G + (int64_t)sl * E;
+  int start = 0;
+  for (int r = 0; r < K; ++r) {  // Gram (r, c), r <= c, row-major upper -> A(c, r); B = I + Gram
+    for (int c = r + lane; c < K; c += 64) at(c, r) = Gs[start + (c - r)] + (c == r ? 1.0 : 0.0);
+    start += K - r;
+  }
+  for (int j = lane; j < K; j += 64) at(K, j) = a.U[(int64_t)sl * K + j];
+  const double* q = a.q1p + (int64_t)sl * 4;
+  const double* l4 = a.ldp + (int64_t)sl * 4;
+  if (lane == 0) at(K, K) = ((q[0] + q[1]) + q[2]) + q[3];
+  const double logdet_d = ((l4[0] + l4[1]) + l4[2]) + l4[3];
+  wave_sync();
+  double logdet_b = 0.0;
+  bool bad = false;
+  for (int p = 0; p < K; ++p) {
+    const double d = at(p, p);
+    bad |= !(d > 0.0);
+    logdet_b += log(d);
+    const double invd = 1.0 / d;
+    const int R = K - p, T = R * (R + 1) / 2;
+    for (int t = lane; t < T; t += 64) {
+      const uint32_t ab = tri[t];
+      const int i = p + 1 + (int)(ab >> 16), j = p + 1 + (int)(ab & 0xffff);
+      at(i, j) = fma(-at(i, p) * invd, at(j, p), at(i, j));
+    }
+    wave_sync();
+  }
+  const double quad = at(K, K);
+  double ll = -0.5 * (quad + (logdet_d + logdet_b) + inf.n * kLog2Pi);  // log_mvnpdf_low_rank.m:30-32
+  if (bad || !(fabs(ll) < INFINITY)) {
+    ll = NAN;
+    if (lane == 0) atomicOr(a.status, 1);
+  }
+  emit(ll);
+}
+
+}  // namespace
+
+hipError_t launch_weights(const WeightsArgs& a, hipStream_t s) {
+  const unsigned blocks = (unsigned)((a.sc + 63) / 64);
+  if (a.num_lines == 3)
+    hipLaunchKernelGGL(weights_kernel<3>, dim3(blocks), dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL(weights_kernel<0>, dim3(blocks), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_ldl_batch(const LdlArgs& a, hipStream_t s) {
+  if (a.k < 1 || a.k > kGemmMaxK) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(ldl_batch_kernel, dim3((unsigned)((a.sc + 3) / 4)), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+}  // namespace gpdla

@@ -86,9 +86,12 @@ struct PrepArgs {
   // params
   double min_lambda, max_lambda, lya, lyman_limit, min_z_cut, max_z_cut, pixel_spacing;
   int32_t absorption_mode;
+  int32_t k;                     // rank (read by the panel-GEMM layout, prep_kernel<0>)
   // outputs
   SpecInfo* info;
-  double* panel;
+  double* panel;                 // fused layout: [slots][kRow]; GEMM layout: [slots][k(k+1)/2]
+  double* panel_m;               // GEMM layout only: [slots][k] M rows
+  double* srow;                  // GEMM layout only: [slots][8] lam, y, noise, mu, om2, valid
   double* lam_pad;
   int32_t* slot_pixel;           // scratch map slot -> pixel (size = total slot capacity)
 };
@@ -106,6 +109,46 @@ constexpr size_t kLineBufDoubles = kLineBufExp2 + 64;
 struct LineArgs {
   const double* buf;   // device line buffer (layout above)
 };
+
+// ---- panel-GEMM path (any rank 1..kGemmMaxK; gemm_path.hip + rocBLAS dgemm in engine.hip)
+constexpr int kGemmMaxK = 64;
+
+struct WeightsArgs {
+  const SpecInfo* info;
+  int32_t q;                     // spectrum within the batch
+  const double* srow;            // this spectrum's slot scalars [cap][8]
+  const double* lam_pad;         // this spectrum's padded wavelengths
+  int64_t cap;                   // this spectrum's slot capacity (GEMM inner dimension)
+  const double* offsets;         // [S] ascending offsets
+  const double* nhi;             // [S]
+  int64_t S, s0;                 // chunk = sorted samples s0 .. s0 + sc - 1 (index S = null model)
+  int32_t sc;
+  int32_t num_lines;
+  LineArgs lines;
+  double* wg;                    // [cap][sc] a^2 / d
+  double* wu;                    // [cap][sc] a r / d
+  double* q1p;                   // [sc][4] per-segment sum r^2 / d
+  double* ldp;                   // [sc][4] per-segment sum log d
+};
+
+struct LdlArgs {
+  const SpecInfo* info;
+  int32_t q;
+  int32_t k;
+  const double* G;               // [sc][k(k+1)/2] Gram, row-major upper triangle per sample
+  const double* U;               // [sc][k]
+  const double* q1p;
+  const double* ldp;
+  int64_t S, s0;
+  int32_t sc;
+  const int32_t* perm;
+  double* sample_ll;             // this spectrum's row, or nullptr
+  double* ll_null;               // this spectrum's entry
+  int32_t* status;
+};
+
+hipError_t launch_weights(const WeightsArgs& a, hipStream_t s);
+hipError_t launch_ldl_batch(const LdlArgs& a, hipStream_t s);
 
 struct LikelihoodArgs {
   int32_t q_count;

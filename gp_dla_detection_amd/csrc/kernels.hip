@@ -8,211 +8,12 @@
 #include <cmath>
 #include <cstdint>
 
+#include "device_common.h"
 #include "internal.h"
-
-// Build-time variant switches (A/B experiments; defaults are the shipped configuration).
-#ifndef GPDLA_WAVES_PER_EU
-#define GPDLA_WAVES_PER_EU 2
-#endif
-#ifndef GPDLA_SCHED_FENCE
-#define GPDLA_SCHED_FENCE 1
-#endif
-#ifndef GPDLA_FAST_EXP
-#define GPDLA_FAST_EXP 1
-#endif
 
 namespace gpdla {
 
 namespace {
-
-constexpr double kLog2Pi = 1.83787706640934534;  // log_mvnpdf_low_rank.m:7
-constexpr double kLn2 = 0.693147180559945309417;
-
-// ---------------------------------------------------------------------------------------------
-// small device helpers
-// ---------------------------------------------------------------------------------------------
-__device__ inline double rcp_nr(double d) {
-  // v_rcp_f64 (~2^-26) refined by two Newton steps -> within 1 ulp of 1/d
-  double r = __builtin_amdgcn_rcp(d);
-  double e = fma(-d, r, 1.0);
-  r = fma(r, e, r);
-  e = fma(-d, r, 1.0);
-  return fma(r, e, r);
-}
-
-// exp(v) for v <= 0 (v = N * total, voigt.c:291): v = (64 m + j) ln2/64 + r, |r| <= ln2/128,
-// exp(v) = 2^m * 2^(j/64) * e^r with 2^(j/64) from a 64-entry LDS table (host-rounded from long
-// double) and e^r a degree-5 Taylor polynomial (truncation < 4e-17).  Underflows to +0 like exp.
-__device__ inline double exp_tab64(double v, const double* __restrict__ tab) {
-  constexpr double kInvL = 92.33248261689366;              // 64 / ln 2
-  constexpr double kLhi = 0.010830424695086549;           // ln2/64 to 33 bits (k*kLhi exact)
-  constexpr double kLlo = 1.162596423439437e-12;           // ln2/64 - kLhi
-  v = fmax(v, -1100.0);                                    // keeps k in int range; exp(-1100) = 0
-  const double k = __builtin_rint(v * kInvL);
-  double r = fma(-k, kLhi, v);
-  r = fma(-k, kLlo, r);
-  double p = fma(r, 1.0 / 120.0, 1.0 / 24.0);
-  p = fma(p, r, 1.0 / 6.0);
-  p = fma(p, r, 0.5);
-  p = fma(p, r, 1.0);
-  p = fma(p, r, 1.0);
-  const int ki = (int)k;
-  return __builtin_ldexp(p * tab[ki & 63], ki >> 6);
-}
-
-template <int SRC>
-__device__ inline double quad_bcast_c(double v) {
-  int lo = __double2loint(v), hi = __double2hiint(v);
-  lo = __builtin_amdgcn_mov_dpp(lo, SRC * 0x55, 0xF, 0xF, false);
-  hi = __builtin_amdgcn_mov_dpp(hi, SRC * 0x55, 0xF, 0xF, false);
-  return __hiloint2double(hi, lo);
-}
-
-// value of lane (quad_base + src) broadcast to the 4 lanes of each quad; src folds to a
-// constant after unrolling
-__device__ inline double quad_bcast(double v, int src) {
-  switch (src & 3) {
-    case 0: return quad_bcast_c<0>(v);
-    case 1: return quad_bcast_c<1>(v);
-    case 2: return quad_bcast_c<2>(v);
-    default: return quad_bcast_c<3>(v);
-  }
-}
-
-__device__ inline int wave_incl_scan(int v) {
-  const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    int t = __shfl_up(v, off);
-    if (lane >= off) v += t;
-  }
-  return v;
-}
-
-// exclusive block scan over 256 threads; returns exclusive prefix, total via *total
-__device__ inline int block_excl_scan(int v, int* lds4, int* total) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  int inc = wave_incl_scan(v);
-  if (lane == 63) lds4[wave] = inc;
-  __syncthreads();
-  int woff = 0, tot = 0;
-#pragma unroll
-  for (int w = 0; w < 4; ++w) {
-    int c = lds4[w];
-    if (w < wave) woff += c;
-    tot += c;
-  }
-  __syncthreads();
-  *total = tot;
-  return woff + inc - v;
-}
-
-__device__ inline double block_reduce_min(double v, double* lds4) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v = fmin(v, __shfl_xor(v, off));
-  if (lane == 0) lds4[wave] = v;
-  __syncthreads();
-  double r = fmin(fmin(lds4[0], lds4[1]), fmin(lds4[2], lds4[3]));
-  __syncthreads();
-  return r;
-}
-
-__device__ inline double block_reduce_max(double v, double* lds4) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v = fmax(v, __shfl_xor(v, off));
-  if (lane == 0) lds4[wave] = v;
-  __syncthreads();
-  double r = fmax(fmax(lds4[0], lds4[1]), fmax(lds4[2], lds4[3]));
-  __syncthreads();
-  return r;
-}
-
-__device__ inline double block_reduce_sum(double v, double* lds4) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-  if (lane == 0) lds4[wave] = v;
-  __syncthreads();
-  double r = (lds4[0] + lds4[1]) + (lds4[2] + lds4[3]);
-  __syncthreads();
-  return r;
-}
-
-// Gram pair e -> (r, c), row-major upper triangle (r <= c)
-template <int K>
-__device__ inline void gram_pair(int e, int& r, int& c) {
-  int rr = 0, start = 0;
-  while (rr < K - 1 && e >= start + (K - rr)) {
-    start += K - rr;
-    ++rr;
-  }
-  r = rr;
-  c = rr + (e - start);
-}
-
-template <int K>
-__device__ __host__ constexpr int gram_index(int r, int c) {
-  return r * K - r * (r - 1) / 2 + (c - r);
-}
-
-// numpy.interp-style linear interpolation index on a strictly increasing grid
-__device__ inline int interp_index(const double* xp, int G, double x) {
-  int lo = 0, hi = G - 1;  // invariant xp[lo] <= x < xp[hi] (x inside the grid)
-  while (hi - lo > 1) {
-    int mid = (lo + hi) >> 1;
-    if (xp[mid] <= x) lo = mid; else hi = mid;
-  }
-  return lo;
-}
-
-__device__ inline double interp_eval(const double* xp, const double* fp, int G, int j, double x) {
-  if (x >= xp[G - 1]) return fp[G - 1];
-  const double slope = (fp[j + 1] - fp[j]) / (xp[j + 1] - xp[j]);
-  return slope * (x - xp[j]) + fp[j];
-}
-
-// ---------------------------------------------------------------------------------------------
-// Voigt raw profile at one padded wavelength: exp(N * total), total = -sum_j lc_j V_j(v_j)
-// (voigt.c:282-292).  x_j = lambda * fac_j / (1+z) - c/(sigma sqrt 2) (voigt.c:278-279,287).
-// ---------------------------------------------------------------------------------------------
-constexpr double kC2 = kCcgs / (kSigma * 1.41421356237309504880);  // c / (sigma sqrt 2)
-
-// generic: any number of lines, core tables in global memory
-__device__ inline double raw_profile(double lam, double zfac, double N, int num_lines,
-                                     const LineArgs& L) {
-  double total = 0.0;
-  for (int j = 0; j < num_lines; ++j) {
-    const double x = fma(lam, L.buf[kLineBufFac + j] * zfac, -kC2);
-    total -= line_profile_eval(L.buf + (size_t)j * kCoreTable,
-                               L.buf + kLineBufWing + (size_t)j * kWingStride, x);
-  }
-  return exp(N * total);
-}
-
-// 3-line fast path (Lyman alpha, beta, gamma; set_parameters.m:63): the damping wing is
-// evaluated branch-free for every lane with its coefficients read from LDS by broadcast
-// (wing_lds), the core polynomial (LDS tables) only by the lanes with |x| < kCoreX.
-__device__ inline double raw_profile3(double lam, const double (&afac)[3], double N,
-                                      const double* __restrict__ core_lds,
-                                      const double* __restrict__ wing_lds,
-                                      const double* __restrict__ exp_lds) {
-  double total = 0.0;
-#pragma unroll
-  for (int j = 0; j < 3; ++j) {
-    const double x = fma(lam, afac[j], -kC2);
-    const double ax = fabs(x);
-    double f = wing_eval(wing_lds + j * kWingStride, x);
-    if (ax < kCoreX) f = core_eval(core_lds + j * kCoreTable, ax);
-    total -= f;
-  }
-#if GPDLA_FAST_EXP
-  return exp_tab64(N * total, exp_lds);
-#else
-  return exp(N * total);
-#endif
-}
 
 // ---------------------------------------------------------------------------------------------
 // prep: process_qsos.m:96-177 for one spectrum per block.  Builds the slot panel (interpolated
@@ -323,35 +124,25 @@ __global__ __launch_bounds__(256) void prep_kernel(PrepArgs a) {
   // steps t >= L that round each segment up to whole chunks are neutral rows (like masked pixels).
   const int Ls = L > 0 ? ((L + kChunkSteps - 1) / kChunkSteps) * kChunkSteps : kChunkSteps;
   for (int64_t j = wave; j < cap; j += 4) {
-    double* row = a.panel + (sb + j) * Lay::kRow;
     const int gg = (int)(j / Ls), t = (int)(j - (int64_t)gg * Ls);
     const int pos = (gg < 4 && t < L) ? gg * L + t : -1;
     const int pix = (pos >= 0 && pos < J) ? smap[pos] : -1;
     const double lam_lead = lam_pad[(pos >= 0 ? pos : j) + 2 * kWidth];  // any finite value if neutral
+    const int KK = K > 0 ? K : a.k;  // K == 0: panel-GEMM layout at runtime rank a.k
+    double sc[6] = {lam_lead, 0.0, 1.0, 0.0, 0.0, 0.0};  // lam, y, noise, mu, om2, valid (neutral)
+    const double* M0 = nullptr;
+    const double* M1 = nullptr;
+    double rest = 0.0, x0 = 0.0, x1 = 1.0;
+    bool at_end = false;
     if (pix >= 0) {
       const double lam = wl[pix];
-      const double rest = lam / (1 + z);
+      rest = lam / (1 + z);
       const int gi = interp_index(rest_g, G, rest);
-      const bool at_end = rest >= rest_g[G - 1];
-      const double* M0 = a.M_rowmajor + (int64_t)gi * K;
-      const double* M1 = a.M_rowmajor + (int64_t)(at_end ? gi : gi + 1) * K;
-      const double x0 = rest_g[gi], x1 = rest_g[at_end ? gi : gi + 1];
-      auto Mi = [&](int col) {
-        if (at_end) return a.M_rowmajor[(int64_t)(G - 1) * K + col];
-        const double slope = (M1[col] - M0[col]) / (x1 - x0);
-        return slope * (rest - x0) + M0[col];
-      };
-      for (int e = lane; e < 4 * Lay::kTiles; e += 64) {
-        double v = 0.0;
-        if (e < Lay::kNGram) {
-          int r, c;
-          gram_pair<K>(e, r, c);
-          v = Mi(r) * Mi(c);
-        } else if (e >= 4 * Lay::kGT && e - 4 * Lay::kGT < K) {
-          v = Mi(e - 4 * Lay::kGT);
-        }
-        row[(e & 3) * Lay::kJS + (e >> 2)] = v;
-      }
+      at_end = rest >= rest_g[G - 1];
+      M0 = a.M_rowmajor + (int64_t)gi * KK;
+      M1 = a.M_rowmajor + (int64_t)(at_end ? gi : gi + 1) * KK;
+      x0 = rest_g[gi];
+      x1 = rest_g[at_end ? gi : gi + 1];
       if (lane == 0) {
         const double mu = interp_eval(rest_g, a.mu, G, gi, rest);             // :139
         const double lom = interp_eval(rest_g, a.log_omega, G, gi, rest);     // :142
@@ -359,28 +150,67 @@ __global__ __launch_bounds__(256) void prep_kernel(PrepArgs a) {
         double om2 = exp(2 * lom);                                            // :143
         const double sf = 1 - exp(-a.tau_0 * pow(1 + lya_z, a.beta)) + a.c_0;  // :145
         om2 = om2 * (sf * sf);                                                // :147
-        row[Lay::kLam] = lam_lead;
-        row[Lay::kY] = a.flux[pb + pix];
-        row[Lay::kNoise] = a.noise[pb + pix];
-        row[Lay::kMu] = mu;
-        row[Lay::kOmega2] = om2;
-        row[Lay::kValid] = 1.0;
-      }
-    } else {
-      for (int e = lane; e < 4 * Lay::kTiles; e += 64) row[(e & 3) * Lay::kJS + (e >> 2)] = 0.0;
-      if (lane == 0) {
-        row[Lay::kLam] = lam_lead;
-        row[Lay::kY] = 0.0;
-        row[Lay::kNoise] = 1.0;
-        row[Lay::kMu] = 0.0;
-        row[Lay::kOmega2] = 0.0;
-        row[Lay::kValid] = 0.0;
+        sc[1] = a.flux[pb + pix];
+        sc[2] = a.noise[pb + pix];
+        sc[3] = mu;
+        sc[4] = om2;
+        sc[5] = 1.0;
       }
     }
-    // zero the remaining spare words
-    for (int w = lane; w < Lay::kRow; w += 64) {
-      const int jj = w / Lay::kJS, t = w % Lay::kJS;
-      if (t >= Lay::kTiles && !((jj == 0 || jj == 1 || jj == 2) && t < Lay::kTiles + 2)) row[w] = 0.0;
+    // M row at this pixel, process_qsos.m:140 (griddedInterpolant 'linear', per column)
+    auto Mi = [&](int col) {
+      if (at_end) return a.M_rowmajor[(int64_t)(G - 1) * KK + col];
+      const double slope = (M1[col] - M0[col]) / (x1 - x0);
+      return slope * (rest - x0) + M0[col];
+    };
+    if constexpr (K > 0) {
+      double* row = a.panel + (sb + j) * Lay::kRow;
+      for (int e = lane; e < 4 * Lay::kTiles; e += 64) {
+        double v = 0.0;
+        if (pix >= 0) {
+          if (e < Lay::kNGram) {
+            int r, c;
+            gram_pair<K>(e, r, c);
+            v = Mi(r) * Mi(c);
+          } else if (e >= 4 * Lay::kGT && e - 4 * Lay::kGT < K) {
+            v = Mi(e - 4 * Lay::kGT);
+          }
+        }
+        row[(e & 3) * Lay::kJS + (e >> 2)] = v;
+      }
+      if (lane == 0) {
+        row[Lay::kLam] = sc[0];
+        row[Lay::kY] = sc[1];
+        row[Lay::kNoise] = sc[2];
+        row[Lay::kMu] = sc[3];
+        row[Lay::kOmega2] = sc[4];
+        row[Lay::kValid] = sc[5];
+      }
+      // zero the remaining spare words
+      for (int w = lane; w < Lay::kRow; w += 64) {
+        const int jj = w / Lay::kJS, t2 = w % Lay::kJS;
+        if (t2 >= Lay::kTiles && !((jj == 0 || jj == 1 || jj == 2) && t2 < Lay::kTiles + 2)) row[w] = 0.0;
+      }
+    } else {
+      // panel-GEMM layout: Khatri-Rao row (row-major upper triangle, (r, c) at r KK - r(r-1)/2 +
+      // c - r), M row, and 8 slot scalars; all zero / neutral for masked and padding slots
+      const int64_t E = (int64_t)KK * (KK + 1) / 2;
+      double* pg = a.panel + (sb + j) * E;
+      double* pm = a.panel_m + (sb + j) * KK;
+      int start = 0;
+      for (int r = 0; r < KK; ++r) {
+        const double mr = pix >= 0 ? Mi(r) : 0.0;
+        for (int c = r + lane; c < KK; c += 64) pg[start + (c - r)] = pix >= 0 ? mr * Mi(c) : 0.0;
+        start += KK - r;
+      }
+      for (int c = lane; c < KK; c += 64) pm[c] = pix >= 0 ? Mi(c) : 0.0;
+      if (lane == 0) {
+        double* sr = a.srow + (sb + j) * 8;
+#pragma unroll
+        for (int w = 0; w < 6; ++w) sr[w] = sc[w];
+        sr[6] = 0.0;
+        sr[7] = 0.0;
+      }
     }
   }
 }
@@ -879,6 +709,7 @@ int panel_lds_row_doubles(int K) {
 }
 
 hipError_t launch_prep(int K, const PrepArgs& a, hipStream_t s) {
+  if (K == 0) return launch_prep_k<0>(a, s);  // panel-GEMM layout, rank a.k
 #define X(k) if (K == k) return launch_prep_k<k>(a, s);
   GPDLA_FOR_EACH_RANK(X)
 #undef X

@@ -24,21 +24,28 @@ def _model_struct(model: dict, keep: list) -> L.Model:
                    log_beta=float(np.ravel(model["log_beta"])[0]))
 
 
-def _params_struct(p: Parameters, max_batch_spectra: int = 0) -> L.Params:
+_PATHS = {"auto": L.PATH_AUTO, "fused": L.PATH_FUSED, "panel_gemm": L.PATH_PANEL_GEMM}
+
+
+def _params_struct(p: Parameters, max_batch_spectra: int = 0, path: str = "auto") -> L.Params:
     return L.Params(num_lines=p.num_lines, width=p.width, pixel_spacing=p.pixel_spacing,
                     min_lambda=p.min_lambda, max_lambda=p.max_lambda,
                     lya_wavelength=p.lya_wavelength, lyman_limit=p.lyman_limit,
                     min_z_cut=p.min_z_cut, max_z_cut=p.max_z_cut,
                     absorption_mode=(L.ABSORPTION_REFERENCE if p.absorption_mode == "reference"
                                      else L.ABSORPTION_UNMASKED),
-                    max_batch_spectra=max_batch_spectra)
+                    max_batch_spectra=max_batch_spectra, path=_PATHS[path])
 
 
 class Engine:
-    """One engine per device: resident model, DLA samples and line-profile tables."""
+    """One engine per device: resident model, DLA samples and line-profile tables.
+
+    ``path``: "auto" (fused single-kernel sweep for the compiled ranks 4 8 10 12 16 20 24, else the
+    panel-GEMM path), "fused", or "panel_gemm" (weights kernel + dgemm + batched LDL^T; ranks
+    1..64)."""
 
     def __init__(self, model: dict, samples: dict, params: Parameters | None = None,
-                 device: int = 0, max_batch_spectra: int = 0):
+                 device: int = 0, max_batch_spectra: int = 0, path: str = "auto"):
         self.lib = L.load()
         self.params = params or set_parameters(k=np.asarray(model["M"]).shape[1])
         if self.params.k != np.asarray(model["M"]).shape[1]:
@@ -50,7 +57,9 @@ class Engine:
         if off.size != nhi.size:
             raise ValueError("offset_samples and nhi_samples differ in length")
         ss = L.Samples(num_samples=off.size, offset_samples=L.ptr(off), nhi_samples=L.ptr(nhi))
-        ps = _params_struct(self.params, max_batch_spectra)
+        if path not in _PATHS:
+            raise ValueError(f"path must be one of {sorted(_PATHS)}")
+        ps = _params_struct(self.params, max_batch_spectra, path)
         h = C.c_void_p()
         L.check(self.lib.gpdla_engine_create(device, C.byref(ms), C.byref(ss), C.byref(ps), C.byref(h)))
         self._h = h

@@ -47,6 +47,12 @@ extern "C" {
 /* absorption-index handling (process_qsos.m:180,189) */
 #define GPDLA_ABSORPTION_REFERENCE 0 /* reproduce the quirk: absorption(1:n) of the m in-range values */
 #define GPDLA_ABSORPTION_UNMASKED 1  /* pair every unmasked pixel with its own profile value */
+/* Likelihood path.  AUTO = the fused single-kernel sweep for the compiled ranks
+ * (4 8 10 12 16 20 24), otherwise the panel-GEMM path (weights kernel + dgemm + batched LDL^T),
+ * which takes any rank 1..64 (BASELINE configs[4]: k = 50). */
+#define GPDLA_PATH_AUTO 0
+#define GPDLA_PATH_FUSED 1
+#define GPDLA_PATH_PANEL_GEMM 2
 
 /* Learned null model (learned_qso_model_<set>.mat, read at process_qsos.m:30-35).  Host memory. */
 typedef struct gpdla_model {
@@ -77,6 +83,7 @@ typedef struct gpdla_params {
   double min_z_cut, max_z_cut;   /* kms_to_z(3000) (set_parameters.m:65,69) */
   int32_t absorption_mode;       /* GPDLA_ABSORPTION_* */
   int32_t max_batch_spectra;     /* spectra per device batch; 0 = library default */
+  int32_t path;                  /* GPDLA_PATH_*: fused kernel or panel-GEMM (see below) */
 } gpdla_params;
 
 /* Preloaded spectra (preloaded_qsos.mat cells, process_qsos.m:46-61), CSR-packed.
