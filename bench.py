@@ -1,8 +1,10 @@
 #!/usr/bin/env python3
 """Benchmark: (spectrum x DLA-sample) log-evidence evaluations per second on MI355X.
 
-Workload (BASELINE.json configs[1]): 1024 synthetic spectra per GPU, n = 800 unmasked pixels,
-k = 20, S = 10^4 DLA samples, fp64.  One step = one pass of the hot path over the batch:
+Default workload (BASELINE.json configs[1], --workload c2): 1024 synthetic spectra per GPU,
+n = 800 unmasked pixels, k = 20, S = 10^4 DLA samples, fp64.  --workload c3 / c4 / c5 run the
+other configs (full DR12Q count on one GPU / split over the ranks; k = 50 with 10^5 samples on the
+panel-GEMM path).  One step = one pass of the hot path over the batch:
 spectrum preparation, the fused Voigt x low-rank-Gaussian likelihood for every (spectrum,
 sample) pair plus the null model, and the per-spectrum log-mean-exp.  Inputs are resident in HBM
 before timing starts; outputs (incl. the 1024 x 10^4 sample log-likelihoods) stay in HBM.
@@ -93,6 +95,20 @@ def cpu_baseline(model, samples, spectra, budget_s: float) -> dict:
                       "available); n=800, k=20, 3 lines"}
 
 
+# BASELINE.json configs.  c2 is the bench line the driver records.
+WORKLOADS = {
+    "c2": dict(spectra=1024, samples=10000, k=20, dr12q=False, scaling="weak",
+               label="configs[1]: 1024 synthetic spectra/GPU x 10^4 DLA samples, k=20, fp64"),
+    "c3": dict(spectra=162861, samples=10000, k=20, dr12q=True, scaling="weak",
+               label="configs[2]: full DR12Q count (162,861 DR12Q-shaped spectra) x 10^4 samples, k=20, fp64, 1 GPU"),
+    "c4": dict(spectra=162861, samples=10000, k=20, dr12q=True, scaling="strong",
+               label="configs[3]: full DR12Q count split over the ranks (spectrum shards), k=20, fp64"),
+    "c5": dict(spectra=128, samples=100000, k=50, dr12q=False, scaling="weak",
+               label="configs[4]: 128 spectra/GPU x 10^5 DLA samples, k=50 (panel-GEMM path; fp64, "
+                     "above the config's fp32)"),
+}
+
+
 # rocprofv3 summary of this workload (tools/profile.sh + tools/summarize_profile.py), committed
 PROFILE_SUMMARY = ROOT / "profiles" / "r1d_summary.json"
 
@@ -115,9 +131,13 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--spectra", type=int, default=1024, help="spectra per GPU")
-    ap.add_argument("--samples", type=int, default=10000)
-    ap.add_argument("--k", type=int, default=20)
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c2",
+                    help="BASELINE.json configs: c2 = configs[1] (default bench line), c3 = configs[2] "
+                         "(full DR12Q, 1 GPU), c4 = configs[3] (full DR12Q split over the ranks), "
+                         "c5 = configs[4] (k=50, 10^5 samples)")
+    ap.add_argument("--spectra", type=int, default=None, help="override: spectra per GPU (c2/c5)")
+    ap.add_argument("--samples", type=int, default=None, help="override: DLA samples")
+    ap.add_argument("--k", type=int, default=None, help="override: rank")
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU-baseline work (0 = skip)")
     args = ap.parse_args()
 
@@ -136,10 +156,24 @@ def main():
     from gp_dla_detection_amd.engine import Engine
     from gp_dla_detection_amd.parameters import set_parameters
 
+    wl = dict(WORKLOADS[args.workload])
+    for key in ("spectra", "samples", "k"):
+        if getattr(args, key) is not None:
+            wl[key] = getattr(args, key)
+    args.k, args.samples = wl["k"], wl["samples"]
     model = syn.make_model(k=args.k)
     samples = syn.make_samples(args.samples)
-    Q = args.spectra
-    spectra = [syn.make_spectrum(model, rank * Q + q) for q in range(Q)]
+    if wl["dr12q"]:
+        # full DR12Q count (162,861) of DR12Q-shaped spectra (n ~ 270-1250): a pool of 4096
+        # distinct synthetic spectra tiled to the count; c3 = all on one GPU, c4 = split over ranks
+        total = wl["spectra"]
+        lo, hi = (0, total) if args.workload == "c3" else (total * rank // world, total * (rank + 1) // world)
+        Q = hi - lo
+        pool = syn.make_dr12q_like_spectra(model, 4096, seed=12, mask_fraction=0.0)
+        spectra = [pool[i % len(pool)] for i in range(lo, hi)]
+    else:
+        Q = wl["spectra"]
+        spectra = [syn.make_spectrum(model, rank * Q + q) for q in range(Q)]
     packed = syn.pack_spectra(spectra)
     # CPU baseline first, while no process has touched the GPU (its workers are spawned)
     cpu = None
@@ -154,6 +188,7 @@ def main():
     o_n = L.DeviceArray(local_rank, Q, np.int32)
 
     eng = Engine(model, samples, set_parameters(k=args.k), device=local_rank)
+    path = "fused" if args.k in (4, 8, 10, 12, 16, 20, 24) else "panel-GEMM"
 
     def step():
         eng.process_device(packed["offsets"], t["wavelengths"].ptr, t["flux"].ptr, t["noise_variance"].ptr,
@@ -180,8 +215,8 @@ def main():
         elapsed = float(tt.item())
 
     # sanity: finite outputs and the calc_cddf.py:246 normalisation invariant
-    sll = o_s.numpy()
-    lld = o_dla.numpy()
+    sll = o_s.numpy(rows=2048)  # the check covers the leading spectra (c3/c4 outputs are 13 GB)
+    lld = o_dla.numpy()[: sll.shape[0]]
     npix = o_n.numpy()
     ok = bool(np.all(np.isfinite(sll)) and np.all(np.isfinite(lld)))
     inv = np.exp(sll - (lld[:, None] + np.log(S))).sum(axis=1)
@@ -207,17 +242,20 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": wl["scaling"],
         "vs_baseline": None,
         "dtype": "f64",
-        "data": "synthetic (seeded; SURVEY.md 8d model/spectra, unscrambled Halton samples)",
-        "config": {"workload": f"configs[1]: {Q} spectra/GPU x {S} DLA samples, n={n_mean:.0f}, k={args.k}, "
-                               f"3 Lyman lines, fp64", "spectra_per_gpu": Q, "num_samples": S,
-                   "k": args.k, "n_pixels": n_mean, "parallelism": f"spectrum-shard x{world}"},
+        "data": "synthetic (seeded; SURVEY.md 8d model/spectra, unscrambled Halton samples)"
+                + ("; DR12Q-shaped pool of 4096 spectra tiled to the count" if wl["dr12q"] else ""),
+        "config": {"workload": f"{wl['label']}; this rank: {Q} spectra, mean n={n_mean:.0f}, 3 Lyman lines",
+                   "spectra_per_gpu": Q, "num_samples": S, "k": args.k, "n_pixels": n_mean,
+                   "likelihood_path": path, "parallelism": f"spectrum-shard x{world}"},
         "roofline": {"bound": "mfma", "achieved": achieved_tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved_tf / FP64_PEAK_TFLOPS, "traffic": traffic,
                      "traffic_source": traffic_src,
-                     "kernel": "likelihood_kernel<20>", "avg_launch_ms": avg_ms,
+                     "kernel": (f"likelihood_kernel<{args.k}>" if path == "fused"
+                                else "weights_kernel + rocBLAS dgemm + ldl_batch_kernel (per batch)"),
+                     "avg_launch_ms": avg_ms,
                      "flops_per_eval": algorithmic_flops_per_eval(n_mean, args.k),
                      "evals_per_launch": evals_per_launch},
         "hbm_effective": {"achieved": eff_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -164,10 +164,12 @@ class DeviceArray:
         check(load().gpdla_memcpy_htod(device, C.c_void_p(out.ptr), arr.ctypes.data_as(C.c_void_p), out.nbytes))
         return out
 
-    def numpy(self):
+    def numpy(self, rows: int | None = None):
+        """Copy to host; ``rows`` limits the copy to the leading rows (C order)."""
         import numpy as np
-        out = np.empty(self.shape, dtype=self.dtype)
-        check(load().gpdla_memcpy_dtoh(self.device, out.ctypes.data_as(C.c_void_p), C.c_void_p(self.ptr), self.nbytes))
+        shape = self.shape if rows is None else (min(rows, self.shape[0]),) + self.shape[1:]
+        out = np.empty(shape, dtype=self.dtype)
+        check(load().gpdla_memcpy_dtoh(self.device, out.ctypes.data_as(C.c_void_p), C.c_void_p(self.ptr), out.nbytes))
         return out
 
     def free(self):
