@@ -1,0 +1,817 @@
+"""MATLAB v7.3 ``.mat`` files (HDF5 behind a 512-byte MATLAB user block), in numpy only.
+
+The reference saves its result with ``save(filename, variables_to_save{:}, '-v7.3')``
+(process_qsos.m:249) and loads its inputs with ``load`` from v7.3 files written by the same
+pipeline (process_qsos.m:4,30-50).  ``sample_log_likelihoods_dla`` is Q x S doubles: 13.0 GB at
+full DR12Q, far over the 2 GB per-variable limit of MATLAB v5 files, and h5py is
+not installed on the GPU box.  So this module writes and reads the HDF5 subset MATLAB uses,
+directly:
+
+writer (``savemat73``)
+  superblock v0 at file offset 512 (base address 512, the layout libhdf5 itself writes for a
+  user block), old-style groups (v1 B-tree + symbol-table nodes + local heap), v1 object
+  headers, contiguous datasets.  Every variable carries MATLAB's ``MATLAB_class`` attribute
+  (plus ``MATLAB_int_decode`` for logical/char, ``MATLAB_empty`` for empties); cell arrays are
+  object-reference datasets into ``#refs#`` as MATLAB writes them.  Array data is laid out
+  MATLAB-style: a MATLAB r x c matrix is HDF5 dims (c, r), column-major bytes.  A variable may be
+  a ``LazyArray`` whose bytes are streamed into a memory map of the file after the metadata is
+  written (how process.save_processed_qsos writes the 13 GB sample array straight from the
+  spectrum-major engine output without a second host copy of it transposed).
+
+reader (``loadmat73``)
+  superblock v0-v3, object headers v1/v2 with continuations, symbol-table and compact link
+  groups, contiguous / compact / chunked (v1 B-tree) layouts with the deflate, shuffle and
+  fletcher32 filters (MATLAB compresses v7.3 variables by default), fixed/float/string/
+  reference/compound(complex) types, attributes, and MATLAB class decoding (double, single,
+  integers, logical, char, cell, struct, empty).
+
+What h5py sees in a file written here matches what it sees in MATLAB's: a Q-vector is (1, Q),
+``sample_log_likelihoods_dla`` is (S, Q) (calc_cddf.py:61-64,92,98).
+"""
+from __future__ import annotations
+
+import os
+import struct
+import time
+import zlib
+from dataclasses import dataclass
+from typing import Callable
+
+import numpy as np
+
+UNDEF = 0xFFFFFFFFFFFFFFFF
+SIGNATURE = b"\x89HDF\r\n\x1a\n"
+USERBLOCK = 512
+LEAF_K = 4          # group leaf node K: a symbol-table node holds 2K entries (libhdf5 default)
+INTERNAL_K = 16     # group internal node K: a B-tree node holds 2K children (libhdf5 default)
+_STREAM_BYTES = 1 << 26  # arrays at least this large are streamed into the file map
+
+_MATLAB_CLASS = {np.dtype(np.float64): "double", np.dtype(np.float32): "single",
+                 np.dtype(np.int8): "int8", np.dtype(np.uint8): "uint8",
+                 np.dtype(np.int16): "int16", np.dtype(np.uint16): "uint16",
+                 np.dtype(np.int32): "int32", np.dtype(np.uint32): "uint32",
+                 np.dtype(np.int64): "int64", np.dtype(np.uint64): "uint64"}
+_CLASS_DTYPE = {v: k for k, v in _MATLAB_CLASS.items()}
+
+
+def _pad8(b: bytes) -> bytes:
+    return b + b"\0" * (-len(b) % 8)
+
+
+# ============================================================================ writer
+@dataclass
+class LazyArray:
+    """A numeric variable whose bytes are produced after the file layout is fixed.
+
+    ``shape`` is the MATLAB shape (e.g. (Q, S)); ``fill(view)`` receives a writable
+    array of that MATLAB shape and dtype (a Fortran-ordered view of the file's bytes) and must
+    assign every element."""
+    shape: tuple
+    dtype: np.dtype
+    fill: Callable[[np.ndarray], None]
+
+
+def _dt_message(dt: np.dtype) -> bytes:
+    dt = np.dtype(dt)
+    if dt.kind == "f":
+        if dt.itemsize == 8:
+            props = struct.pack("<HHBBBBI", 0, 64, 52, 11, 0, 52, 1023)
+            bits = (0x20, 63, 0)
+        elif dt.itemsize == 4:
+            props = struct.pack("<HHBBBBI", 0, 32, 23, 8, 0, 23, 127)
+            bits = (0x20, 31, 0)
+        else:
+            raise TypeError(f"unsupported float width {dt.itemsize}")
+        return bytes([0x11, *bits]) + struct.pack("<I", dt.itemsize) + props
+    if dt.kind in "iub":
+        signed = 0x08 if dt.kind == "i" else 0
+        return bytes([0x10, signed, 0, 0]) + struct.pack("<IHH", dt.itemsize, 0, 8 * dt.itemsize)
+    raise TypeError(f"unsupported dtype {dt}")
+
+
+def _dt_string(n: int) -> bytes:
+    return bytes([0x13, 0x00, 0, 0]) + struct.pack("<I", n)      # fixed, null-terminated ASCII
+
+
+_DT_OBJREF = bytes([0x17, 0x00, 0, 0]) + struct.pack("<I", 8)
+
+
+def _dataspace(dims) -> bytes:
+    return bytes([1, len(dims), 0, 0, 0, 0, 0, 0]) + b"".join(struct.pack("<Q", int(d)) for d in dims)
+
+
+def _attr_message(name: str, value) -> bytes:
+    nm = name.encode() + b"\0"
+    if isinstance(value, str):
+        raw = value.encode("ascii")
+        dt, ds, data = _dt_string(len(raw)), _dataspace(()), raw
+    else:
+        arr = np.asarray(value)
+        dt, ds, data = _dt_message(arr.dtype), _dataspace(()), arr.astype(arr.dtype.newbyteorder("<")).tobytes()
+    body = struct.pack("<BBHHH", 1, 0, len(nm), len(dt), len(ds)) + _pad8(nm) + _pad8(dt) + _pad8(ds) + data
+    return _pad8(body)
+
+
+def _object_header(messages: list[tuple[int, bytes]]) -> bytes:
+    body = b"".join(struct.pack("<HHB3x", t, len(m), 0) + m for t, m in messages)
+    return struct.pack("<BBHII4x", 1, 0, len(messages), 1, len(body)) + body
+
+
+class _Node:
+    """One object to lay out: a dataset (data bytes or lazy) or a group (children)."""
+
+    def __init__(self, name, kind, **kw):
+        self.name, self.kind = name, kind
+        self.__dict__.update(kw)
+        self.addr = None
+
+
+def _matlab_node(name: str, value, refs: list) -> _Node:
+    """Map a Python/numpy value to MATLAB's HDF5 representation."""
+    attrs: list = []
+    if isinstance(value, LazyArray):
+        dt = np.dtype(value.dtype)
+        return _Node(name, "dataset", dims=tuple(reversed(value.shape)), dtype=dt, data=None,
+                     lazy=value, attrs=[("MATLAB_class", _MATLAB_CLASS[dt])])
+    if isinstance(value, dict):
+        # MATLAB scalar struct: a group with MATLAB_class "struct", one member per field (this is
+        # also the side format for the catalogue's containers.Map variables, SURVEY.md 7 viii)
+        kids = [_matlab_node(k, v, refs) for k, v in value.items()]
+        return _Node(name, "group", entries=kids, attrs=[("MATLAB_class", "struct")])
+    if isinstance(value, str):
+        codes = np.frombuffer(value.encode("utf-16-le"), dtype="<u2") if value else np.zeros(0, "<u2")
+        arr, cls = codes.reshape(1, -1), "char"
+        attrs.append(("MATLAB_int_decode", np.int32(2)))
+    elif isinstance(value, (list, tuple)) or (isinstance(value, np.ndarray) and value.dtype == object):
+        if isinstance(value, (list, tuple)):
+            cells = np.empty(len(value), dtype=object)
+            for i, v in enumerate(value):
+                cells[i] = v
+        else:
+            cells = value
+        if cells.ndim == 1:
+            cells = cells.reshape(-1, 1)                    # MATLAB n x 1 cell (like preload_qsos)
+        targets = []
+        for v in cells.ravel(order="F"):
+            idx = len(refs)
+            refs.append(None)                               # reserve the name before recursing
+            refs[idx] = child = _matlab_node(_refname(idx), v, refs)
+            targets.append(child)
+        if not targets:
+            return _empty_node(name, cells.shape, "cell")
+        return _Node(name, "dataset", dims=tuple(reversed(cells.shape)), dtype=None, ref_targets=targets,
+                     data=None, lazy=None, attrs=[("MATLAB_class", "cell")])
+    else:
+        arr = np.asarray(value)
+        if arr.dtype == bool:
+            arr, cls = arr.astype(np.uint8), "logical"
+            attrs.append(("MATLAB_int_decode", np.int32(1)))
+        elif arr.dtype.kind in "iuf" and arr.dtype in _MATLAB_CLASS:
+            cls = _MATLAB_CLASS[arr.dtype]
+        elif arr.dtype.kind in "iu":
+            arr, cls = arr.astype(np.int64), "int64"
+        else:
+            raise TypeError(f"{name}: cannot store dtype {arr.dtype} in a MATLAB file")
+        if arr.ndim == 0:
+            arr = arr.reshape(1, 1)
+        elif arr.ndim == 1:
+            arr = arr.reshape(-1, 1)                          # MATLAB column vector (oned_as column)
+    if arr.size == 0:
+        return _empty_node(name, arr.shape, cls, extra=attrs)
+    if arr.nbytes >= _STREAM_BYTES:
+        # large: copy straight into the file map in row blocks (no transposed host copy)
+        src = arr
+
+        def fill(view, src=src):
+            step = max(1, (_STREAM_BYTES // 4) // max(1, src[0].nbytes))
+            for a in range(0, src.shape[0], step):
+                view[a:a + step] = src[a:a + step]
+
+        return _Node(name, "dataset", dims=tuple(reversed(arr.shape)), dtype=arr.dtype, data=None,
+                     lazy=LazyArray(arr.shape, arr.dtype, fill), attrs=[("MATLAB_class", cls)] + attrs)
+    data = np.asfortranarray(arr)
+    return _Node(name, "dataset", dims=tuple(reversed(arr.shape)), dtype=data.dtype, data=data, lazy=None,
+                 attrs=[("MATLAB_class", cls)] + attrs)
+
+
+def _empty_node(name, shape, cls, extra=()):
+    # MATLAB stores an empty array as its dimensions (uint64) plus MATLAB_empty = 1
+    dims = np.array(shape if len(shape) >= 2 else (0, 0), dtype=np.uint64)
+    return _Node(name, "dataset", dims=(dims.size,), dtype=np.dtype(np.uint64), data=dims, lazy=None,
+                 attrs=[("MATLAB_class", cls), ("MATLAB_empty", np.uint8(1))] + list(extra))
+
+
+def _refname(i: int) -> str:
+    """MATLAB's #refs# naming: a, b, ..., z, ba, bb, ... (base 26 on the letters a-z)."""
+    s = ""
+    while True:
+        s = chr(ord("a") + i % 26) + s
+        i //= 26
+        if i == 0:
+            return s
+
+
+def _dataset_header(node: _Node, data_addr: int) -> bytes:
+    if getattr(node, "ref_targets", None) is not None:
+        dt, nbytes = _DT_OBJREF, 8 * len(node.ref_targets)
+    else:
+        dt = _dt_message(node.dtype)
+        nbytes = int(np.prod(node.dims)) * node.dtype.itemsize
+    msgs = [(0x0001, _pad8(_dataspace(node.dims))), (0x0003, _pad8(dt)),
+            (0x0008, _pad8(bytes([3, 1]) + struct.pack("<QQ", data_addr, nbytes)))]
+    msgs += [(0x000C, _attr_message(k, v)) for k, v in node.attrs]
+    return _object_header(msgs)
+
+
+def _group_header(node: _Node, btree: int, heap: int) -> bytes:
+    msgs = [(0x0011, struct.pack("<QQ", btree, heap))]
+    msgs += [(0x000C, _attr_message(k, v)) for k, v in node.attrs]
+    return _object_header(msgs)
+
+
+def _group_blocks(entries: list[_Node]):
+    """Heap + symbol-table nodes + B-tree for a group; returns sizes so the layout can be fixed
+    before addresses are known, and an emitter that encodes them once they are."""
+    entries = sorted(entries, key=lambda e: e.name.encode())
+    heap_data = bytearray(b"\0" * 8)                              # offset 0: the empty name
+    name_off = {}
+    for e in entries:
+        name_off[e.name] = len(heap_data)
+        heap_data += _pad8(e.name.encode() + b"\0")
+    snods = [entries[i:i + 2 * LEAF_K] for i in range(0, len(entries), 2 * LEAF_K)] or [[]]
+    snod_size = 8 + 2 * LEAF_K * 40
+    node_size = 24 + 2 * INTERNAL_K * 8 + (2 * INTERNAL_K + 1) * 8
+    # B-tree levels: level 0 over the SNODs, higher levels over nodes, until one root
+    levels = []
+    count = len(snods)
+    while True:
+        n_nodes = -(-count // (2 * INTERNAL_K))
+        levels.append(n_nodes)
+        if n_nodes == 1:
+            break
+        count = n_nodes
+    return entries, bytes(heap_data), name_off, snods, snod_size, node_size, levels
+
+
+class _Layout:
+    def __init__(self):
+        self.pos = 0
+        self.blobs: list[tuple[int, bytes]] = []
+
+    def alloc(self, size: int, align: int = 8) -> int:
+        self.pos += -self.pos % align
+        a = self.pos
+        self.pos += size
+        return a
+
+
+def savemat73(path: str, variables: dict, created: str | None = None) -> None:
+    """Write ``variables`` (name -> numpy array / scalar / str / list(cell) / LazyArray) as a
+    MATLAB v7.3 file.  1-D arrays become MATLAB column vectors (process_qsos.m's nan(Q, 1))."""
+    refs: list = []
+    top = [_matlab_node(name, val, refs) for name, val in variables.items()]
+    root = _Node("/", "group", entries=list(top), attrs=[])
+    if refs:
+        root.entries.append(_Node("#refs#", "group", entries=refs, attrs=[]))
+    groups, datasets = [], []
+
+    def collect(g):
+        groups.append(g)
+        for e in g.entries:
+            (collect(e) if e.kind == "group" else datasets.append(e))
+
+    collect(root)
+    L = _Layout()
+    sb_addr = L.alloc(96)
+    # pass 1: addresses of every metadata structure (sizes do not depend on addresses)
+    gmeta = []
+    for gnode in groups:
+        entries_sorted, heap_data, name_off, snods, snod_size, node_size, levels = _group_blocks(gnode.entries)
+        g = dict(entries=entries_sorted, heap_data=heap_data, name_off=name_off, snods=snods)
+        g["ohdr"] = L.alloc(len(_group_header(gnode, 0, 0)))
+        g["heap"] = L.alloc(32)
+        g["heap_data_addr"] = L.alloc(len(heap_data))
+        g["snod_addr"] = [L.alloc(snod_size) for _ in snods]
+        g["levels"] = [[L.alloc(node_size) for _ in range(n)] for n in levels]
+        gnode.addr, gnode.g, g["node"] = g["ohdr"], g, gnode
+        gmeta.append(g)
+    rg = gmeta[0]
+    for n in datasets:
+        n.addr = L.alloc(len(_dataset_header(n, 0)))
+    data_addr = {}
+
+    def nbytes(n):
+        if getattr(n, "ref_targets", None) is not None:
+            return 8 * len(n.ref_targets)
+        return int(np.prod(n.dims)) * n.dtype.itemsize
+
+    for n in datasets:                      # eager data first, lazy (large) regions last
+        if n.lazy is None:
+            data_addr[id(n)] = L.alloc(max(nbytes(n), 1))
+    meta_end = L.pos
+    for n in datasets:
+        if n.lazy is not None:
+            data_addr[id(n)] = L.alloc(max(nbytes(n), 1), align=4096)
+    eof = L.pos
+    # pass 2: encode the metadata and the eager data
+    img = bytearray(meta_end)
+
+    def put(addr, b):
+        img[addr:addr + len(b)] = b
+
+    sb = SIGNATURE + bytes([0, 0, 0, 0, 0, 8, 8, 0]) + struct.pack("<HHI", LEAF_K, INTERNAL_K, 0)
+    sb += struct.pack("<QQQQ", USERBLOCK, UNDEF, USERBLOCK + eof, UNDEF)
+    sb += struct.pack("<QQII", 0, rg["ohdr"], 1, 0) + struct.pack("<QQ", rg["levels"][-1][0], rg["heap"])
+    put(sb_addr, sb)
+    for g in gmeta:
+        put(g["ohdr"], _group_header(g["node"], g["levels"][-1][0], g["heap"]))
+        # free-list head 1 = H5HL_FREE_NULL (no free block)
+        put(g["heap"], b"HEAP" + bytes(4) + struct.pack("<QQQ", len(g["heap_data"]), 1, g["heap_data_addr"]))
+        put(g["heap_data_addr"], g["heap_data"])
+        for sn_addr, sn in zip(g["snod_addr"], g["snods"]):
+            b = b"SNOD" + bytes([1, 0]) + struct.pack("<H", len(sn))
+            for e in sn:
+                if e.kind == "group":
+                    b += struct.pack("<QQII", g["name_off"][e.name], e.addr, 1, 0)
+                    b += struct.pack("<QQ", e.g["levels"][-1][0], e.g["heap"])
+                else:
+                    b += struct.pack("<QQII", g["name_off"][e.name], e.addr, 0, 0) + bytes(16)
+            put(sn_addr, b)
+        # B-tree: level-0 children are the SNODs; key i+1 = heap offset of the last name under child i
+        children = g["snod_addr"]
+        child_last = [g["name_off"][sn[-1].name] if sn else 0 for sn in g["snods"]]
+        per = 2 * INTERNAL_K
+        for level, nodes in enumerate(g["levels"]):
+            new_last = []
+            for j, node_addr in enumerate(nodes):
+                ch = children[j * per:(j + 1) * per]
+                lk = child_last[j * per:(j + 1) * per]
+                b = b"TREE" + bytes([0, level]) + struct.pack("<H", len(ch)) + struct.pack("<QQ", UNDEF, UNDEF)
+                b += struct.pack("<Q", 0)
+                for c, k in zip(ch, lk):
+                    b += struct.pack("<QQ", c, k)
+                put(node_addr, b)
+                new_last.append(lk[-1])
+            children, child_last = nodes, new_last
+    for n in datasets:
+        put(n.addr, _dataset_header(n, data_addr[id(n)]))
+        if getattr(n, "ref_targets", None) is not None:
+            put(data_addr[id(n)], np.array([t.addr for t in n.ref_targets], dtype="<u8").tobytes())
+        elif n.data is not None:
+            put(data_addr[id(n)], np.ascontiguousarray(n.data.ravel(order="F")).astype(
+                n.data.dtype.newbyteorder("<"), copy=False).tobytes())
+    hdr = (f"MATLAB 7.3 MAT-file, Platform: GLNXA64, Created on: "
+           f"{created or time.strftime('%a %b %d %H:%M:%S %Y')} HDF5 schema 1.00 .").encode()
+    ub = hdr.ljust(116, b" ")[:116] + bytes(8) + struct.pack("<H", 0x0200) + b"IM"
+    ub = ub.ljust(USERBLOCK, b"\0")
+    lazies = [n for n in datasets if n.lazy is not None]
+    with open(path, "wb") as f:
+        f.write(ub)
+        f.write(bytes(img))
+        f.truncate(USERBLOCK + eof)     # lazy regions: sparse until filled through the memory map
+    for n in lazies:
+        dt = np.dtype(n.dtype).newbyteorder("<")
+        mm = np.memmap(path, dtype=dt, mode="r+", offset=USERBLOCK + data_addr[id(n)],
+                       shape=n.dims)                         # HDF5 (C-order) view
+        n.lazy.fill(mm.T)                                    # = MATLAB shape, column-major
+        mm.flush()
+        del mm
+
+
+# ============================================================================ reader
+class _Reader:
+    def __init__(self, path: str):
+        self.f = open(path, "rb")
+        self.mm = np.memmap(path, dtype=np.uint8, mode="r")
+        self.base = self._find_superblock()
+
+    def close(self):
+        del self.mm
+        self.f.close()
+
+    def read(self, addr: int, n: int, absolute: bool = False) -> bytes:
+        a = addr if absolute else self.base + addr
+        return self.mm[a:a + n].tobytes()
+
+    def _find_superblock(self) -> int:
+        off = 0
+        while off + 8 <= self.mm.size:
+            if self.mm[off:off + 8].tobytes() == SIGNATURE:
+                ver = int(self.mm[off + 8])
+                if ver in (0, 1):
+                    so, sl = int(self.mm[off + 13]), int(self.mm[off + 14])
+                    if (so, sl) != (8, 8):
+                        raise ValueError("only 8-byte offsets/lengths are supported")
+                    # addresses are relative to the superblock (libhdf5 moves the base there)
+                    p = off + 24 + (4 if ver == 1 else 0)
+                    ent = self.mm[p + 32:p + 72].tobytes()        # root symbol-table entry
+                    self.root_ohdr = struct.unpack("<Q", ent[8:16])[0]
+                    return off
+                if ver in (2, 3):
+                    p = off + 12
+                    self.root_ohdr = struct.unpack("<QQQQ", self.mm[p:p + 32].tobytes())[3]
+                    return off
+                raise ValueError(f"unsupported superblock version {ver}")
+            off = 512 if off == 0 else off * 2
+        raise ValueError("not an HDF5 file")
+
+    # ------------------------------------------------------------------ object headers
+    def messages(self, addr: int) -> list[tuple[int, bytes]]:
+        head = self.read(addr, 16)
+        out = []
+        if head[:4] == b"OHDR":
+            ver, flags = head[4], head[5]
+            p = 6 + (16 if flags & 0x20 else 0) + (4 if flags & 0x10 else 0)
+            sz_bytes = 1 << (flags & 3)
+            hdr = self.read(addr, p + sz_bytes)
+            chunk0 = int.from_bytes(hdr[p:p + sz_bytes], "little")
+            start = addr + p + sz_bytes
+            chunks = [(start, chunk0, True)]
+            track = bool(flags & 0x04)
+            while chunks:
+                a, n, first = chunks.pop(0)
+                buf = self.read(a, n)
+                q = 0 if first else 4  # continuation chunks start with "OCHK"
+                end = n - 4            # checksum
+                while q + 4 <= end:
+                    t = buf[q]
+                    size = struct.unpack("<H", buf[q + 1:q + 3])[0]
+                    q += 4 + (2 if track else 0)
+                    body = buf[q:q + size]
+                    q += size
+                    if t == 0x10:
+                        ca, cl = struct.unpack("<QQ", body[:16])
+                        chunks.append((ca, cl, False))
+                    elif t != 0:
+                        out.append((t, body))
+            return out
+        ver, _, nmsg, _rc, size = struct.unpack("<BBHII", head[:12])
+        if ver != 1:
+            raise ValueError(f"unsupported object header version {ver}")
+        chunks = [(addr + 16, size)]
+        remaining = nmsg
+        while chunks and remaining > 0:
+            a, n = chunks.pop(0)
+            buf = self.read(a, n)
+            q = 0
+            while q + 8 <= n and remaining > 0:
+                t, size_m, _flags = struct.unpack("<HHB", buf[q:q + 5])
+                body = buf[q + 8:q + 8 + size_m]
+                q += 8 + size_m
+                remaining -= 1
+                if t == 0x10:
+                    ca, cl = struct.unpack("<QQ", body[:16])
+                    chunks.append((ca, cl))
+                elif t != 0:
+                    out.append((t, body))
+        return out
+
+    # ------------------------------------------------------------------ groups
+    def group_links(self, addr: int) -> dict:
+        links = {}
+        for t, body in self.messages(addr):
+            if t == 0x11:
+                btree, heap = struct.unpack("<QQ", body[:16])
+                hh = self.read(heap, 32)
+                dsize, _free, daddr = struct.unpack("<QQQ", hh[8:32])
+                heap_data = self.read(daddr, dsize)
+                for name_off, obj in self._walk_group_btree(btree):
+                    end = heap_data.index(b"\0", name_off)
+                    links[heap_data[name_off:end].decode()] = obj
+            elif t == 0x06:
+                name, obj = self._link_message(body)
+                if obj is not None:
+                    links[name] = obj
+            elif t == 0x02:
+                p = 2 + (8 if body[1] & 1 else 0)
+                if struct.unpack("<Q", body[p:p + 8])[0] != UNDEF:
+                    raise NotImplementedError("dense (fractal-heap) link storage is not supported")
+        return links
+
+    def _walk_group_btree(self, addr):
+        h = self.read(addr, 24)
+        if h[:4] != b"TREE":
+            raise ValueError("bad group B-tree node")
+        level, used = h[5], struct.unpack("<H", h[6:8])[0]
+        buf = self.read(addr + 24, 8 + used * 16)
+        children = [struct.unpack("<Q", buf[8 + 16 * i:16 + 16 * i])[0] for i in range(used)]
+        for c in children:
+            if level > 0:
+                yield from self._walk_group_btree(c)
+            else:
+                sh = self.read(c, 8)
+                if sh[:4] != b"SNOD":
+                    raise ValueError("bad symbol table node")
+                n = struct.unpack("<H", sh[6:8])[0]
+                ents = self.read(c + 8, 40 * n)
+                for i in range(n):
+                    name_off, obj = struct.unpack("<QQ", ents[40 * i:40 * i + 16])
+                    yield name_off, obj
+
+    @staticmethod
+    def _link_message(body):
+        ver, flags = body[0], body[1]
+        p = 2
+        ltype = 0
+        if flags & 0x08:
+            ltype = body[p]
+            p += 1
+        if flags & 0x04:
+            p += 8
+        if flags & 0x10:
+            p += 1
+        nlen_sz = 1 << (flags & 3)
+        nlen = int.from_bytes(body[p:p + nlen_sz], "little")
+        p += nlen_sz
+        name = body[p:p + nlen].decode()
+        p += nlen
+        if ltype != 0:
+            return name, None
+        return name, struct.unpack("<Q", body[p:p + 8])[0]
+
+    # ------------------------------------------------------------------ datasets
+    @staticmethod
+    def _dataspace(body):
+        ver, rank = body[0], body[1]
+        flags = body[2]
+        if ver == 1:
+            p = 8
+        else:
+            if body[3] == 2:  # null dataspace
+                return None
+            p = 4
+        dims = struct.unpack(f"<{rank}Q", body[p:p + 8 * rank]) if rank else ()
+        return tuple(dims)
+
+    @staticmethod
+    def _datatype(body):
+        cls, ver = body[0] & 0x0F, body[0] >> 4
+        bits = body[1:4]
+        size = struct.unpack("<I", body[4:8])[0]
+        if cls == 0:
+            signed = bool(bits[0] & 0x08)
+            order = ">" if bits[0] & 1 else "<"
+            return np.dtype(f"{order}{'i' if signed else 'u'}{size}"), "int"
+        if cls == 1:
+            order = ">" if bits[0] & 1 else "<"
+            return np.dtype(f"{order}f{size}"), "float"
+        if cls == 3:
+            return np.dtype(f"S{size}"), "string"
+        if cls == 7:
+            if bits[0] & 0x0F != 0:
+                raise NotImplementedError("region references are not supported")
+            return np.dtype("<u8"), "ref"
+        if cls == 6:
+            nmembers = struct.unpack("<H", bits[:2])[0]
+            fields = []
+            p = 8
+            for _ in range(nmembers):
+                end = body.index(b"\0", p)
+                name = body[p:end].decode()
+                # names are padded to a multiple of 8 bytes before version 3
+                p = p + ((end - p + 8) // 8) * 8 if ver < 3 else end + 1
+                if ver == 1:
+                    off = struct.unpack("<I", body[p:p + 4])[0]
+                    p += 4 + 1 + 3 + 4 + 4 + 16
+                elif ver == 2:
+                    off = struct.unpack("<I", body[p:p + 4])[0]
+                    p += 4
+                else:
+                    nb = max(1, (size.bit_length() + 7) // 8)
+                    off = int.from_bytes(body[p:p + nb], "little")
+                    p += nb
+                mdt, _ = _Reader._datatype(body[p:])
+                p += _Reader._datatype_size(body[p:])
+                fields.append((name, mdt, off))
+            return np.dtype({"names": [f[0] for f in fields], "formats": [f[1] for f in fields],
+                             "offsets": [f[2] for f in fields], "itemsize": size}), "compound"
+        raise NotImplementedError(f"datatype class {cls}")
+
+    @staticmethod
+    def _datatype_size(body):
+        cls = body[0] & 0x0F
+        return 8 + {0: 4, 1: 12, 3: 0, 7: 0}.get(cls, 0) if cls != 6 else len(body)
+
+    def _attributes(self, msgs) -> dict:
+        attrs = {}
+        for t, body in msgs:
+            if t != 0x0C:
+                continue
+            ver = body[0]
+            if ver == 1:
+                nlen, dtlen, dslen = struct.unpack("<HHH", body[2:8])
+                p = 8
+                name = body[p:p + nlen].rstrip(b"\0").decode()
+                p += nlen + (-nlen % 8)
+                dtb = body[p:p + dtlen]
+                p += dtlen + (-dtlen % 8)
+                dsb = body[p:p + dslen]
+                p += dslen + (-dslen % 8)
+            else:
+                nlen, dtlen, dslen = struct.unpack("<HHH", body[2:8])
+                p = 8 + (1 if ver == 3 else 0)
+                name = body[p:p + nlen].rstrip(b"\0").decode()
+                p += nlen
+                dtb = body[p:p + dtlen]
+                p += dtlen
+                dsb = body[p:p + dslen]
+                p += dslen
+            dt, kind = self._datatype(dtb)
+            dims = self._dataspace(dsb)
+            n = int(np.prod(dims)) if dims else 1
+            raw = body[p:p + n * dt.itemsize]
+            val = np.frombuffer(raw, dtype=dt, count=n)
+            if kind == "string":
+                attrs[name] = val[0].split(b"\0")[0].decode() if n == 1 else [v.decode() for v in val]
+            else:
+                attrs[name] = val[0] if not dims else val.reshape(dims)
+        return attrs
+
+    def dataset(self, addr: int):
+        msgs = self.messages(addr)
+        dims = dt = layout = None
+        filters = []
+        kind = None
+        for t, body in msgs:
+            if t == 0x01:
+                dims = self._dataspace(body)
+            elif t == 0x03:
+                dt, kind = self._datatype(body)
+            elif t == 0x08:
+                layout = body
+            elif t == 0x0B:
+                filters = self._filters(body)
+        attrs = self._attributes(msgs)
+        if dims is None:
+            return np.zeros(0, dtype=dt), attrs, kind
+        n = int(np.prod(dims)) if dims else 1
+        raw = self._read_layout(layout, dims, dt, filters)
+        arr = np.frombuffer(raw, dtype=dt, count=n).reshape(dims if dims else ())
+        return arr, attrs, kind
+
+    @staticmethod
+    def _filters(body):
+        ver, nf = body[0], body[1]
+        p = 8 if ver == 1 else 2
+        out = []
+        for _ in range(nf):
+            fid = struct.unpack("<H", body[p:p + 2])[0]
+            if ver == 1 or fid >= 256:
+                nlen = struct.unpack("<H", body[p + 2:p + 4])[0]
+                flags, ncd = struct.unpack("<HH", body[p + 4:p + 8])
+                p += 8 + nlen + (-nlen % 8 if ver == 1 else 0)
+            else:
+                flags, ncd = struct.unpack("<HH", body[p + 2:p + 6])
+                p += 6
+            cd = struct.unpack(f"<{ncd}I", body[p:p + 4 * ncd])
+            p += 4 * ncd
+            if ver == 1 and ncd % 2:
+                p += 4
+            out.append((fid, cd))
+        return out
+
+    def _read_layout(self, body, dims, dt, filters) -> bytes:
+        ver = body[0]
+        if ver not in (3, 4):
+            raise NotImplementedError(f"data layout version {ver}")
+        cls = body[1]
+        nbytes = (int(np.prod(dims)) if dims else 1) * dt.itemsize
+        if cls == 0:
+            size = struct.unpack("<H", body[2:4])[0]
+            return body[4:4 + size]
+        if cls == 1:
+            addr, size = struct.unpack("<QQ", body[2:18])
+            if addr == UNDEF:
+                return bytes(nbytes)
+            return self.read(addr, size)
+        if cls == 2 and ver == 3:
+            ndims = body[2]
+            btree = struct.unpack("<Q", body[3:11])[0]
+            cdims = struct.unpack(f"<{ndims}I", body[11:11 + 4 * ndims])
+            chunk = cdims[:-1]
+            out = np.zeros(dims, dtype=np.dtype(f"V{dt.itemsize}")) if dims else None
+            if btree == UNDEF:
+                return bytes(nbytes)
+            for offs, caddr, csize, fmask in self._walk_chunk_btree(btree, ndims):
+                raw = self.read(caddr, csize)
+                raw = self._unfilter(raw, filters, fmask, dt.itemsize)
+                block = np.frombuffer(raw, dtype=out.dtype, count=int(np.prod(chunk))).reshape(chunk)
+                sl = tuple(slice(o, min(o + c, d)) for o, c, d in zip(offs, chunk, dims))
+                out[sl] = block[tuple(slice(0, s.stop - s.start) for s in sl)]
+            return out.tobytes()
+        raise NotImplementedError(f"layout class {cls} (version {ver})")
+
+    def _walk_chunk_btree(self, addr, ndims):
+        h = self.read(addr, 24)
+        if h[:4] != b"TREE" or h[4] != 1:
+            raise ValueError("bad chunk B-tree node")
+        level, used = h[5], struct.unpack("<H", h[6:8])[0]
+        ksize = 8 + 8 * ndims
+        buf = self.read(addr + 24, (used + 1) * ksize + used * 8)
+        p = 0
+        for _ in range(used):
+            csize, fmask = struct.unpack("<II", buf[p:p + 8])
+            offs = struct.unpack(f"<{ndims}Q", buf[p + 8:p + ksize])[:-1]
+            child = struct.unpack("<Q", buf[p + ksize:p + ksize + 8])[0]
+            p += ksize + 8
+            if level > 0:
+                yield from self._walk_chunk_btree(child, ndims)
+            else:
+                yield offs, child, csize, fmask
+
+    @staticmethod
+    def _unfilter(raw, filters, fmask, itemsize):
+        for i, (fid, cd) in reversed(list(enumerate(filters))):
+            if fmask & (1 << i):
+                continue
+            if fid == 1:
+                raw = zlib.decompress(raw)
+            elif fid == 2:
+                a = np.frombuffer(raw, dtype=np.uint8)
+                n = a.size // itemsize
+                raw = a[: n * itemsize].reshape(itemsize, n).T.tobytes() + a[n * itemsize:].tobytes()
+            elif fid == 3:
+                raw = raw[:-4]
+            else:
+                raise NotImplementedError(f"HDF5 filter {fid}")
+        return raw
+
+    def is_group(self, addr: int) -> bool:
+        return any(t in (0x11, 0x06, 0x02) for t, _ in self.messages(addr))
+
+
+def _decode(r: _Reader, addr: int):
+    """An HDF5 object in MATLAB terms."""
+    if r.is_group(addr):
+        # MATLAB struct: a group whose members are the fields
+        return {name: _decode(r, a) for name, a in r.group_links(addr).items() if not name.startswith("#")}
+    arr, attrs, kind = r.dataset(addr)
+    cls = attrs.get("MATLAB_class", None)
+    if isinstance(cls, bytes):
+        cls = cls.decode()
+    if attrs.get("MATLAB_empty", 0):
+        mshape = tuple(int(x) for x in np.asarray(arr).ravel())
+        if cls == "char":
+            return ""
+        if cls == "cell":
+            return np.empty(mshape, dtype=object)
+        return np.zeros(mshape, dtype=_CLASS_DTYPE.get(cls, np.float64) if cls != "logical" else bool)
+    mshape = tuple(reversed(arr.shape))
+    if kind == "ref":
+        flat = arr.ravel()                       # C order over HDF5 dims == MATLAB column-major
+        cells = np.empty(flat.size, dtype=object)
+        for i, a in enumerate(flat):
+            cells[i] = _decode(r, int(a))
+        return cells.reshape(mshape, order="F")
+    if kind == "compound":
+        names = arr.dtype.names
+        if names and set(names) >= {"real", "imag"}:
+            arr = arr["real"] + 1j * arr["imag"]
+        else:
+            raise NotImplementedError("compound dataset that is not a MATLAB complex array")
+    out = np.asarray(arr).T.astype(arr.dtype.newbyteorder("="), copy=False)   # MATLAB shape
+    if cls == "char":
+        rows = ["".join(chr(c) for c in row) for row in np.atleast_2d(out).astype(np.uint32)]
+        return rows[0] if len(rows) == 1 else rows
+    if cls == "logical":
+        return out.astype(bool)
+    return out
+
+
+def loadmat73(path: str, variable_names=None) -> dict:
+    """Read a MATLAB v7.3 file into {name: value} with MATLAB shapes (a Q x 1 vector comes back
+    as a (Q, 1) array; ``squeeze`` it as scipy's ``squeeze_me`` would)."""
+    r = _Reader(path)
+    try:
+        links = r.group_links(r.root_ohdr)
+        out = {}
+        for name, addr in links.items():
+            if name.startswith("#"):
+                continue
+            if variable_names is not None and name not in variable_names:
+                continue
+            out[name] = _decode(r, addr)
+        return out
+    finally:
+        r.close()
+
+
+def is_matv73(path: str) -> bool:
+    with open(path, "rb") as f:
+        head = f.read(128)
+        if len(head) < 128:
+            return False
+        f.seek(USERBLOCK)
+        return head[124:126] == struct.pack("<H", 0x0200) and f.read(8) == SIGNATURE
+
+
+def loadmat(path: str, variable_names=None) -> dict:
+    """``load`` for either MATLAB format: v7.3 via this module, v5/v7 via scipy."""
+    if is_matv73(path):
+        return loadmat73(path, variable_names)
+    from scipy.io import loadmat as _lm
+    d = _lm(path, variable_names=variable_names)
+    return {k: v for k, v in d.items() if not k.startswith("__")}
+
+
+__all__ = ["LazyArray", "savemat73", "loadmat73", "loadmat", "is_matv73"]

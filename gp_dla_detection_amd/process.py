@@ -129,17 +129,170 @@ PROCESSED_VARIABLES = ("training_release", "training_set_name", "dla_catalog_nam
                        "p_dlas")
 
 
-def save_processed_qsos(path: str, out: dict) -> None:
-    """Write the processed_qsos variables with MATLAB shapes (Q-vectors as Q x 1 columns,
-    sample_log_likelihoods_dla as Q x S).  Format: MATLAB v5 .mat via scipy (each variable must
-    stay under 2 GB; the reference's -v7.3/HDF5 container is a listed next step)."""
-    from scipy.io import savemat
+def save_processed_qsos(path: str, out: dict, format: str = "v7.3") -> None:
+    """``save(filename, variables_to_save{:}, '-v7.3')`` (process_qsos.m:235-249).
+
+    MATLAB shapes: Q-vectors are Q x 1 columns, ``sample_log_likelihoods_dla`` is Q x S,
+    ``model_posteriors`` Q x 2, strings are char rows, ``test_ind``/``prior_ind`` logical.  The
+    default container is v7.3 (HDF5, matv73.py): what the reference writes and what
+    calc_cddf.py reads with h5py (Q-vectors as (1, Q), the sample array as (S, Q)); it has no
+    per-variable size limit and streams the sample array into the file.  ``format="v5"`` writes
+    a scipy MATLAB v5 file instead (each variable must then stay under 2 GB)."""
     mat = {}
     for key in PROCESSED_VARIABLES:
         if key not in out:
             continue
         v = out[key]
-        if isinstance(v, np.ndarray) and v.ndim == 1:
-            v = v[:, None]
+        if isinstance(v, (int, float, np.integer, np.floating)) and not isinstance(v, bool):
+            v = np.float64(v)          # MATLAB numeric literals are double (num_lines = 3)
         mat[key] = v
-    savemat(path, mat, do_compression=False, oned_as="column")
+    if format == "v7.3":
+        from .matv73 import savemat73
+        savemat73(path, mat)
+    elif format == "v5":
+        from scipy.io import savemat
+        mat = {k: (v[:, None] if isinstance(v, np.ndarray) and v.ndim == 1 else v) for k, v in mat.items()}
+        savemat(path, mat, do_compression=False, oned_as="column")
+    else:
+        raise ValueError("format must be 'v7.3' or 'v5'")
+
+
+# ------------------------------------------------------------------------------ file-level driver
+def processed_directory(base_directory: str, release: str) -> str:
+    """set_parameters.m:85-86."""
+    return f"{base_directory}/{release}/processed"
+
+
+class _MatStruct:
+    """Attribute access over a loaded .mat dict so the reference's index expressions
+    (README.md:242-253, e.g. ``prior_catalog.in_dr9 & prior_catalog.los_inds(dla_catalog_name)``)
+    evaluate as written; a containers.Map variable (stored as a struct, matv73.py) is called
+    with its key."""
+
+    def __init__(self, d: dict):
+        self._d = d
+
+    def __getattr__(self, name):
+        v = self._d[name]
+        if isinstance(v, dict):
+            return _MatMap(v)
+        v = np.asarray(v)
+        return v.ravel() if v.ndim == 2 and 1 in v.shape else v
+
+
+class _MatMap:
+    def __init__(self, d: dict):
+        self._d = d
+
+    def __call__(self, key):
+        v = self._d[key]
+        if isinstance(v, np.ndarray) and v.dtype != object and v.ndim == 2 and 1 in v.shape:
+            return v.ravel()
+        if isinstance(v, np.ndarray) and v.dtype == object:
+            return list(v.ravel(order="F"))
+        return v
+
+
+def evaluate_index(expr, **names) -> np.ndarray:
+    """``if (ischar(ind)) ind = eval(ind); end`` (process_qsos.m:7-9,53-55).  A boolean/integer
+    array passes through; a callable gets the named structs; a string is evaluated as the
+    reference's MATLAB index expression (``&``, ``|``, ``==``, ``~``, field access and Map
+    lookup) in a namespace holding only those structs."""
+    if callable(expr):
+        return np.asarray(expr(**names))
+    if isinstance(expr, str):
+        py = expr.replace("~=", "!=")
+        ns = {k: _MatStruct(v) if isinstance(v, dict) else v for k, v in names.items()}
+        return np.asarray(eval(py, {"__builtins__": {}}, ns))
+    return np.asarray(expr)
+
+
+def _as_list(cells) -> list:
+    if isinstance(cells, np.ndarray) and cells.dtype == object:
+        return [np.asarray(c).ravel() for c in cells.ravel(order="F")]
+    return [np.asarray(c).ravel() for c in cells]
+
+
+def load_model(path: str) -> dict:
+    """process_qsos.m:29-35 (learned_qso_model_<training_set_name>.mat)."""
+    from .matv73 import loadmat
+    d = loadmat(path, ["rest_wavelengths", "mu", "M", "log_omega", "log_c_0", "log_tau_0", "log_beta"])
+    out = {k: np.asarray(d[k], dtype=np.float64).ravel() for k in ("rest_wavelengths", "mu", "log_omega")}
+    out["M"] = np.asfortranarray(np.asarray(d["M"], dtype=np.float64))
+    for k in ("log_c_0", "log_tau_0", "log_beta"):
+        out[k] = float(np.asarray(d[k]).ravel()[0])
+    return out
+
+
+def load_dla_samples(path: str) -> dict:
+    """process_qsos.m:37-40 (dla_samples.mat)."""
+    from .matv73 import loadmat
+    d = loadmat(path, ["offset_samples", "log_nhi_samples", "nhi_samples"])
+    return {k: np.asarray(v, dtype=np.float64).ravel() for k, v in d.items()}
+
+
+def save_dla_samples(path: str, samples: dict, **extra) -> None:
+    """dla_samples.mat (generate_dla_samples.m:59-63): the sample vectors are MATLAB 1 x S rows
+    (h5py sees (S, 1); calc_cddf.py:121-123 reads ``[:, 0]``)."""
+    from .matv73 import savemat73
+    var = {k: np.asarray(samples[k], dtype=np.float64).reshape(1, -1)
+           for k in ("offset_samples", "log_nhi_samples", "nhi_samples") if k in samples}
+    var.update(extra)
+    savemat73(path, var)
+
+
+def load_preloaded_qsos(path: str, test_ind=None) -> list[dict]:
+    """process_qsos.m:45-60 (preloaded_qsos.mat cells, selected by test_ind); z_QSO is attached
+    by the caller from the catalogue."""
+    from .matv73 import loadmat
+    d = loadmat(path, ["all_wavelengths", "all_flux", "all_noise_variance", "all_pixel_mask"])
+    cols = {k: _as_list(d[k]) for k in d}
+    n = len(cols["all_wavelengths"])
+    idx = np.arange(n) if test_ind is None else (
+        np.flatnonzero(test_ind) if np.asarray(test_ind).dtype == bool else np.asarray(test_ind))
+    return [dict(wavelengths=cols["all_wavelengths"][i], flux=cols["all_flux"][i],
+                 noise_variance=cols["all_noise_variance"][i],
+                 pixel_mask=cols["all_pixel_mask"][i].astype(bool)) for i in idx]
+
+
+def run_process_qsos(base_directory: str, training_release: str, training_set_name: str,
+                     dla_catalog_name: str, prior_ind, release: str, test_set_name: str, test_ind,
+                     params: Parameters | None = None, device: int = 0, save: bool = True) -> dict:
+    """The whole ``process_qsos`` script (process_qsos.m:1-249) on files laid out as the reference
+    lays them out (set_parameters.m:79-86):
+
+      <base>/<training_release>/processed/catalog.mat                  (prior catalogue)
+      <base>/<training_release>/processed/learned_qso_model_<set>.mat
+      <base>/<training_release>/processed/dla_samples.mat
+      <base>/<release>/processed/catalog.mat, preloaded_qsos.mat
+      -> <base>/<release>/processed/processed_qsos_<test_set_name>.mat  (v7.3)
+
+    ``prior_ind`` / ``test_ind`` are the reference's index expressions (strings such as
+    ``'(catalog.filter_flags == 0)'``), callables or boolean arrays.  The catalogue's
+    containers.Map variables (los_inds, dla_inds, z_dlas) are read as structs keyed by catalogue
+    name (MATLAB's MCOS Map objects are opaque outside MATLAB, SURVEY.md 7 viii)."""
+    from .matv73 import loadmat
+    tdir, rdir = processed_directory(base_directory, training_release), processed_directory(base_directory, release)
+    prior_catalog = loadmat(f"{tdir}/catalog.mat")
+    pind = evaluate_index(prior_ind, prior_catalog=prior_catalog, dla_catalog_name=dla_catalog_name).astype(bool).ravel()
+    pz = np.asarray(prior_catalog["z_qsos"], dtype=np.float64).ravel()[pind]
+    pdla = np.asarray(_MatMap(prior_catalog["dla_inds"])(dla_catalog_name)).astype(bool).ravel()[pind]
+    z_dlas_all = _MatMap(prior_catalog["z_dlas"])(dla_catalog_name)
+    pzd = [z_dlas_all[i] for i in np.flatnonzero(pind)]
+    model = load_model(f"{tdir}/learned_qso_model_{training_set_name}.mat")
+    samples = load_dla_samples(f"{tdir}/dla_samples.mat")
+    catalog = loadmat(f"{rdir}/catalog.mat")
+    tind = evaluate_index(test_ind, catalog=catalog).astype(bool).ravel()
+    spectra = load_preloaded_qsos(f"{rdir}/preloaded_qsos.mat", tind)
+    z_qsos = np.asarray(catalog["z_qsos"], dtype=np.float64).ravel()[tind]
+    for s, z in zip(spectra, z_qsos):
+        s["z_qso"] = float(z)
+    meta = dict(training_release=training_release, training_set_name=training_set_name,
+                dla_catalog_name=dla_catalog_name, prior_ind=pind, release=release,
+                test_set_name=test_set_name)
+    prior = dict(z_qsos=pz, dla_ind=pdla, z_dlas=pzd)
+    out = process_qsos(model, samples, spectra, prior, params=params, device=device, metadata=meta)
+    out["test_ind"] = tind
+    if save:
+        save_processed_qsos(f"{rdir}/processed_qsos_{test_set_name}.mat", out)
+    return out

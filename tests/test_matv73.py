@@ -1,0 +1,250 @@
+"""MATLAB v7.3 I/O (gp_dla_detection_amd/matv73.py) and the processed_qsos file layout
+(process_qsos.m:235-249).
+
+Pins, in order of strength:
+* the reference's own consumer (CDDF_analysis/calc_cddf.py DLACatalogue) reads a file this
+  package wrote and gets the same values (needs /root/reference and an h5py interpreter; this
+  container has both, the GPU box neither -- skipped there);
+* libhdf5 (h5py) reads our files with the shapes MATLAB files have;
+* our reader reads libhdf5-written MATLAB-style files (committed fixtures from
+  tests/golden/make_mat73_fixtures.py, both libhdf5 format generations);
+* write -> read round trips for every MATLAB class the pipeline stores.
+"""
+import json
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+from gp_dla_detection_amd import matv73 as M
+from gp_dla_detection_amd import process as PR
+from gp_dla_detection_amd import synthetic as syn
+
+GOLDEN = Path(__file__).parent / "golden"
+H5PY_PY = "/opt/conda/bin/python3.9"
+REF_CDDF = "/root/reference/CDDF_analysis"
+
+
+def _has_h5py():
+    if not os.path.exists(H5PY_PY):
+        return False
+    r = subprocess.run([H5PY_PY, "-c", "import h5py"], capture_output=True)
+    return r.returncode == 0
+
+
+needs_h5py = pytest.mark.skipif(not _has_h5py(), reason="no interpreter with h5py")
+
+
+def test_roundtrip_matlab_classes(tmp_path):
+    rng = np.random.default_rng(0)
+    Q, S = 37, 53
+    big = rng.standard_normal((Q, S))
+    v = dict(p_dlas=rng.uniform(size=Q), test_ind=rng.uniform(size=100) < 0.5, release="dr12q",
+             num_lines=np.float64(3), model_posteriors=rng.uniform(size=(Q, 2)), empty=np.zeros((0, 0)),
+             i32=np.arange(7, dtype=np.int32), u8=np.arange(5, dtype=np.uint8), f32=np.float32([1.5, 2.5]),
+             cells=[rng.standard_normal(n) for n in (5, 0, 9)], nested=[["ab", np.arange(3.0)], "xyz"],
+             struct=dict(dr9q_concordance=np.array([True, False]), dr12q_visual=np.array([False, True])),
+             sample_log_likelihoods_dla=M.LazyArray((Q, S), np.float64, lambda view: view.__setitem__(slice(None), big)))
+    for i in range(40):                       # > 8 links: several symbol-table nodes
+        v[f"var{i:02d}"] = float(i)
+    path = tmp_path / "t.mat"
+    M.savemat73(str(path), v)
+    assert M.is_matv73(str(path))
+    r = M.loadmat73(str(path))
+    assert np.array_equal(r["sample_log_likelihoods_dla"], big)
+    assert r["p_dlas"].shape == (Q, 1) and np.array_equal(r["p_dlas"][:, 0], v["p_dlas"])
+    assert r["test_ind"].dtype == bool and np.array_equal(r["test_ind"][:, 0], v["test_ind"])
+    assert r["release"] == "dr12q"
+    assert r["num_lines"].shape == (1, 1) and r["num_lines"][0, 0] == 3
+    assert np.array_equal(r["model_posteriors"], v["model_posteriors"])
+    assert r["empty"].shape == (0, 0)
+    assert r["i32"].dtype == np.int32 and r["u8"].dtype == np.uint8 and r["f32"].dtype == np.float32
+    assert [c.size for c in r["cells"].ravel()] == [5, 0, 9]
+    assert np.array_equal(r["cells"][2, 0].ravel(), v["cells"][2])
+    assert r["nested"][1, 0] == "xyz" and r["nested"][0, 0][0, 0] == "ab"
+    assert np.array_equal(r["struct"]["dr12q_visual"].ravel(), [False, True])
+    assert all(f"var{i:02d}" in r for i in range(40))
+
+
+def test_large_array_streams_in_blocks(tmp_path):
+    a = np.random.default_rng(1).standard_normal((1500, 6000))     # 72 MB > the stream threshold
+    path = tmp_path / "big.mat"
+    M.savemat73(str(path), dict(big=a))
+    assert np.array_equal(M.loadmat73(str(path))["big"], a)
+
+
+@pytest.mark.parametrize("tag", ["earliest", "latest"])
+def test_reads_libhdf5_written_matlab_files(tag):
+    """Files written by libhdf5 the way MATLAB -v7.3 does (chunked + deflate + shuffle, cells in
+    #refs#, complex compound, logical, char, empty), superblock v0 and v3 generations."""
+    exp = np.load(GOLDEN / "mat73_expected.npz")
+    r = M.loadmat73(str(GOLDEN / f"mat73_{tag}.mat"))
+    keys = [k.split("__", 1)[1] for k in exp.files if k.startswith(tag + "__")]
+    for k in keys:
+        if k.startswith("cell_"):
+            continue
+        assert r[k].shape == exp[f"{tag}__{k}"].shape, k
+        assert np.array_equal(r[k], exp[f"{tag}__{k}"]), k
+    cells = r["all_flux"].ravel(order="F")
+    assert np.array_equal([c.shape[0] for c in cells], exp[f"{tag}__cell_lengths"])
+    assert np.array_equal(np.concatenate([c[:, 0] for c in cells]), exp[f"{tag}__cell_concat"])
+    if tag == "earliest":
+        assert r["release"] == "dr12q" and r["empty_var"].shape == (0, 5)
+
+
+def _processed_out(Q=6, S=200, k=8):
+    """processed_qsos variables from the CPU oracle (the checker, never the product)."""
+    from oracle import gpdla_oracle as O
+    model = syn.make_model(k=k)
+    samples = syn.make_samples(S)
+    spectra = syn.make_spectra(model, Q, dla_fraction=0.5)
+    res = [O.process_spectrum(s["wavelengths"], s["flux"], s["noise_variance"], s["pixel_mask"], s["z_qso"],
+                              model, samples["offset_samples"], samples["nhi_samples"]) for s in spectra]
+    out = dict(training_release="dr12q", training_set_name="dr9q_minus_concordance",
+               dla_catalog_name="dr9q_concordance", prior_ind=np.ones(50, dtype=bool), release="dr12q",
+               test_set_name="dr12q", test_ind=np.r_[np.ones(Q, dtype=bool), np.zeros(3, dtype=bool)],
+               prior_z_qso_increase=PR.P.PRIOR_Z_QSO_INCREASE, max_z_cut=PR.P.MAX_Z_CUT, num_lines=3,
+               min_z_dlas=np.array([r["min_z_dla"] for r in res]), max_z_dlas=np.array([r["max_z_dla"] for r in res]),
+               log_likelihoods_no_dla=np.array([r["log_likelihood_no_dla"] for r in res]),
+               sample_log_likelihoods_dla=np.stack([r["sample_log_likelihoods_dla"] for r in res]),
+               log_likelihoods_dla=np.array([r["log_likelihood_dla"] for r in res]))
+    out["log_priors_no_dla"] = np.full(Q, np.log(0.8))
+    out["log_priors_dla"] = np.full(Q, np.log(0.2))
+    out["log_posteriors_no_dla"] = out["log_priors_no_dla"] + out["log_likelihoods_no_dla"]
+    out["log_posteriors_dla"] = out["log_priors_dla"] + out["log_likelihoods_dla"]
+    out["model_posteriors"], out["p_no_dlas"], out["p_dlas"] = PR.model_posteriors(
+        out["log_posteriors_no_dla"], out["log_posteriors_dla"])
+    return out, samples
+
+
+def test_processed_qsos_layout(tmp_path):
+    out, _ = _processed_out()
+    path = tmp_path / "processed_qsos_dr12q.mat"
+    PR.save_processed_qsos(str(path), out)
+    r = M.loadmat73(str(path))
+    assert sorted(r) == sorted(k for k in PR.PROCESSED_VARIABLES if k in out)
+    Q, S = out["sample_log_likelihoods_dla"].shape
+    assert r["sample_log_likelihoods_dla"].shape == (Q, S)
+    assert np.array_equal(r["sample_log_likelihoods_dla"], out["sample_log_likelihoods_dla"])
+    assert r["p_dlas"].shape == (Q, 1) and r["model_posteriors"].shape == (Q, 2)
+    assert r["test_ind"].dtype == bool and r["training_set_name"] == "dr9q_minus_concordance"
+    assert r["num_lines"].dtype == np.float64
+
+
+@needs_h5py
+def test_h5py_sees_matlab_shapes(tmp_path):
+    out, _ = _processed_out()
+    path = tmp_path / "processed_qsos_dr12q.mat"
+    PR.save_processed_qsos(str(path), out)
+    code = ("import h5py,json,sys; f=h5py.File(sys.argv[1],'r'); "
+            "print(json.dumps({k: [list(f[k].shape), f[k].attrs['MATLAB_class'].decode()] for k in f if k[0] != '#'}))")
+    res = subprocess.run([H5PY_PY, "-c", code, str(path)], capture_output=True, text=True, check=True)
+    shapes = json.loads(res.stdout.strip().splitlines()[-1])
+    Q, S = out["sample_log_likelihoods_dla"].shape
+    assert shapes["sample_log_likelihoods_dla"] == [[S, Q], "double"]      # calc_cddf.py:92,98
+    assert shapes["p_dlas"] == [[1, Q], "double"]                          # calc_cddf.py:64
+    assert shapes["test_ind"] == [[1, Q + 3], "logical"]                   # calc_cddf.py:69
+    assert shapes["release"] == [[5, 1], "char"]
+
+
+@needs_h5py
+@pytest.mark.skipif(not os.path.isdir(REF_CDDF), reason="reference not present (GPU box)")
+def test_reference_consumer_reads_our_file(tmp_path):
+    """calc_cddf.py's DLACatalogue loads processed_qsos + dla_samples written here and recovers
+    p_dla, z ranges, test_ind and the normalised sample likelihoods (with its own
+    0.95 < sum < 1.05 assert, calc_cddf.py:246)."""
+    out, samples = _processed_out()
+    proc = tmp_path / "processed_qsos_dr12q.mat"
+    samp = tmp_path / "dla_samples.mat"
+    snrs = tmp_path / "snrs_qsos_dr12q.mat"
+    PR.save_processed_qsos(str(proc), out)
+    PR.save_dla_samples(str(samp), samples)
+    Q = out["p_dlas"].size
+    M.savemat73(str(snrs), dict(snrs=np.full(Q, 5.0)))
+    res = subprocess.run([H5PY_PY, str(Path(__file__).parent / "cddf_consumer.py"), REF_CDDF, str(proc),
+                          str(samp), str(snrs)], capture_output=True, text=True)
+    assert res.returncode == 0, res.stderr[-2000:]
+    got = json.loads(res.stdout.strip().splitlines()[-1])
+    assert np.array_equal(got["p_dla"], out["p_dlas"])
+    assert np.array_equal(got["z_min"], out["min_z_dlas"]) and np.array_equal(got["z_max"], out["max_z_dlas"])
+    assert got["real_index"] == list(range(Q))
+    assert np.array_equal(got["z_offsets"], samples["offset_samples"])
+    assert np.array_equal(got["lnhi"], samples["log_nhi_samples"])
+    S = out["sample_log_likelihoods_dla"].shape[1]
+    norm = {**got["log_norm_like"], **got["log_norm_like_on_demand"]}
+    assert norm, "no spectrum passed the reference's p_dla threshold"
+    for spec, vals in norm.items():
+        spec = int(spec)
+        want = out["sample_log_likelihoods_dla"][spec] - (out["log_likelihoods_dla"][spec] + np.log(S))
+        np.testing.assert_allclose(vals, want, rtol=0, atol=1e-12)
+
+
+def test_index_expressions_from_readme():
+    """process_qsos.m:7-9,53-55 eval the README's index strings (README.md:242-253)."""
+    prior_catalog = dict(in_dr9=np.array([[1], [1], [0], [1]], dtype=bool),
+                         filter_flags=np.array([[0], [1], [0], [0]], dtype=np.uint8),
+                         los_inds=dict(dr9q_concordance=np.array([[True], [True], [True], [False]])))
+    expr = (" prior_catalog.in_dr9 & "
+            "(prior_catalog.filter_flags == 0) & "
+            " prior_catalog.los_inds(dla_catalog_name)")
+    got = PR.evaluate_index(expr, prior_catalog=prior_catalog, dla_catalog_name="dr9q_concordance")
+    assert got.tolist() == [True, False, False, False]
+    got = PR.evaluate_index("(catalog.filter_flags == 0)", catalog=prior_catalog)
+    assert got.tolist() == [True, False, True, True]
+    got = PR.evaluate_index("~catalog.in_dr9", catalog=prior_catalog)
+    assert got.tolist() == [False, False, True, False]
+    mask = np.array([True, False])
+    assert PR.evaluate_index(mask) is not None and PR.evaluate_index(mask).tolist() == [True, False]
+    with pytest.raises(Exception):
+        PR.evaluate_index("__import__('os')", catalog=prior_catalog)
+
+
+def write_reference_tree(base, Q=5, S=64, k=8, seed=3):
+    """The reference's processed/ directory (set_parameters.m:85-86) with every file process_qsos
+    reads, written by this package: catalog.mat (containers.Map variables as structs),
+    learned_qso_model_<set>.mat, dla_samples.mat and preloaded_qsos.mat (cells)."""
+    rng = np.random.default_rng(seed)
+    model = syn.make_model(k=k)
+    samples = syn.make_samples(S)
+    spectra = syn.make_dr12q_like_spectra(model, Q, seed=seed)
+    d = Path(base) / "dr12q" / "processed"
+    d.mkdir(parents=True, exist_ok=True)
+    Np = 40
+    prior_z = rng.uniform(2.0, 5.0, Np)
+    catalog = dict(z_qsos=np.r_[[s["z_qso"] for s in spectra], rng.uniform(2, 4, Np - Q)],
+                   filter_flags=np.r_[np.zeros(Q, np.uint8), np.ones(Np - Q, np.uint8)],
+                   in_dr9=rng.uniform(size=Np) < 0.8,
+                   los_inds=dict(dr9q_concordance=rng.uniform(size=Np) < 0.9),
+                   dla_inds=dict(dr9q_concordance=rng.uniform(size=Np) < 0.3),
+                   z_dlas=dict(dr9q_concordance=[np.array([z - 0.3]) for z in prior_z]))
+    catalog["z_qsos"][Q:] = prior_z[Q:]
+    M.savemat73(str(d / "catalog.mat"), catalog)
+    M.savemat73(str(d / "learned_qso_model_dr9q_minus_concordance.mat"),
+                dict(rest_wavelengths=model["rest_wavelengths"], mu=model["mu"], M=model["M"],
+                     log_omega=model["log_omega"], log_c_0=model["log_c_0"], log_tau_0=model["log_tau_0"],
+                     log_beta=model["log_beta"]))
+    PR.save_dla_samples(str(d / "dla_samples.mat"), samples)
+    pad = [syn.make_spectrum(model, 100 + i, dla_fraction=0.0) for i in range(Np - Q)]
+    allq = spectra + pad
+    M.savemat73(str(d / "preloaded_qsos.mat"),
+                dict(all_wavelengths=[s["wavelengths"] for s in allq], all_flux=[s["flux"] for s in allq],
+                     all_noise_variance=[s["noise_variance"] for s in allq],
+                     all_pixel_mask=[np.asarray(s["pixel_mask"], dtype=bool) for s in allq]))
+    return model, samples, spectra, catalog
+
+
+def test_reference_tree_loaders(tmp_path):
+    model, samples, spectra, catalog = write_reference_tree(tmp_path)
+    d = tmp_path / "dr12q" / "processed"
+    m2 = PR.load_model(str(d / "learned_qso_model_dr9q_minus_concordance.mat"))
+    assert np.array_equal(m2["M"], model["M"]) and m2["log_beta"] == model["log_beta"]
+    s2 = PR.load_dla_samples(str(d / "dla_samples.mat"))
+    assert np.array_equal(s2["nhi_samples"], samples["nhi_samples"])
+    tind = PR.evaluate_index("(catalog.filter_flags == 0)", catalog=M.loadmat73(str(d / "catalog.mat")))
+    sp = PR.load_preloaded_qsos(str(d / "preloaded_qsos.mat"), tind)
+    assert len(sp) == len(spectra)
+    for a, b in zip(sp, spectra):
+        assert np.array_equal(a["flux"], b["flux"]) and np.array_equal(a["pixel_mask"], b["pixel_mask"])
