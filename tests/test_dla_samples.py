@@ -1,0 +1,97 @@
+"""generate_dla_samples (generate_dla_samples.m:1-63) restated in gp_dla_detection_amd/dla_samples.py.
+
+Parity is pinned by the published definitions the reference calls (no sample file or catalogue
+ships with it): RR2-scrambled Halton digits (Kocis & Whiten 1997), MATLAB ksdensity's default
+bandwidth rule and Gaussian kernel, and the mixture CDF / its inverse."""
+import numpy as np
+import pytest
+from scipy import integrate, stats
+
+from gp_dla_detection_amd import dla_samples as D
+from gp_dla_detection_amd import matv73 as M
+from gp_dla_detection_amd import process as PR
+
+
+def test_rr2_permutations():
+    assert D.rr2_permutation(2).tolist() == [0, 1]
+    assert D.rr2_permutation(3).tolist() == [0, 2, 1]          # 2-bit reversal 0,2,1,3 minus 3
+    assert D.rr2_permutation(5).tolist() == [0, 4, 2, 1, 3]     # 3-bit reversal 0,4,2,6,1,5,3,7 below 5
+
+
+def test_halton_rr2_first_points():
+    h = D.halton_rr2(7)
+    assert h[0].tolist() == [0.0, 0.0]                           # MATLAB haltonset starts at the origin
+    np.testing.assert_allclose(h[:, 0], [0, .5, .25, .75, .125, .625, .375], rtol=0, atol=1e-16)
+    # base 3 digits 1 -> 2, 2 -> 1: i=1 '1' -> 2/3; i=2 '2' -> 1/3; i=3 '10' -> 2/9; i=4 '11' -> 8/9;
+    # i=5 '12' -> 1/3 + 2/9; i=6 '20' -> 1/9
+    np.testing.assert_allclose(h[:, 1], [0, 2 / 3, 1 / 3, 2 / 9, 8 / 9, 5 / 9, 1 / 9], rtol=0, atol=1e-16)
+    assert np.array_equal(D.halton_rr2(5, start=2), h[2:7])
+
+
+def test_ksdensity_matches_gaussian_kde_at_the_matlab_bandwidth():
+    rng = np.random.default_rng(4)
+    x = rng.normal(20.6, 0.35, 500)
+    h = D.ksdensity_bandwidth(x)
+    mad = np.median(np.abs(x - np.median(x)))
+    assert h == pytest.approx(mad / 0.6745 * (4 / (3 * x.size)) ** 0.2, rel=1e-15)
+    pts = np.linspace(20, 22, 1000)
+    kde = stats.gaussian_kde(x, bw_method=h / np.std(x, ddof=1))
+    np.testing.assert_allclose(D.ksdensity(x, pts), kde(pts), rtol=1e-12)
+
+
+@pytest.fixture(scope="module")
+def prior():
+    rng = np.random.default_rng(5)
+    log_nhis = np.r_[rng.normal(20.55, 0.3, 800), rng.uniform(20.3, 21.8, 200)]
+    return D.ColumnDensityPrior(log_nhis), log_nhis
+
+
+def test_prior_normalised_and_fit_integral(prior):
+    p, _ = prior
+    # the fitted density integrates to Z over [20, 25] (generate_dla_samples.m:37-38), by quadrature
+    q, _ = integrate.quad(lambda t: float(p._fit_pdf(t)), 20, 25, epsabs=0, epsrel=1e-13, limit=200)
+    assert p.Z == pytest.approx(q, rel=1e-12)
+    assert p.cdf(20.0) == 0.0
+    assert p.cdf(25.0) == pytest.approx(1.0, abs=1e-14)
+    tt = np.linspace(20, 24, 41)
+    for a, b in zip(tt[:-1], tt[1:]):
+        q, _ = integrate.quad(lambda t: float(p.pdf(t)), a, b, epsabs=0, epsrel=1e-13, points=[23.0] if a < 23 < b else None)
+        assert p.cdf(b) - p.cdf(a) == pytest.approx(q, rel=1e-10, abs=1e-15)
+
+
+def test_inverse_cdf_roundtrip(prior):
+    p, _ = prior
+    u = D.halton_rr2(2000)[:, 1]
+    t = p.inverse_cdf(u)
+    assert t[0] == 20.0                                            # u = 0 at the origin point
+    np.testing.assert_allclose(p.cdf(t), u, rtol=0, atol=1e-14)   # the CDF's own rounding
+    assert np.all(np.diff(t[np.argsort(u)]) >= 0)
+
+
+def test_generate_dla_samples_marginals(prior):
+    _, log_nhis = prior
+    out = D.generate_dla_samples(list(np.array_split(log_nhis, 50)) + [np.zeros(0)], num_dla_samples=4000)
+    assert out["offset_samples"].shape == (4000,) and out["log_nhi_samples"].shape == (4000,)
+    np.testing.assert_array_equal(out["nhi_samples"], 10.0 ** out["log_nhi_samples"])
+    assert out["log_nhi_samples"].min() >= 20.0 and out["log_nhi_samples"].max() < 25.0
+    # quasi-random samples reproduce the mixture CDF (Kolmogorov distance well below MC noise)
+    p = D.ColumnDensityPrior(log_nhis)
+    grid = np.linspace(20, 23.5, 200)
+    emp = np.searchsorted(np.sort(out["log_nhi_samples"]), grid, side="right") / 4000
+    assert np.max(np.abs(emp - p.cdf(grid))) < 2e-3
+    assert np.max(np.abs(np.sort(out["offset_samples"]) - (np.arange(4000) + 0.5) / 4000)) < 1e-3
+
+
+def test_run_generate_dla_samples_files(tmp_path, prior):
+    _, log_nhis = prior
+    d = tmp_path / "dr12q" / "processed"
+    d.mkdir(parents=True)
+    cells = list(np.array_split(log_nhis, 100))
+    M.savemat73(str(d / "catalog.mat"), dict(log_nhis=dict(dr9q_concordance=cells)))
+    out = D.run_generate_dla_samples(str(tmp_path), "dr12q", "dr9q_concordance", num_dla_samples=500)
+    r = M.loadmat73(str(d / "dla_samples.mat"))
+    assert r["offset_samples"].shape == (1, 500)                   # MATLAB row (h5py (500, 1))
+    np.testing.assert_array_equal(r["log_nhi_samples"].ravel(), out["log_nhi_samples"])
+    assert float(r["alpha"][0, 0]) == 0.9
+    s = PR.load_dla_samples(str(d / "dla_samples.mat"))
+    np.testing.assert_array_equal(s["nhi_samples"], out["nhi_samples"])
