@@ -82,6 +82,12 @@ SIGNATURES = {
     "gpdla_voigt_f64": (C.c_int, [dp, C.c_int64, C.c_double, C.c_double, C.c_int32, dp]),
     "gpdla_voigt_batch_f64": (C.c_int, [dp, C.c_int64, dp, dp, C.c_int64, C.c_int32, dp]),
     "gpdla_log_mvnpdf_low_rank_f64": (C.c_int, [dp, dp, dp, dp, C.c_int64, C.c_int32, dp]),
+    "gpdla_objective_create": (C.c_int, [C.c_int32, C.c_int64, C.c_int64, C.c_int32, dp, dp, dp, C.c_int32,
+                                         C.POINTER(C.c_void_p)]),
+    "gpdla_objective_eval": (C.c_int, [C.c_void_p, dp, dp, dp]),
+    "gpdla_objective_destroy": (None, [C.c_void_p]),
+    "gpdla_spectrum_loss_f64": (C.c_int, [dp, dp, dp, dp, dp, C.c_int64, C.c_int32, C.c_double, C.c_double,
+                                          C.c_double, dp, dp, dp, dp, dp, dp]),
     "gpdla_diag_faddeeva_w": (C.c_int, [C.c_double, C.c_double, dp, dp]),
     "gpdla_diag_line_table_error": (C.c_int, [C.c_int32, dp]),
     "gpdla_device_malloc": (C.c_int, [C.c_int32, C.c_int64, C.POINTER(C.c_void_p)]),

@@ -18,8 +18,10 @@
 using namespace gpdla;
 
 namespace {
-
 thread_local std::string g_last_error;
+}  // namespace
+
+namespace gpdla {
 
 int set_error(int code, const char* fmt, ...) {
   char buf[512];
@@ -31,14 +33,20 @@ int set_error(int code, const char* fmt, ...) {
   return code;
 }
 
-#define HIP_TRY(expr)                                                                       \
-  do {                                                                                      \
-    hipError_t e_ = (expr);                                                                 \
-    if (e_ != hipSuccess)                                                                   \
-      return set_error(e_ == hipErrorOutOfMemory ? GPDLA_ENOMEM : GPDLA_EDEVICE,            \
-                       "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__,     \
-                       __LINE__);                                                           \
-  } while (0)
+int check_device(int32_t device) {
+  int count = 0;
+  hipError_t e = hipGetDeviceCount(&count);
+  if (e != hipSuccess || count == 0)
+    return set_error(GPDLA_EDEVICE, "no HIP device available (%s): libgpdla has no CPU fallback",
+                     hipGetErrorString(e));
+  if (device < 0 || device >= count)
+    return set_error(GPDLA_EINVAL, "device %d out of range (%d devices)", device, count);
+  return GPDLA_OK;
+}
+
+}  // namespace gpdla
+
+namespace {
 
 // ---- line-profile data (fitted once per process on the host; layout in internal.h)
 struct HostLineData {
@@ -69,17 +77,6 @@ LineArgs make_line_args(const double* d_buf) {
   LineArgs l{};
   l.buf = d_buf;
   return l;
-}
-
-int check_device(int32_t device) {
-  int count = 0;
-  hipError_t e = hipGetDeviceCount(&count);
-  if (e != hipSuccess || count == 0)
-    return set_error(GPDLA_EDEVICE, "no HIP device available (%s): libgpdla has no CPU fallback",
-                     hipGetErrorString(e));
-  if (device < 0 || device >= count)
-    return set_error(GPDLA_EINVAL, "device %d out of range (%d devices)", device, count);
-  return GPDLA_OK;
 }
 
 template <class T>

@@ -7,7 +7,22 @@
 #include "line_profile.h"
 #include "lyman_series.h"
 
+// HIP call -> C-ABI status (GPDLA_ENOMEM / GPDLA_EDEVICE with a message), in functions returning int
+#define HIP_TRY(expr)                                                                       \
+  do {                                                                                      \
+    hipError_t e_ = (expr);                                                                 \
+    if (e_ != hipSuccess)                                                                   \
+      return ::gpdla::set_error(e_ == hipErrorOutOfMemory ? GPDLA_ENOMEM : GPDLA_EDEVICE,   \
+                                "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_),      \
+                                __FILE__, __LINE__);                                        \
+  } while (0)
+
 namespace gpdla {
+
+// C-ABI error reporting shared by the translation units (engine.hip): sets gpdla_last_error()
+int set_error(int code, const char* fmt, ...);
+// GPDLA_OK if `device` is a usable HIP device, else GPDLA_EDEVICE / GPDLA_EINVAL (no CPU fallback)
+int check_device(int32_t device);
 
 // ---------------------------------------------------------------------------------------------
 // Device data layout (HBM)

@@ -145,6 +145,28 @@ int gpdla_voigt_batch_f64(const double* lambdas, int64_t n_padded, const double*
 int gpdla_log_mvnpdf_low_rank_f64(const double* y, const double* mu, const double* M,
                                   const double* d, int64_t n, int32_t k, double* out);
 
+/* ---- GP null-model training objective ----------------------------------------
+ * objective.m: f(x) = sum_i spectrum_loss(...) and its gradient g(x), with
+ *   x = [M(:) (num_pixels x k, column-major); log_omega (num_pixels); log_c_0; log_tau_0; log_beta]
+ * (objective.m:21-30).  The training data are the matrices of learn_qso_model.m:63-84,
+ * num_quasars x num_pixels, ROW-major here (row i = quasar i; NaN = missing pixel, objective.m:43).
+ * As in the reference, the tau_0 and beta priors enter g only, not f (objective.m:59-71).
+ * gpdla_objective_create copies host data to the device (memory = GPDLA_MEM_HOST) or borrows
+ * device arrays (GPDLA_MEM_DEVICE, which must outlive the handle); each _eval takes host x and
+ * writes host f and g (g may be NULL).  num_pixels <= 4096, k <= 64. */
+typedef struct gpdla_objective gpdla_objective;
+int gpdla_objective_create(int32_t device, int64_t num_quasars, int64_t num_pixels, int32_t k,
+                           const double* centered_rest_fluxes, const double* lya_1pzs,
+                           const double* rest_noise_variances, int32_t memory, gpdla_objective** out);
+int gpdla_objective_eval(gpdla_objective* objective, const double* x, double* f, double* g);
+void gpdla_objective_destroy(gpdla_objective* objective);
+/* spectrum_loss.m:14-76 for one spectrum (host buffers): n pixels, M n x k column-major, omega2
+ * per pixel.  Any gradient output may be NULL. */
+int gpdla_spectrum_loss_f64(const double* y, const double* lya_1pz, const double* noise_variance,
+                            const double* M, const double* omega2, int64_t n, int32_t k, double c_0,
+                            double tau_0, double beta, double* nlog_p, double* dM, double* dlog_omega,
+                            double* dlog_c_0, double* dlog_tau_0, double* dlog_beta);
+
 /* Diagnostics (test support; not used by the compute path).
  * Re/Im of the Faddeeva function the line tables are fitted from (host, long double). */
 int gpdla_diag_faddeeva_w(double x, double y, double* re, double* im);

@@ -15,6 +15,8 @@ What it restates (reference = sbird/gp_dla_detection, paths relative to the repo
                               ``ind = ~this_pixel_mask(ind)`` absorption-index quirk, the
                               per-sample modulated likelihood, log-mean-exp).
 * ``dla_priors`` / ``model_posteriors`` -- process_qsos.m:4-27,122-132,222-232.
+* ``spectrum_loss`` / ``objective`` -- spectrum_loss.m:14-76 and objective.m:13-74 (the GP
+                              null-model training likelihood and gradient).
 
 Third-party dependency on the path: **libcerf** ``voigt(x, sigma, gamma)`` (called at
 voigt.c:288; install note README.md:210-218; not vendored, *no pinned version*).  libcerf 1.x
@@ -308,3 +310,67 @@ def model_posteriors(log_posteriors_no_dla, log_posteriors_dla):
     post = post / np.sum(post, axis=1, keepdims=True)                           # :229
     p_no = post[:, 0]                                                           # :231
     return post, p_no, 1 - p_no                                                 # :232
+
+
+# ----------------------------------------------------------------------------------------
+# GP null-model training objective: spectrum_loss.m:14-76 and
+# objective.m:13-74, MATLAB operation order
+# ----------------------------------------------------------------------------------------
+def spectrum_loss(y, lya_1pz, noise_variance, M, omega2, c_0, tau_0, beta):
+    n, k = M.shape                                                               # :20
+    lya_optical_depth = tau_0 * lya_1pz ** beta                                  # :23
+    lya_absorption = np.exp(-lya_optical_depth)                                  # :24
+    scaling_factor = 1 - lya_absorption + c_0                                    # :27
+    absorption_noise = omega2 * scaling_factor ** 2                              # :28
+    d = noise_variance + absorption_noise                                        # :30
+    d_inv = 1 / d                                                                # :32
+    D_inv_y = d_inv * y                                                          # :33
+    D_inv_M = d_inv[:, None] * M                                                 # :34
+    B = M.T @ D_inv_M                                                            # :41
+    B[np.diag_indices(k)] += 1                                                   # :42
+    L = cholesky(B, lower=False)                                                 # :43
+    C = solve_triangular(L, solve_triangular(L, D_inv_M.T, trans='T', lower=False),
+                         lower=False)                                            # :45
+    K_inv_y = D_inv_y - D_inv_M @ (C @ y)                                        # :47
+    log_det_K = np.sum(np.log(d)) + 2 * np.sum(np.log(np.diag(L)))               # :49
+    nlog_p = 0.5 * (y @ K_inv_y + log_det_K + n * LOG_2PI)                       # :53
+    K_inv_M = D_inv_M - D_inv_M @ (C @ M)                                        # :56
+    dM = -(np.outer(K_inv_y, K_inv_y @ M) - K_inv_M)                             # :57
+    diag_K_inv = d_inv - np.sum(C * D_inv_M.T, axis=0)                           # :60
+    dlog_omega = -(absorption_noise * (K_inv_y ** 2 - diag_K_inv))               # :63
+    da = c_0 * omega2 * scaling_factor                                           # :66
+    dlog_c_0 = -(K_inv_y * da) @ K_inv_y + diag_K_inv @ da                       # :67
+    da = omega2 * scaling_factor * lya_optical_depth * lya_absorption            # :70
+    dlog_tau_0 = -(K_inv_y * da) @ K_inv_y + diag_K_inv @ da                     # :71
+    da = da * np.log(lya_1pz) * beta                                             # :74
+    dlog_beta = -(K_inv_y * da) @ K_inv_y + diag_K_inv @ da                      # :75
+    return nlog_p, dM, dlog_omega, dlog_c_0, dlog_tau_0, dlog_beta
+
+
+def objective(x, centered_rest_fluxes, lya_1pzs, rest_noise_variances):
+    num_quasars, num_pixels = centered_rest_fluxes.shape                         # :16
+    k = (x.size - 3) // num_pixels - 1                                           # :18
+    M = x[:num_pixels * k].reshape(num_pixels, k, order="F")                     # :20-21
+    log_omega = x[num_pixels * k:num_pixels * (k + 1)]                           # :23-24
+    log_c_0, log_tau_0, log_beta = x[-3], x[-2], x[-1]                           # :26-28
+    omega2 = np.exp(2 * log_omega)                                               # :30
+    c_0, tau_0, beta = np.exp(log_c_0), np.exp(log_tau_0), np.exp(log_beta)      # :31-33
+    f = 0.0
+    dM = np.zeros_like(M)
+    dlog_omega = np.zeros_like(log_omega)
+    dlog_c_0 = dlog_tau_0 = dlog_beta = 0.0
+    for i in range(num_quasars):                                                 # :42
+        ind = ~np.isnan(centered_rest_fluxes[i])                                 # :43
+        tf, tdM, tdo, tc, tt, tb = spectrum_loss(
+            centered_rest_fluxes[i, ind], lya_1pzs[i, ind], rest_noise_variances[i, ind],
+            M[ind], omega2[ind], c_0, tau_0, beta)                               # :45-50
+        f += tf
+        dM[ind] += tdM
+        dlog_omega[ind] += tdo
+        dlog_c_0 += tc
+        dlog_tau_0 += tt
+        dlog_beta += tb
+    dlog_tau_0 += tau_0 * (tau_0 - 0.0023) / 0.0007 ** 2                         # :60-64
+    dlog_beta += beta * (beta - 3.65) / 0.21 ** 2                                # :67-71
+    g = np.concatenate([dM.ravel(order="F"), dlog_omega, [dlog_c_0, dlog_tau_0, dlog_beta]])
+    return f, g                                                                  # :73
