@@ -192,7 +192,12 @@ def initial_parameters(centered_rest_fluxes, k: int = P.K):
     initial_M = coefficients[:, :k] * np.sqrt(np.maximum(latent[:k], 0))      # :90
     with warnings.catch_warnings():
         warnings.simplefilter("ignore", RuntimeWarning)
-        initial_log_omega = np.log(np.nanstd(centered_rest_fluxes, axis=0, ddof=1))  # :92
+        # MATLAB nanstd normalises by N - 1, except a single observation (std 0); no data -> NaN
+        cnt = np.sum(~np.isnan(centered_rest_fluxes), axis=0)
+        sd = np.nanstd(centered_rest_fluxes, axis=0, ddof=1)
+        sd = np.where(cnt == 1, 0.0, sd)
+        with np.errstate(divide="ignore"):
+            initial_log_omega = np.log(sd)                                    # :92
     x0 = np.concatenate([initial_M.ravel(order="F"), initial_log_omega,
                          [np.log(P.INITIAL_C_0), np.log(P.INITIAL_TAU_0), np.log(P.INITIAL_BETA)]])
     return x0, initial_M, initial_log_omega
@@ -205,6 +210,14 @@ def learn_qso_model(spectra, z_qsos, k: int = P.K, max_iter: int = 2000, max_fun
     rest_wavelengths, mu, centered, lya_1pzs, noise = prepare_training_data(spectra, z_qsos)
     x0, initial_M, initial_log_omega = initial_parameters(centered, k)
     R = rest_wavelengths.size
+    # Rest pixels seen by fewer than two training spectra get log omega = -Inf / NaN from nanstd
+    # (as in MATLAB); real training sets cover the grid, but the optimiser cannot start from a
+    # non-finite point, so those entries start at the median finite value instead (reported).
+    lo = x0[R * k:R * (k + 1)]
+    bad = ~np.isfinite(lo)
+    if np.any(bad):
+        lo[bad] = np.median(lo[~bad]) if np.any(~bad) else np.log(0.1)
+    x0 = np.nan_to_num(x0, nan=0.0)
     with Objective(centered, lya_1pzs, noise, k, device) as obj:
         res = minimize(obj, x0, jac=True, method="L-BFGS-B",
                        options=dict(maxiter=max_iter, maxfun=max_fun_evals))
@@ -216,4 +229,5 @@ def learn_qso_model(spectra, z_qsos, k: int = P.K, max_iter: int = 2000, max_fun
                 M=x[:R * k].reshape(R, k, order="F"), log_omega=x[R * k:R * (k + 1)],
                 log_c_0=x[-3], log_tau_0=x[-2], log_beta=x[-1], log_likelihood=res.fun,
                 max_noise_variance=P.MAX_NOISE_VARIANCE,
-                minFunc_output=dict(iterations=res.nit, funcCount=evals, message=str(res.message)))
+                minFunc_output=dict(iterations=res.nit, funcCount=evals, message=str(res.message),
+                                    nonfinite_initial_log_omega=int(np.count_nonzero(bad))))

@@ -1,0 +1,103 @@
+"""Spectrum ingest (read_spec.m, preload_qsos.m).  The numpy FITS reader is
+checked against a file written by astropy (tests/golden/make_fits_fixture.py); read_spec and
+preload_qsos against the rules of read_spec.m:27-38 and preload_qsos.m:25-72."""
+import shutil
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+from gp_dla_detection_amd import ingest as I
+from gp_dla_detection_amd import matv73 as M
+from gp_dla_detection_amd import parameters as P
+
+GOLDEN = Path(__file__).parent / "golden"
+
+
+def test_bintable_reader_matches_astropy_file():
+    exp = np.load(GOLDEN / "speclite_fixture.npz")
+    cols = I.read_bintable(str(GOLDEN / "speclite_fixture.fits"), 1)
+    assert len(cols) == 8
+    for got, key in zip(cols[:4], ("flux", "loglam", "ivar", "and_mask")):
+        assert np.array_equal(got, exp[key]) and got.dtype == exp[key].dtype
+    u16, flag, name, vec, k64 = I.read_bintable(str(GOLDEN / "speclite_fixture.fits"), 2)
+    assert u16.tolist() == [0, 1000, 2000, 3000, 4000]                 # TZERO = 32768 convention
+    assert flag.tolist() == [True, False, True, True, False]
+    assert [s.decode().rstrip() for s in name] == ["abc", "de", "f", "ghijkl", ""]
+    assert np.array_equal(vec, np.arange(15.0).reshape(5, 3))
+    assert k64.tolist() == [1, -2, 3, 2 ** 40, -(2 ** 40)]
+
+
+def test_read_spec_rules():
+    exp = np.load(GOLDEN / "speclite_fixture.npz")
+    w, f, nv, pm = I.read_spec(str(GOLDEN / "speclite_fixture.fits"))
+    assert w.dtype == np.float32                                         # fitsread 'E' -> single
+    assert np.array_equal(w, np.float32(10) ** exp["loglam"])           # :28
+    with np.errstate(divide="ignore"):
+        assert np.array_equal(nv, np.float32(1) / exp["ivar"])          # :31
+    want = (exp["ivar"] == 0) | ((exp["and_mask"] & (1 << 23)) != 0)   # :36-38, BRIGHTSKY = bit 24
+    assert np.array_equal(pm, want) and pm.any() and (~pm).any()
+
+
+def _spectrum(z, n_lo=3400, n_hi=5600, step=1e-4, mask_window=False, seed=0):
+    rng = np.random.default_rng(seed)
+    loglam = np.arange(np.log10(n_lo), np.log10(n_hi), step).astype(np.float32)
+    w = np.float32(10) ** loglam
+    f = rng.normal(3, 0.2, w.size).astype(np.float32)
+    nv = rng.uniform(0.01, 0.02, w.size).astype(np.float32)
+    pm = rng.uniform(size=w.size) < 0.1
+    if mask_window:
+        rest = w / np.float32(1 + z)
+        pm |= (rest >= 1310) & (rest <= 1325)
+    return w, f, nv, pm
+
+
+def test_preload_qsos_flags_normalisation_and_range():
+    z = np.array([2.5, 2.5, 2.5, 3.2, 2.5])
+    flags = np.array([0, 1, 0, 0, 0], dtype=np.uint8)
+    specs = {0: _spectrum(2.5, seed=1), 2: _spectrum(2.5, mask_window=True, seed=2),
+             3: _spectrum(3.2, n_lo=5000, seed=3), 4: _spectrum(2.5, seed=4)}
+    out = I.preload_qsos(z, [0, 1, 2, 3, 4], [0] * 5, [0] * 5, flags, lambda p, m, f: specs[p])
+    ff = out["filter_flags"]
+    assert ff[1] == 1                                                   # already filtered: skipped
+    assert ff[2] == 4                                                   # bit 3: no normalising pixel
+    assert ff[3] == 8                                                   # bit 4: < min_num_pixels
+    assert ff[0] == 0 and ff[4] == 0
+    for q in (0, 4):
+        w, f, nv, pm = specs[q]
+        rest = w / np.float32(1 + z[q])
+        win = (rest >= P.NORMALIZATION_MIN_LAMBDA) & (rest <= P.NORMALIZATION_MAX_LAMBDA) & ~pm
+        med = np.median(f[win])
+        assert out["all_normalizers"][q] == med
+        ind = (rest >= P.LOADING_MIN_LAMBDA) & (rest <= P.LOADING_MAX_LAMBDA)
+        first, last = np.flatnonzero(ind)[[0, -1]]
+        avail = np.flatnonzero(~ind & ~pm)
+        keep = ind.copy()
+        if (avail > last).any():
+            keep[avail[avail > last].min()] = True
+        if (avail < first).any():                       # MATLAB: ind(max([])) = true is a no-op
+            keep[avail[avail < first].max()] = True
+        assert np.array_equal(out["all_wavelengths"][q], w[keep].astype(np.float64))
+        assert np.array_equal(out["all_flux"][q], (f / med)[keep].astype(np.float64))
+        assert np.array_equal(out["all_noise_variance"][q], (nv / (med * med))[keep].astype(np.float64))
+        assert np.array_equal(out["all_pixel_mask"][q], pm[keep])
+    assert out["all_wavelengths"][2].size == 0 and out["all_normalizers"][2] == 0
+
+
+def test_run_preload_qsos_tree(tmp_path):
+    spectra = tmp_path / "dr12q" / "spectra"
+    for plate, mjd, fiber in ((4000, 55000, 12), (4001, 55001, 7)):
+        d = spectra / str(plate)
+        d.mkdir(parents=True)
+        shutil.copy(GOLDEN / "speclite_fixture.fits", d / f"spec-{plate}-{mjd}-{fiber:04d}.fits")
+    proc = tmp_path / "dr12q" / "processed"
+    proc.mkdir(parents=True)
+    M.savemat73(str(proc / "catalog.mat"), dict(z_qsos=np.array([2.03, 2.5]), plates=np.array([4000, 4001.0]),
+                                                mjds=np.array([55000, 55001.0]), fiber_ids=np.array([12, 7.0]),
+                                                filter_flags=np.array([0, 2], dtype=np.uint8)))
+    out = I.run_preload_qsos(str(tmp_path), "dr12q")
+    assert out["filter_flags"].tolist() == [8, 2]        # too few in-range pixels in the fixture; pre-filtered
+    cat = M.loadmat73(str(proc / "catalog.mat"))
+    assert cat["filter_flags"].ravel().tolist() == [8, 2]
+    pre = M.loadmat73(str(proc / "preloaded_qsos.mat"))
+    assert pre["all_flux"].shape == (2, 1) and float(pre["min_num_pixels"][0, 0]) == 200

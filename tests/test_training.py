@@ -150,10 +150,13 @@ def test_gpu_objective_batches_and_repeat_evaluations_deterministic():
 @pytest.mark.gpu
 def test_gpu_learn_qso_model_decreases_objective():
     model = syn.make_model(k=4)
-    spectra = syn.make_dr12q_like_spectra(model, 8, seed=8)
+    spectra = syn.make_dr12q_like_spectra(model, 24, seed=8)
     out = T.learn_qso_model(spectra, [s["z_qso"] for s in spectra], k=4, max_iter=5, max_fun_evals=20)
     _, _, y, lya, nv = T.prepare_training_data(spectra, [s["z_qso"] for s in spectra])
-    x0, _, _ = T.initial_parameters(y, 4)
+    x0, _, lo = T.initial_parameters(y, 4)
+    bad = ~np.isfinite(lo)
+    x0[4 * 1217:5 * 1217][bad] = np.median(lo[~bad])
+    x0 = np.nan_to_num(x0)
     f0, _ = O.objective(x0, y, lya, nv)
     assert out["M"].shape == (1217, 4) and np.isfinite(out["log_likelihood"])
     assert out["log_likelihood"] < f0
