@@ -20,6 +20,9 @@
 #ifndef GPDLA_FAST_EXP
 #define GPDLA_FAST_EXP 1
 #endif
+#ifndef GPDLA_LDL_REGISTERS
+#define GPDLA_LDL_REGISTERS 1
+#endif
 
 namespace gpdla {
 

@@ -183,6 +183,107 @@ __global__ __launch_bounds__(256) void ldl_batch_kernel(LdlArgs a) {
   emit(ll);
 }
 
+// Register form of the same augmented LDL^T (k <= 63): one wave per sample, lane j holds column
+// j of [[I + Gram, u], [u', sum r^2/d]] (rows 0..k) in VGPRs.  At pivot p every lane j > p
+// updates its column with column p.  Column p is row p by symmetry, and row p is spread over the
+// lanes (lane i holds A(p, i) = A(i, p) in col[p]): one ds_write_b64 per pivot publishes it to a
+// 64-double LDS line that every lane then reads by broadcast (2 entries per ds_read_b128), so the
+// update is ~1.5 instructions per entry with no cross-lane shuffles and no barrier (the wave's
+// LDS operations complete in order).  KB bounds k + 1 at compile time (register arrays, unrolled
+// pivots); the rank itself is a.k.
+__device__ inline double readlane_d(double v, int lane) {
+  const int lo = __builtin_amdgcn_readlane(__double2loint(v), lane);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), lane);
+  return __hiloint2double(hi, lo);
+}
+
+template <int KB>
+__global__ __launch_bounds__(256) void ldl_reg_kernel(LdlArgs a) {
+  constexpr int kStage = (KB - 1) * KB / 2 + KB;  // packed Gram + u of the largest rank in the bucket
+  __shared__ __attribute__((aligned(16))) double rowp_all[4][64];
+  __shared__ __attribute__((aligned(16))) double stage_all[4][kStage];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  double* rowp = rowp_all[wave];
+  double* stage = stage_all[wave];
+  const int sl = blockIdx.x * 4 + wave;
+  if (sl >= a.sc) return;  // wave-uniform
+  const int K = a.k;
+  const int64_t s = a.s0 + sl;
+  const SpecInfo inf = a.info[a.q];
+  auto emit = [&](double ll) {
+    if (lane != 0) return;
+    if (s == a.S) *a.ll_null = ll;
+    else if (a.sample_ll) a.sample_ll[a.perm[s]] = ll;
+  };
+  if (inf.J == 0) {
+    emit(NAN);
+    return;
+  }
+  const int64_t E = (int64_t)K * (K + 1) / 2;
+  const double* Gs = a.G + (int64_t)sl * E;
+  const double* Us = a.U + (int64_t)sl * K;
+  const double* q = a.q1p + (int64_t)sl * 4;
+  const double* l4 = a.ldp + (int64_t)sl * 4;
+  const int j = lane;
+  // the sample's packed Gram and u, copied coalesced into this wave's LDS slice, then gathered
+  // column-wise (the lower half of a column is strided in the packed layout)
+  for (int t = lane; t < E; t += 64) stage[t] = Gs[t];
+  for (int t = lane; t < K; t += 64) stage[E + t] = Us[t];
+  __builtin_amdgcn_wave_barrier();
+  double col[KB];
+#pragma unroll
+  for (int i = 0; i < KB; ++i) {
+    double v = 0.0;
+    if (i <= K && j <= K) {
+      if (i < K && j < K) {
+        const int r = i < j ? i : j, c = i < j ? j : i;  // Gram (r, c), row-major upper
+        v = stage[r * K - r * (r - 1) / 2 + (c - r)] + (i == j ? 1.0 : 0.0);  // B = I + Gram
+      } else if (i == K && j == K) {
+        v = ((q[0] + q[1]) + q[2]) + q[3];  // sum r^2 / d
+      } else {
+        v = stage[E + (i == K ? j : i)];  // u in row k / column k
+      }
+    }
+    col[i] = v;
+  }
+  double pb = 1.0;  // prod D_p = pb 2^eb (frexp-renormalised, one log at the end)
+  int eb = 0;
+  bool bad = false;
+#pragma unroll
+  for (int p = 0; p < KB - 1; ++p) {
+    if (p < K) {
+      rowp[j] = col[p];                 // row p = column p, lane i -> A(i, p)
+      __builtin_amdgcn_wave_barrier();
+      const double d = readlane_d(col[p], p);  // the pivot straight from lane p (no LDS round trip)
+      bad |= !(d > 0.0);
+      pb *= d;
+      if ((p & 3) == 3) {
+        int ex;
+        pb = frexp(pb, &ex);
+        eb += ex;
+      }
+      const double f = (j > p && j <= K) ? col[p] * rcp_nr(d) : 0.0;  // A(j, p) / D_p
+      // rows past k hold zeros in every lane and stay zero: no per-row guard
+#pragma unroll
+      for (int i = p + 1; i < KB; ++i) col[i] = fma(-rowp[i], f, col[i]);  // A(i,j) -= A(i,p) A(j,p) / D_p
+      __builtin_amdgcn_wave_barrier();
+    }
+  }
+  double diag = 0.0;  // A(k, k) of lane k = r'D^-1 r - u'B^-1 u
+#pragma unroll
+  for (int i = 0; i < KB; ++i)
+    if (i == K) diag = col[i];
+  const double quad = readlane_d(diag, K);
+  const double logdet_d = ((l4[0] + l4[1]) + l4[2]) + l4[3];
+  const double logdet_b = log(pb) + eb * kLn2;
+  double ll = -0.5 * (quad + (logdet_d + logdet_b) + inf.n * kLog2Pi);  // log_mvnpdf_low_rank.m:30-32
+  if (bad || !(fabs(ll) < INFINITY)) {
+    ll = NAN;
+    if (lane == 0) atomicOr(a.status, 1);
+  }
+  emit(ll);
+}
+
 }  // namespace
 
 hipError_t launch_weights(const WeightsArgs& a, hipStream_t s) {
@@ -196,7 +297,17 @@ hipError_t launch_weights(const WeightsArgs& a, hipStream_t s) {
 
 hipError_t launch_ldl_batch(const LdlArgs& a, hipStream_t s) {
   if (a.k < 1 || a.k > kGemmMaxK) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(ldl_batch_kernel, dim3((unsigned)((a.sc + 3) / 4)), dim3(256), 0, s, a);
+  const dim3 grid((unsigned)((a.sc + 3) / 4)), blk(256);
+#if GPDLA_LDL_REGISTERS
+  // register path: column j of the augmented (k+1) x (k+1) matrix in lane j (k <= 63)
+  if (a.k <= 15) hipLaunchKernelGGL(ldl_reg_kernel<16>, grid, blk, 0, s, a);
+  else if (a.k <= 31) hipLaunchKernelGGL(ldl_reg_kernel<32>, grid, blk, 0, s, a);
+  else if (a.k <= 47) hipLaunchKernelGGL(ldl_reg_kernel<48>, grid, blk, 0, s, a);
+  else if (a.k <= 51) hipLaunchKernelGGL(ldl_reg_kernel<52>, grid, blk, 0, s, a);   // configs[4]: k = 50
+  else if (a.k <= 63) hipLaunchKernelGGL(ldl_reg_kernel<64>, grid, blk, 0, s, a);
+  else
+#endif
+    hipLaunchKernelGGL(ldl_batch_kernel, grid, blk, 0, s, a);
   return hipGetLastError();
 }
 
