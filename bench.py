@@ -112,7 +112,7 @@ WORKLOADS = {
 
 
 # rocprofv3 summary of this workload (tools/profile.sh + tools/summarize_profile.py), committed
-PROFILE_SUMMARY = ROOT / "profiles" / "r1d_summary.json"
+PROFILE_SUMMARY = ROOT / "profiles" / "r1e_summary.json"
 
 
 def profiled_traffic(Q: int, S: int, k: int):
@@ -256,7 +256,7 @@ def main():
                      "frac": achieved_tf / FP64_PEAK_TFLOPS, "traffic": traffic,
                      "traffic_source": traffic_src,
                      "kernel": (f"likelihood_kernel<{args.k}>" if path == "fused"
-                                else "weights_kernel + rocBLAS dgemm + ldl_batch_kernel (per batch)"),
+                                else "weights_kernel + rocBLAS dgemm + ldl_reg_kernel (per batch)"),
                      "avg_launch_ms": avg_ms,
                      "flops_per_eval": algorithmic_flops_per_eval(n_mean, args.k),
                      "evals_per_launch": evals_per_launch},
