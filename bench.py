@@ -128,6 +128,21 @@ def profiled_traffic(Q: int, S: int, k: int):
     return None, None
 
 
+class _stdout_to_stderr:
+    """Route fd 1 to fd 2 for a block, so native libraries' prints cannot interleave with the
+    one JSON line rank 0 writes to stdout."""
+
+    def __enter__(self):
+        sys.stdout.flush()
+        self.saved = os.dup(1)
+        os.dup2(2, 1)
+
+    def __exit__(self, *exc):
+        sys.stdout.flush()
+        os.dup2(self.saved, 1)
+        os.close(self.saved)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -151,7 +166,8 @@ def main():
         import torch
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        with _stdout_to_stderr():  # gloo prints its connection banner on stdout (fd 1)
+            dist.init_process_group("gloo", rank=rank, world_size=world)
 
     from gp_dla_detection_amd import _lib as L
     from gp_dla_detection_amd import synthetic as syn
@@ -181,15 +197,17 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and args.cpu_budget > 0:
         cpu = cpu_baseline(model, samples, spectra, args.cpu_budget)
-    D = lambda a: L.DeviceArray.from_numpy(a, device=local_rank)
+    # one GPU per local rank; on a box with fewer GPUs than ranks (rehearsal) ranks share devices
+    dev = local_rank % max(1, L.load().gpdla_device_count())
+    D = lambda a: L.DeviceArray.from_numpy(a, device=dev)
     t = {key: D(packed[key]) for key in ("wavelengths", "flux", "noise_variance", "pixel_mask", "z_qsos")}
     S = args.samples
-    o_null = L.DeviceArray(local_rank, Q, np.float64)
-    o_dla = L.DeviceArray(local_rank, Q, np.float64)
-    o_s = L.DeviceArray(local_rank, (Q, S), np.float64)
-    o_n = L.DeviceArray(local_rank, Q, np.int32)
+    o_null = L.DeviceArray(dev, Q, np.float64)
+    o_dla = L.DeviceArray(dev, Q, np.float64)
+    o_s = L.DeviceArray(dev, (Q, S), np.float64)
+    o_n = L.DeviceArray(dev, Q, np.int32)
 
-    eng = Engine(model, samples, set_parameters(k=args.k), device=local_rank)
+    eng = Engine(model, samples, set_parameters(k=args.k), device=dev)
     path = "fused" if args.k in (4, 8, 10, 12, 16, 20, 24) else "panel-GEMM"
 
     def step():
@@ -274,7 +292,8 @@ def main():
         print(json.dumps(result), flush=True)
     eng.close()
     if world > 1:
-        dist.destroy_process_group()
+        with _stdout_to_stderr():
+            dist.destroy_process_group()
 
 
 if __name__ == "__main__":
