@@ -446,8 +446,8 @@ int gpdla_engine_process(gpdla_engine* e, const gpdla_spectra* sp, const gpdla_r
       if ((rc = grow(&e->d_wu, &e->cap_wu, (size_t)(cap_max * sc_max)))) return rc;
       if ((rc = grow(&e->d_G, &e->cap_G, (size_t)(E * sc_max)))) return rc;
       if ((rc = grow(&e->d_U, &e->cap_U, (size_t)(e->K * sc_max)))) return rc;
-      if ((rc = grow(&e->d_q1p, &e->cap_q1p, (size_t)(4 * sc_max)))) return rc;
-      if ((rc = grow(&e->d_ldp, &e->cap_ldp, (size_t)(4 * sc_max)))) return rc;
+      if ((rc = grow(&e->d_q1p, &e->cap_q1p, (size_t)(kWeightParts * sc_max)))) return rc;
+      if ((rc = grow(&e->d_ldp, &e->cap_ldp, (size_t)(kWeightParts * sc_max)))) return rc;
     } else {
       if ((rc = grow(&e->d_scratch, &e->cap_scr, (size_t)blocks_x * nq * kSamplesPerBlock * es))) return rc;
     }

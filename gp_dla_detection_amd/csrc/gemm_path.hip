@@ -19,9 +19,12 @@ namespace gpdla {
 
 namespace {
 
-// One wave per segment (4 per block), lanes over 64 consecutive samples of the chunk; the wave
-// walks its segment's slots with the same register sliding window as the fused kernel.  Writes
-// are coalesced (sample-contiguous rows), slot scalars are wave-uniform loads.
+// One wave per (segment g, quarter h) of the slot sweep (4 per block, blockIdx.y = h), lanes over
+// 64 consecutive samples of the chunk; the wave walks its Ls/4 slots with the same register
+// sliding window as the fused kernel (warmed up at its first slot).  Splitting each segment in
+// four gives 16 waves per CU for a 16,384-sample chunk (4 with whole segments).  Writes are
+// coalesced (sample-contiguous rows), slot scalars are wave-uniform loads; sum r^2/d and
+// sum log d are left as kWeightParts partials per sample.
 template <int NL>
 __global__ __launch_bounds__(256) void weights_kernel(WeightsArgs a) {
   constexpr int kWingLds = 4 * ((3 * kWingStride + 3) / 4);
@@ -44,6 +47,9 @@ __global__ __launch_bounds__(256) void weights_kernel(WeightsArgs a) {
   }
   const int L = inf.L;
   const int Ls = ((L + kChunkSteps - 1) / kChunkSteps) * kChunkSteps;
+  const int h = blockIdx.y;                       // quarter of the segment
+  const int Lq = Ls / kWeightQuarters;            // Ls is a multiple of kChunkSteps = 4
+  const int t0 = h * Lq;
   // null model (s == S) and idle lanes: N = 0, absorption exactly 1 (see kernels.hip)
   const double off = (s < a.S) ? a.offsets[s] : 0.5;
   const double N = (s < a.S) ? a.nhi[s] : 0.0;
@@ -56,13 +62,15 @@ __global__ __launch_bounds__(256) void weights_kernel(WeightsArgs a) {
     if constexpr (NL == 3) return raw_profile3(lam, afac, N, core_lds, wing_lds, exp_lds);
     else return raw_profile(lam, zfac, N, a.num_lines, a.lines);
   };
-  const double* lamp = a.lam_pad + (int64_t)g * L;
+  // window at pixel-order position g L + t0: raw profile at padded positions +0..+5 (the tail
+  // beyond the spectrum is replicated, so every position is finite)
+  const double* lamp = a.lam_pad + (int64_t)g * L + t0;
   double w0 = raw(lamp[0]), w1 = raw(lamp[1]), w2 = raw(lamp[2]);
   double w3 = raw(lamp[3]), w4 = raw(lamp[4]), w5 = raw(lamp[5]);
   double q1 = 0.0, pm = 1.0;
   int pe = 0;
   const int64_t ldw = a.sc;
-  for (int t = 0; t < Ls; ++t) {
+  for (int t = t0; t < t0 + Lq; ++t) {
     const int64_t slot = (int64_t)g * Ls + t;
     const double* sr = a.srow + slot * 8;
     const double lam = sr[0], y = sr[1], noise = sr[2], mu = sr[3], om2 = sr[4];
@@ -82,7 +90,7 @@ __global__ __launch_bounds__(256) void weights_kernel(WeightsArgs a) {
     const double rd = r * dinv;
     q1 = fma(r, rd, q1);
     pm *= d;
-    if ((t & 3) == 3) {
+    if (((t - t0) & 3) == 3) {
       int ex;
       pm = frexp(pm, &ex);
       pe += ex;
@@ -93,16 +101,26 @@ __global__ __launch_bounds__(256) void weights_kernel(WeightsArgs a) {
     }
   }
   // slots past the 4 segments (capacity slack) are neutral rows of the panel: weight 0
-  for (int64_t slot = 4 * (int64_t)Ls + g; slot < a.cap; slot += 4) {
-    if (active) {
-      a.wg[slot * ldw + sl] = 0.0;
-      a.wu[slot * ldw + sl] = 0.0;
+  if (h == 0) {
+    for (int64_t slot = 4 * (int64_t)Ls + g; slot < a.cap; slot += 4) {
+      if (active) {
+        a.wg[slot * ldw + sl] = 0.0;
+        a.wu[slot * ldw + sl] = 0.0;
+      }
     }
   }
   if (active) {
-    a.q1p[(int64_t)sl * 4 + g] = q1;
-    a.ldp[(int64_t)sl * 4 + g] = log(pm) + pe * kLn2;
+    a.q1p[(int64_t)sl * kWeightParts + g * kWeightQuarters + h] = q1;
+    a.ldp[(int64_t)sl * kWeightParts + g * kWeightQuarters + h] = log(pm) + pe * kLn2;
   }
+}
+
+// the kWeightParts per-sample partials of sum r^2/d or sum log d, in slot order
+__device__ inline double sum_parts(const double* p) {
+  double acc = 0.0;
+#pragma unroll
+  for (int i = 0; i < kWeightParts; ++i) acc += p[i];
+  return acc;
 }
 
 // Augmented LDL^T per sample, one wave per sample (4 per block), matrix packed lower-triangular
@@ -154,10 +172,10 @@ __global__ __launch_bounds__(256) void ldl_batch_kernel(LdlArgs a) {
     start += K - r;
   }
   for (int j = lane; j < K; j += 64) at(K, j) = a.U[(int64_t)sl * K + j];
-  const double* q = a.q1p + (int64_t)sl * 4;
-  const double* l4 = a.ldp + (int64_t)sl * 4;
-  if (lane == 0) at(K, K) = ((q[0] + q[1]) + q[2]) + q[3];
-  const double logdet_d = ((l4[0] + l4[1]) + l4[2]) + l4[3];
+  const double* q = a.q1p + (int64_t)sl * kWeightParts;
+  const double* l4 = a.ldp + (int64_t)sl * kWeightParts;
+  if (lane == 0) at(K, K) = sum_parts(q);
+  const double logdet_d = sum_parts(l4);
   wave_sync();
   double logdet_b = 0.0;
   bool bad = false;
@@ -222,8 +240,8 @@ __global__ __launch_bounds__(256) void ldl_reg_kernel(LdlArgs a) {
   const int64_t E = (int64_t)K * (K + 1) / 2;
   const double* Gs = a.G + (int64_t)sl * E;
   const double* Us = a.U + (int64_t)sl * K;
-  const double* q = a.q1p + (int64_t)sl * 4;
-  const double* l4 = a.ldp + (int64_t)sl * 4;
+  const double* q = a.q1p + (int64_t)sl * kWeightParts;
+  const double* l4 = a.ldp + (int64_t)sl * kWeightParts;
   const int j = lane;
   // the sample's packed Gram and u, copied coalesced into this wave's LDS slice, then gathered
   // column-wise (the lower half of a column is strided in the packed layout)
@@ -239,7 +257,7 @@ __global__ __launch_bounds__(256) void ldl_reg_kernel(LdlArgs a) {
         const int r = i < j ? i : j, c = i < j ? j : i;  // Gram (r, c), row-major upper
         v = stage[r * K - r * (r - 1) / 2 + (c - r)] + (i == j ? 1.0 : 0.0);  // B = I + Gram
       } else if (i == K && j == K) {
-        v = ((q[0] + q[1]) + q[2]) + q[3];  // sum r^2 / d
+        v = sum_parts(q);  // sum r^2 / d
       } else {
         v = stage[E + (i == K ? j : i)];  // u in row k / column k
       }
@@ -274,7 +292,7 @@ __global__ __launch_bounds__(256) void ldl_reg_kernel(LdlArgs a) {
   for (int i = 0; i < KB; ++i)
     if (i == K) diag = col[i];
   const double quad = readlane_d(diag, K);
-  const double logdet_d = ((l4[0] + l4[1]) + l4[2]) + l4[3];
+  const double logdet_d = sum_parts(l4);
   const double logdet_b = log(pb) + eb * kLn2;
   double ll = -0.5 * (quad + (logdet_d + logdet_b) + inf.n * kLog2Pi);  // log_mvnpdf_low_rank.m:30-32
   if (bad || !(fabs(ll) < INFINITY)) {
@@ -287,11 +305,11 @@ __global__ __launch_bounds__(256) void ldl_reg_kernel(LdlArgs a) {
 }  // namespace
 
 hipError_t launch_weights(const WeightsArgs& a, hipStream_t s) {
-  const unsigned blocks = (unsigned)((a.sc + 63) / 64);
+  const dim3 grid((unsigned)((a.sc + 63) / 64), kWeightQuarters);
   if (a.num_lines == 3)
-    hipLaunchKernelGGL(weights_kernel<3>, dim3(blocks), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(weights_kernel<3>, grid, dim3(256), 0, s, a);
   else
-    hipLaunchKernelGGL(weights_kernel<0>, dim3(blocks), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(weights_kernel<0>, grid, dim3(256), 0, s, a);
   return hipGetLastError();
 }
 

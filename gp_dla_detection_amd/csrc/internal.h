@@ -127,6 +127,8 @@ struct LineArgs {
 
 // ---- panel-GEMM path (any rank 1..kGemmMaxK; gemm_path.hip + rocBLAS dgemm in engine.hip)
 constexpr int kGemmMaxK = 64;
+constexpr int kWeightQuarters = 4;                 // weights_kernel: waves per segment
+constexpr int kWeightParts = 4 * kWeightQuarters;  // per-sample partial sums (segment x quarter)
 
 struct WeightsArgs {
   const SpecInfo* info;
@@ -142,8 +144,8 @@ struct WeightsArgs {
   LineArgs lines;
   double* wg;                    // [cap][sc] a^2 / d
   double* wu;                    // [cap][sc] a r / d
-  double* q1p;                   // [sc][4] per-segment sum r^2 / d
-  double* ldp;                   // [sc][4] per-segment sum log d
+  double* q1p;                   // [sc][kWeightParts] partial sum r^2 / d
+  double* ldp;                   // [sc][kWeightParts] partial sum log d
 };
 
 struct LdlArgs {
