@@ -218,10 +218,9 @@ __device__ inline double readlane_d(double v, int lane) {
 template <int KB>
 __global__ __launch_bounds__(256) void ldl_reg_kernel(LdlArgs a) {
   constexpr int kStage = (KB - 1) * KB / 2 + KB;  // packed Gram + u of the largest rank in the bucket
-  __shared__ __attribute__((aligned(16))) double rowp_all[4][64];
+  __shared__ __attribute__((aligned(16))) double rowp_all[4][2][64];  // double-buffered by pivot parity
   __shared__ __attribute__((aligned(16))) double stage_all[4][kStage];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  double* rowp = rowp_all[wave];
   double* stage = stage_all[wave];
   const int sl = blockIdx.x * 4 + wave;
   if (sl >= a.sc) return;  // wave-uniform
@@ -245,8 +244,20 @@ __global__ __launch_bounds__(256) void ldl_reg_kernel(LdlArgs a) {
   const int j = lane;
   // the sample's packed Gram and u, copied coalesced into this wave's LDS slice, then gathered
   // column-wise (the lower half of a column is strided in the packed layout)
-  for (int t = lane; t < E; t += 64) stage[t] = Gs[t];
-  for (int t = lane; t < K; t += 64) stage[E + t] = Us[t];
+  {  // all loads in flight before the first LDS store (one global-memory latency, not ~20)
+    constexpr int kIt = (kStage + 63) / 64;
+    double tmp[kIt];
+#pragma unroll
+    for (int it = 0; it < kIt; ++it) {
+      const int t = it * 64 + lane;
+      tmp[it] = t < E ? Gs[t] : (t < E + K ? Us[t - E] : 0.0);
+    }
+#pragma unroll
+    for (int it = 0; it < kIt; ++it) {
+      const int t = it * 64 + lane;
+      if (t < E + K) stage[t] = tmp[it];
+    }
+  }
   __builtin_amdgcn_wave_barrier();
   double col[KB];
 #pragma unroll
@@ -270,6 +281,9 @@ __global__ __launch_bounds__(256) void ldl_reg_kernel(LdlArgs a) {
 #pragma unroll
   for (int p = 0; p < KB - 1; ++p) {
     if (p < K) {
+      // two LDS lines alternate, so pivot p + 1's store cannot overwrite the line pivot p is
+      // still reading; the one wave barrier orders this pivot's store before its loads
+      double* rowp = rowp_all[wave][p & 1];
       rowp[j] = col[p];                 // row p = column p, lane i -> A(i, p)
       __builtin_amdgcn_wave_barrier();
       const double d = readlane_d(col[p], p);  // the pivot straight from lane p (no LDS round trip)
@@ -284,7 +298,6 @@ __global__ __launch_bounds__(256) void ldl_reg_kernel(LdlArgs a) {
       // rows past k hold zeros in every lane and stay zero: no per-row guard
 #pragma unroll
       for (int i = p + 1; i < KB; ++i) col[i] = fma(-rowp[i], f, col[i]);  // A(i,j) -= A(i,p) A(j,p) / D_p
-      __builtin_amdgcn_wave_barrier();
     }
   }
   double diag = 0.0;  // A(k, k) of lane k = r'D^-1 r - u'B^-1 u
