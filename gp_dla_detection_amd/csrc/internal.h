@@ -51,8 +51,12 @@ struct Layout {
   static constexpr int kTiles = kGT + kUT;
   static constexpr int kJS = ((kTiles + 2) + 1) & ~1;  // per-j stride (doubles), even
   static constexpr int kRow = 4 * kJS;                 // doubles per slot row (HBM panel stride)
-  static constexpr int kRowL = (kRow + 127) & ~127;    // LDS row stride: whole 1 KiB DMA pieces
+  static constexpr int kRowL = (kRow + 127) & ~127;    // DMA span per row: whole 1 KiB pieces
   static constexpr int kPieces = kRowL / 128;          // global_load_lds_dwordx4 per staged row
+  // LDS row stride: the span plus 16 B, so the 4 segment rows a ds_read_b128 lane group touches
+  // start in different bank quads (with the bare span, rows g and g+1 hit the same banks: every
+  // B-operand read was a 2-way conflict, SQ_LDS_BANK_CONFLICT = 36% of LDS cycles, profiles/r1f)
+  static constexpr int kRowS = kRowL + 2;
   static constexpr int kES = 4 * kTiles + 8;           // epilogue doubles per sample (Gram, u, scalars)
   // slot scalars in the spare words
   static constexpr int kLam = 0 * kJS + kTiles;        // padded wavelength at slot + 6

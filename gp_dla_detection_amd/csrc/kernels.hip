@@ -315,7 +315,7 @@ __device__ inline void stage_chunk(const double* __restrict__ panel, int Ls, int
 #pragma unroll
   for (int tt = 0; tt < kChunkSteps; ++tt) {
     const double* src = panel + ((int64_t)wave_s * Ls + c * kChunkSteps + tt) * Lay::kRow;
-    const uint32_t dst = buf + (uint32_t)((tt * 4 + wave_s) * Lay::kRowL * 8);
+    const uint32_t dst = buf + (uint32_t)((tt * 4 + wave_s) * Lay::kRowS * 8);
 #pragma unroll
     for (int h = 0; h < Lay::kPieces; ++h) {
 #pragma clang diagnostic push
@@ -332,9 +332,9 @@ __global__ __launch_bounds__(256, (K <= 20 ? GPDLA_WAVES_PER_EU : 1)) void likel
   using Lay = Layout<K>;
   constexpr int kTiles = Lay::kTiles;
   constexpr int kGT = Lay::kGT;
-  constexpr int kRowL = Lay::kRowL;
+  constexpr int kRowS = Lay::kRowS;
   constexpr int kJS = Lay::kJS;
-  constexpr int kBuf = 4 * kChunkSteps * kRowL;
+  constexpr int kBuf = 4 * kChunkSteps * kRowS;
   static_assert(kWavesPerBlock == 4, "stage_chunk: one wave per segment");
   constexpr int kWingLds = 4 * ((3 * kWingStride + 3) / 4);
   constexpr int kCoreLds = NL == 3 ? 3 * kCoreTable + kWingLds + 64 : 1;
@@ -420,7 +420,7 @@ __global__ __launch_bounds__(256, (K <= 20 ? GPDLA_WAVES_PER_EU : 1)) void likel
       stage_chunk<K>(panel, Ls, c + 1, lds_base + (uint32_t)(((c + 1) & 1) * kBuf * 8), wave_s, voff);
 #pragma unroll
     for (int tt = 0; tt < kChunkSteps; ++tt) {
-      const double* row = cur + (tt * 4 + g) * kRowL;
+      const double* row = cur + (tt * 4 + g) * kRowS;
       double lam, y, noise, mu, om2;
       if constexpr ((kTiles & 1) == 0) {
         const double2 s0 = *reinterpret_cast<const double2*>(row + Lay::kLam);
