@@ -8,6 +8,8 @@ VARIANTS = {
     "f1_e1": dict(GPDLA_SCHED_FENCE=1, GPDLA_FAST_EXP=1),
     "f1_e0": dict(GPDLA_SCHED_FENCE=1, GPDLA_FAST_EXP=0),
     "f0_e1": dict(GPDLA_SCHED_FENCE=0, GPDLA_FAST_EXP=1),
+    "f1_w1": dict(GPDLA_SCHED_FENCE=1, GPDLA_WAVES_PER_EU=1),
+    "f0_w1": dict(GPDLA_SCHED_FENCE=0, GPDLA_WAVES_PER_EU=1),
 }
 if __name__ == "__main__":
     names = sys.argv[1:] or list(VARIANTS)
