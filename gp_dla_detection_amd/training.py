@@ -231,3 +231,31 @@ def learn_qso_model(spectra, z_qsos, k: int = P.K, max_iter: int = 2000, max_fun
                 max_noise_variance=P.MAX_NOISE_VARIANCE,
                 minFunc_output=dict(iterations=res.nit, funcCount=evals, message=str(res.message),
                                     nonfinite_initial_log_omega=int(np.count_nonzero(bad))))
+
+
+def run_learn_qso_model(base_directory: str, training_release: str, training_set_name: str, train_ind,
+                        k: int = P.K, max_iter: int = 2000, max_fun_evals: int = 4000, device: int = 0) -> dict:
+    """The script on files (learn_qso_model.m:1-131): catalog.mat and preloaded_qsos.mat of
+    ``training_release`` in, learned_qso_model_<training_set_name>.mat (v7.3) out.  ``train_ind``
+    is the reference's index expression over ``catalog`` (e.g. README.md:148-152), a callable or
+    a boolean array."""
+    from .matv73 import loadmat, savemat73
+    from .process import evaluate_index, load_preloaded_qsos, processed_directory
+    d = processed_directory(base_directory, training_release)
+    catalog = loadmat(f"{d}/catalog.mat")
+    tind = evaluate_index(train_ind, catalog=catalog).astype(bool).ravel()
+    spectra = load_preloaded_qsos(f"{d}/preloaded_qsos.mat", tind)                 # :10-19
+    z_qsos = np.asarray(catalog["z_qsos"], dtype=np.float64).ravel()[tind]          # :21
+    out = learn_qso_model(spectra, z_qsos, k=k, max_iter=max_iter, max_fun_evals=max_fun_evals, device=device)
+    save = {key: val for key, val in out.items() if key != "minFunc_output"}
+    save["minFunc_output"] = {kk: (vv if isinstance(vv, str) else np.float64(vv))
+                              for kk, vv in out["minFunc_output"].items()}
+    save.update(training_release=training_release, train_ind=tind,
+                minFunc_options=dict(MaxIter=np.float64(max_iter), MaxFunEvals=np.float64(max_fun_evals)))
+    for key in ("rest_wavelengths", "mu", "log_omega", "initial_log_omega"):
+        save[key] = np.asarray(save[key], dtype=np.float64).reshape(1, -1)          # MATLAB rows
+    for key in ("log_c_0", "log_tau_0", "log_beta", "log_likelihood", "initial_log_c_0",
+                "initial_tau_0", "initial_beta", "max_noise_variance"):
+        save[key] = np.float64(save[key])
+    savemat73(f"{d}/learned_qso_model_{training_set_name}.mat", save)              # :122-131
+    return out

@@ -101,3 +101,16 @@ def test_run_preload_qsos_tree(tmp_path):
     assert cat["filter_flags"].ravel().tolist() == [8, 2]
     pre = M.loadmat73(str(proc / "preloaded_qsos.mat"))
     assert pre["all_flux"].shape == (2, 1) and float(pre["min_num_pixels"][0, 0]) == 200
+
+
+def test_own_fits_writer_roundtrip(tmp_path):
+    """The test-side writer (tests/fits_writer.py) produces files the reader reads back exactly."""
+    from fits_writer import write_speclite
+    rng = np.random.default_rng(5)
+    n = 300
+    f, ll = rng.normal(3, 1, n).astype(np.float32), (3.55 + 1e-4 * np.arange(n)).astype(np.float32)
+    iv, am = rng.uniform(0, 2, n).astype(np.float32), rng.integers(0, 2 ** 30, n).astype(np.int32)
+    write_speclite(str(tmp_path / "s.fits"), f, ll, iv, am)
+    got = I.read_bintable(str(tmp_path / "s.fits"), 1)
+    for a, b in zip(got, (f, ll, iv, am)):
+        assert np.array_equal(a, b)
