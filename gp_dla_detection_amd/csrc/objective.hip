@@ -330,12 +330,21 @@ int obj_run(gpdla_objective* o, const double* dM_src, const double* lo_src, cons
     a.part_dlo = o->part_dlo;
     a.part_s = o->part_s;
     const dim3 grid((unsigned)nq), blk(kObjThreads);
-    if (k <= 8) hipLaunchKernelGGL(objective_spectrum_kernel<8>, grid, blk, shm, o->stream, a);
-    else if (k <= 16) hipLaunchKernelGGL(objective_spectrum_kernel<16>, grid, blk, shm, o->stream, a);
-    else if (k <= 24) hipLaunchKernelGGL(objective_spectrum_kernel<24>, grid, blk, shm, o->stream, a);
-    else if (k <= 32) hipLaunchKernelGGL(objective_spectrum_kernel<32>, grid, blk, shm, o->stream, a);
-    else hipLaunchKernelGGL(objective_spectrum_kernel<64>, grid, blk, shm, o->stream, a);
-    HIP_TRY(hipGetLastError());
+    // dynamic LDS above 64 KiB (long rest grids with high rank) must be opted into per kernel
+    auto launch = [&](auto kern) -> int {
+      if (shm > 65536)
+        HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
+      hipLaunchKernelGGL(kern, grid, blk, shm, o->stream, a);
+      HIP_TRY(hipGetLastError());
+      return GPDLA_OK;
+    };
+    int rc = k <= 8 ? launch(objective_spectrum_kernel<8>)
+             : k <= 16 ? launch(objective_spectrum_kernel<16>)
+             : k <= 24 ? launch(objective_spectrum_kernel<24>)
+             : k <= 32 ? launch(objective_spectrum_kernel<32>)
+                       : launch(objective_spectrum_kernel<64>);
+    if (rc) return rc;
     hipLaunchKernelGGL(objective_sum_kernel, dim3((unsigned)((per_dM + 255) / 256)), dim3(256), 0, o->stream,
                        nq, per_dM, (const double*)o->part_dM, o->tot);
     hipLaunchKernelGGL(objective_sum_kernel, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, o->stream,

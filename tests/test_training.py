@@ -160,3 +160,20 @@ def test_gpu_learn_qso_model_decreases_objective():
     f0, _ = O.objective(x0, y, lya, nv)
     assert out["M"].shape == (1217, 4) and np.isfinite(out["log_likelihood"])
     assert out["log_likelihood"] < f0
+
+
+@pytest.mark.gpu
+def test_gpu_objective_large_grid_high_rank():
+    """> 64 KiB of dynamic LDS per block (3,000-pixel rows, k = 40) against the oracle."""
+    rng = np.random.default_rng(9)
+    Q, Pn, k = 3, 3000, 40
+    y = 0.3 * rng.standard_normal((Q, Pn))
+    y[rng.uniform(size=y.shape) < 0.2] = np.nan
+    lya = rng.uniform(2.5, 4.5, (Q, Pn))
+    nv = rng.uniform(0.01, 0.1, (Q, Pn))
+    x = np.concatenate([0.05 * rng.standard_normal(Pn * k), np.log(0.15) + 0.1 * rng.standard_normal(Pn),
+                        [np.log(0.1), np.log(0.0023), np.log(3.65)]])
+    f, g = T.objective(x, y, lya, nv)
+    fr, gr = O.objective(x, y, lya, nv)
+    assert f == pytest.approx(fr, rel=1e-11)
+    np.testing.assert_allclose(g, gr, rtol=1e-8, atol=1e-11 * np.abs(gr).max())
