@@ -65,10 +65,10 @@ class LazyArray:
 
     ``shape`` is the MATLAB shape (e.g. (Q, S)); ``fill(view)`` receives a writable
     array of that MATLAB shape and dtype (a Fortran-ordered view of the file's bytes) and must
-    assign every element."""
+    assign every element.  ``fill=None`` defers the bytes to other writers (``open_region``)."""
     shape: tuple
     dtype: np.dtype
-    fill: Callable[[np.ndarray], None]
+    fill: Callable[[np.ndarray], None] | None = None
 
 
 def _dt_message(dt: np.dtype) -> bytes:
@@ -265,9 +265,10 @@ class _Layout:
         return a
 
 
-def savemat73(path: str, variables: dict, created: str | None = None) -> None:
+def savemat73(path: str, variables: dict, created: str | None = None) -> dict:
     """Write ``variables`` (name -> numpy array / scalar / str / list(cell) / LazyArray) as a
-    MATLAB v7.3 file.  1-D arrays become MATLAB column vectors (process_qsos.m's nan(Q, 1))."""
+    MATLAB v7.3 file.  1-D arrays become MATLAB column vectors (process_qsos.m's nan(Q, 1)).
+    Returns {name: Region} for the LazyArray variables."""
     refs: list = []
     top = [_matlab_node(name, val, refs) for name, val in variables.items()]
     root = _Node("/", "group", entries=list(top), attrs=[])
@@ -369,13 +370,35 @@ def savemat73(path: str, variables: dict, created: str | None = None) -> None:
         f.write(ub)
         f.write(bytes(img))
         f.truncate(USERBLOCK + eof)     # lazy regions: sparse until filled through the memory map
+    regions = {}
     for n in lazies:
-        dt = np.dtype(n.dtype).newbyteorder("<")
-        mm = np.memmap(path, dtype=dt, mode="r+", offset=USERBLOCK + data_addr[id(n)],
-                       shape=n.dims)                         # HDF5 (C-order) view
-        n.lazy.fill(mm.T)                                    # = MATLAB shape, column-major
+        reg = Region(USERBLOCK + data_addr[id(n)], tuple(int(d) for d in n.dims), np.dtype(n.dtype).str)
+        regions[n.name] = reg
+        if n.lazy.fill is None:
+            continue                                         # deferred: filled later via open_region
+        mm = open_region(path, reg)
+        n.lazy.fill(mm)
         mm.flush()
         del mm
+    return regions
+
+
+@dataclass(frozen=True)
+class Region:
+    """Where a variable's bytes live in a written file: absolute byte offset, HDF5 (C-order) dims
+    and numpy dtype string.  A ``LazyArray`` with ``fill=None`` is left for other writers (e.g.
+    one process per GPU, each writing its own spectra) to fill through ``open_region``."""
+    offset: int
+    dims: tuple
+    dtype: str
+
+
+def open_region(path: str, region: Region, mode: str = "r+") -> np.ndarray:
+    """A writable view of a variable's data in MATLAB shape (the transpose of a memory map of
+    the HDF5 C-order dims).  Several processes may fill disjoint parts of it concurrently."""
+    mm = np.memmap(path, dtype=np.dtype(region.dtype).newbyteorder("<"), mode=mode,
+                   offset=region.offset, shape=region.dims)
+    return mm.T
 
 
 # ============================================================================ reader
@@ -778,6 +801,42 @@ def _decode(r: _Reader, addr: int):
     return out
 
 
+class MatFile:
+    """Random access to a v7.3 file: ``names()``, ``load(name)`` and ``cell_elements(name,
+    indices)``, which decodes only the selected cells of a cell array (preloaded_qsos.mat at full
+    DR12Q holds 4 x 162,861 cells; a process working on one shard needs its own)."""
+
+    def __init__(self, path: str):
+        self._r = _Reader(path)
+        self._links = self._r.group_links(self._r.root_ohdr)
+
+    def names(self):
+        return [n for n in self._links if not n.startswith("#")]
+
+    def load(self, name: str):
+        return _decode(self._r, self._links[name])
+
+    def cell_elements(self, name: str, indices) -> list:
+        arr, attrs, kind = self._r.dataset(self._links[name])
+        if kind != "ref":
+            raise TypeError(f"{name} is not a cell array")
+        flat = arr.ravel()                  # MATLAB column-major order
+        return [_decode(self._r, int(flat[i])) for i in np.asarray(indices, dtype=np.int64)]
+
+    def cell_count(self, name: str) -> int:
+        arr, _, kind = self._r.dataset(self._links[name])
+        return int(arr.size)
+
+    def close(self):
+        self._r.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
 def loadmat73(path: str, variable_names=None) -> dict:
     """Read a MATLAB v7.3 file into {name: value} with MATLAB shapes (a Q x 1 vector comes back
     as a (Q, 1) array; ``squeeze`` it as scipy's ``squeeze_me`` would)."""
@@ -814,4 +873,4 @@ def loadmat(path: str, variable_names=None) -> dict:
     return {k: v for k, v in d.items() if not k.startswith("__")}
 
 
-__all__ = ["LazyArray", "savemat73", "loadmat73", "loadmat", "is_matv73"]
+__all__ = ["LazyArray", "Region", "MatFile", "savemat73", "open_region", "loadmat73", "loadmat", "is_matv73"]

@@ -81,29 +81,31 @@ def _select(spectra, test_ind):
     return pack_spectra(lst)
 
 
-def process_qsos(model: dict, samples: dict, spectra, prior: dict | None = None,
-                 params: Parameters | None = None, test_ind=None, engine: Engine | None = None,
-                 device: int = 0, metadata: dict | None = None) -> dict:
-    """Run the DLA search (process_qsos.m:88-232) and return the saved variables."""
-    params = params or set_parameters(k=np.asarray(model["M"]).shape[1])
-    packed = _select(spectra, test_ind)
+def _engine_compute(model: dict, samples: dict, packed: dict, params: Parameters, device: int = 0,
+                    engine: Engine | None = None) -> dict:
+    """The hot path on the GPU: per-spectrum null / sample / DLA log likelihoods and z ranges."""
     eng = engine or Engine(model, samples, params, device=device)
     try:
-        res = eng.process(packed, want_samples=True)
+        return eng.process(packed, want_samples=True)
     finally:
         if engine is None:
             eng.close()
-    Q = packed["z_qsos"].size
+
+
+def _finish(res: dict, z_qsos, prior: dict | None, params: Parameters, metadata: dict | None) -> dict:
+    """process_qsos.m:122-132, 150-155, 202-232: priors, posteriors and the saved scalars."""
+    Q = np.asarray(z_qsos).size
     out = dict(
         min_z_dlas=res["min_z_dlas"], max_z_dlas=res["max_z_dlas"],
         log_likelihoods_no_dla=res["log_likelihoods_no_dla"],
-        sample_log_likelihoods_dla=res["sample_log_likelihoods_dla"],
         log_likelihoods_dla=res["log_likelihoods_dla"], num_pixels=res["num_pixels"],
         num_lines=params.num_lines, max_z_cut=params.max_z_cut,
         prior_z_qso_increase=params.prior_z_qso_increase)
+    if "sample_log_likelihoods_dla" in res:
+        out["sample_log_likelihoods_dla"] = res["sample_log_likelihoods_dla"]
     if prior is not None:
         dla_ind = filter_prior_dlas(prior["z_qsos"], prior["dla_ind"], prior.get("z_dlas", [None] * len(prior["z_qsos"])))
-        lp_no, lp_dla = dla_priors(packed["z_qsos"], prior["z_qsos"], dla_ind, params.prior_z_qso_increase)
+        lp_no, lp_dla = dla_priors(z_qsos, prior["z_qsos"], dla_ind, params.prior_z_qso_increase)
     else:
         lp_no, lp_dla = np.full(Q, np.log(0.5)), np.full(Q, np.log(0.5))
     out["log_priors_no_dla"], out["log_priors_dla"] = lp_no, lp_dla
@@ -111,12 +113,23 @@ def process_qsos(model: dict, samples: dict, spectra, prior: dict | None = None,
     out["log_posteriors_dla"] = lp_dla + out["log_likelihoods_dla"]           # process_qsos.m:211-212
     post, p_no, p_dla = model_posteriors(out["log_posteriors_no_dla"], out["log_posteriors_dla"])
     out["model_posteriors"], out["p_no_dlas"], out["p_dlas"] = post, p_no, p_dla
-    if test_ind is not None:
-        out["test_ind"] = np.asarray(test_ind)
     if "numeric_warning" in res:
         out["numeric_warning"] = res["numeric_warning"]
     for key, val in (metadata or {}).items():
         out[key] = val
+    return out
+
+
+def process_qsos(model: dict, samples: dict, spectra, prior: dict | None = None,
+                 params: Parameters | None = None, test_ind=None, engine: Engine | None = None,
+                 device: int = 0, metadata: dict | None = None) -> dict:
+    """Run the DLA search (process_qsos.m:88-232) and return the saved variables."""
+    params = params or set_parameters(k=np.asarray(model["M"]).shape[1])
+    packed = _select(spectra, test_ind)
+    res = _engine_compute(model, samples, packed, params, device, engine)
+    out = _finish(res, packed["z_qsos"], prior, params, metadata)
+    if test_ind is not None:
+        out["test_ind"] = np.asarray(test_ind)
     return out
 
 
@@ -129,7 +142,7 @@ PROCESSED_VARIABLES = ("training_release", "training_set_name", "dla_catalog_nam
                        "p_dlas")
 
 
-def save_processed_qsos(path: str, out: dict, format: str = "v7.3") -> None:
+def save_processed_qsos(path: str, out: dict, format: str = "v7.3") -> dict:
     """``save(filename, variables_to_save{:}, '-v7.3')`` (process_qsos.m:235-249).
 
     MATLAB shapes: Q-vectors are Q x 1 columns, ``sample_log_likelihoods_dla`` is Q x S,
@@ -148,13 +161,13 @@ def save_processed_qsos(path: str, out: dict, format: str = "v7.3") -> None:
         mat[key] = v
     if format == "v7.3":
         from .matv73 import savemat73
-        savemat73(path, mat)
+        return savemat73(path, mat)
     elif format == "v5":
         from scipy.io import savemat
         mat = {k: (v[:, None] if isinstance(v, np.ndarray) and v.ndim == 1 else v) for k, v in mat.items()}
         savemat(path, mat, do_compression=False, oned_as="column")
-    else:
-        raise ValueError("format must be 'v7.3' or 'v5'")
+        return {}
+    raise ValueError("format must be 'v7.3' or 'v5'")
 
 
 # ------------------------------------------------------------------------------ file-level driver
@@ -243,21 +256,35 @@ def save_dla_samples(path: str, samples: dict, **extra) -> None:
 
 def load_preloaded_qsos(path: str, test_ind=None) -> list[dict]:
     """process_qsos.m:45-60 (preloaded_qsos.mat cells, selected by test_ind); z_QSO is attached
-    by the caller from the catalogue."""
-    from .matv73 import loadmat
-    d = loadmat(path, ["all_wavelengths", "all_flux", "all_noise_variance", "all_pixel_mask"])
-    cols = {k: _as_list(d[k]) for k in d}
-    n = len(cols["all_wavelengths"])
-    idx = np.arange(n) if test_ind is None else (
-        np.flatnonzero(test_ind) if np.asarray(test_ind).dtype == bool else np.asarray(test_ind))
-    return [dict(wavelengths=cols["all_wavelengths"][i], flux=cols["all_flux"][i],
-                 noise_variance=cols["all_noise_variance"][i],
-                 pixel_mask=cols["all_pixel_mask"][i].astype(bool)) for i in idx]
+    by the caller from the catalogue.  v7.3 files decode only the selected cells."""
+    from .matv73 import MatFile, is_matv73, loadmat
+    keys = ("all_wavelengths", "all_flux", "all_noise_variance", "all_pixel_mask")
+    if is_matv73(path):
+        with MatFile(path) as mf:
+            n = mf.cell_count("all_wavelengths")
+            idx = _indices(test_ind, n)
+            cols = {k: [np.asarray(c).ravel() for c in mf.cell_elements(k, idx)] for k in keys}
+    else:
+        d = loadmat(path, list(keys))
+        full = {k: _as_list(d[k]) for k in d}
+        idx = _indices(test_ind, len(full["all_wavelengths"]))
+        cols = {k: [full[k][i] for i in idx] for k in keys}
+    return [dict(wavelengths=w, flux=f, noise_variance=v, pixel_mask=m.astype(bool))
+            for w, f, v, m in zip(cols["all_wavelengths"], cols["all_flux"], cols["all_noise_variance"],
+                                  cols["all_pixel_mask"])]
+
+
+def _indices(sel, n: int) -> np.ndarray:
+    if sel is None:
+        return np.arange(n)
+    sel = np.asarray(sel)
+    return np.flatnonzero(sel) if sel.dtype == bool else sel.astype(np.int64)
 
 
 def run_process_qsos(base_directory: str, training_release: str, training_set_name: str,
                      dla_catalog_name: str, prior_ind, release: str, test_set_name: str, test_ind,
-                     params: Parameters | None = None, device: int = 0, save: bool = True) -> dict:
+                     params: Parameters | None = None, device: int = 0, save: bool = True,
+                     rank: int = 0, world: int = 1, compute=None) -> dict:
     """The whole ``process_qsos`` script (process_qsos.m:1-249) on files laid out as the reference
     lays them out (set_parameters.m:79-86):
 
@@ -270,8 +297,19 @@ def run_process_qsos(base_directory: str, training_release: str, training_set_na
     ``prior_ind`` / ``test_ind`` are the reference's index expressions (strings such as
     ``'(catalog.filter_flags == 0)'``), callables or boolean arrays.  The catalogue's
     containers.Map variables (los_inds, dla_inds, z_dlas) are read as structs keyed by catalogue
-    name (MATLAB's MCOS Map objects are opaque outside MATLAB, SURVEY.md 7 viii)."""
-    from .matv73 import loadmat
+    name (MATLAB's MCOS Map objects are opaque outside MATLAB, SURVEY.md 7 viii).
+
+    Multi-GPU (``world`` > 1; one process per GPU with a torch.distributed process group already
+    initialised, gloo suffices): rank r decodes and evaluates only its contiguous shard of the
+    test spectra on ``device``.  Rank 0 gathers the per-spectrum scalars (not the sample
+    arrays), computes priors and posteriors, and writes the file with the Q x S sample array as a
+    deferred region; every rank then writes its own rows of that region in place (disjoint
+    parts of one memory-mapped file), so the 13 GB full-DR12Q array is never gathered.
+    ``compute(model, samples, packed, params, device) -> dict`` replaces the engine (tests).
+    Rank 0 returns the saved scalars; other ranks their local results."""
+    from .matv73 import LazyArray, loadmat, open_region
+    from .shard import contiguous_shards, merge_shards
+    compute = compute or _engine_compute
     tdir, rdir = processed_directory(base_directory, training_release), processed_directory(base_directory, release)
     prior_catalog = loadmat(f"{tdir}/catalog.mat")
     pind = evaluate_index(prior_ind, prior_catalog=prior_catalog, dla_catalog_name=dla_catalog_name).astype(bool).ravel()
@@ -281,18 +319,53 @@ def run_process_qsos(base_directory: str, training_release: str, training_set_na
     pzd = [z_dlas_all[i] for i in np.flatnonzero(pind)]
     model = load_model(f"{tdir}/learned_qso_model_{training_set_name}.mat")
     samples = load_dla_samples(f"{tdir}/dla_samples.mat")
+    params = params or set_parameters(k=np.asarray(model["M"]).shape[1])
     catalog = loadmat(f"{rdir}/catalog.mat")
     tind = evaluate_index(test_ind, catalog=catalog).astype(bool).ravel()
-    spectra = load_preloaded_qsos(f"{rdir}/preloaded_qsos.mat", tind)
-    z_qsos = np.asarray(catalog["z_qsos"], dtype=np.float64).ravel()[tind]
-    for s, z in zip(spectra, z_qsos):
-        s["z_qso"] = float(z)
+    tidx = np.flatnonzero(tind)
+    z_all = np.asarray(catalog["z_qsos"], dtype=np.float64).ravel()[tidx]
+    shards = contiguous_shards(tidx.size, world)
+    mine = shards[rank]
+    spectra = load_preloaded_qsos(f"{rdir}/preloaded_qsos.mat", tidx[mine])
+    for sp, z in zip(spectra, z_all[mine]):
+        sp["z_qso"] = float(z)
+    packed = pack_spectra(spectra) if spectra else dict(
+        offsets=np.zeros(1, np.int64), wavelengths=np.zeros(0), flux=np.zeros(0), noise_variance=np.zeros(0),
+        pixel_mask=np.zeros(0, np.uint8), z_qsos=np.zeros(0))
+    res = compute(model, samples, packed, params, device)
     meta = dict(training_release=training_release, training_set_name=training_set_name,
                 dla_catalog_name=dla_catalog_name, prior_ind=pind, release=release,
                 test_set_name=test_set_name)
     prior = dict(z_qsos=pz, dla_ind=pdla, z_dlas=pzd)
-    out = process_qsos(model, samples, spectra, prior, params=params, device=device, metadata=meta)
-    out["test_ind"] = tind
+    path = f"{rdir}/processed_qsos_{test_set_name}.mat"
+    if world == 1:
+        out = _finish(res, z_all, prior, params, meta)
+        out["test_ind"] = tind
+        if save:
+            save_processed_qsos(path, out)
+        return out
+    import torch.distributed as dist
+    small = {k: v for k, v in res.items() if k != "sample_log_likelihoods_dla"}
+    gathered = [None] * world if rank == 0 else None
+    dist.gather_object(small, gathered, dst=0)
+    region = [None]
+    if rank == 0:
+        merged = merge_shards(tidx.size, shards, gathered)
+        out = _finish(merged, z_all, prior, params, meta)
+        out["test_ind"] = tind
+        if save:
+            S = np.asarray(samples["nhi_samples"]).size
+            out["sample_log_likelihoods_dla"] = LazyArray((tidx.size, S), np.float64)   # deferred
+            region[0] = save_processed_qsos(path, out)["sample_log_likelihoods_dla"]
+            del out["sample_log_likelihoods_dla"]
     if save:
-        save_processed_qsos(f"{rdir}/processed_qsos_{test_set_name}.mat", out)
-    return out
+        dist.broadcast_object_list(region, src=0)
+        view = open_region(path, region[0])
+        if mine.size:
+            view[mine[0]:mine[-1] + 1] = res["sample_log_likelihoods_dla"]      # this rank's rows
+        view.base.flush()
+        del view
+        dist.barrier()
+    return out if rank == 0 else res
+
+

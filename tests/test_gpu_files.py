@@ -47,3 +47,58 @@ def test_run_process_qsos_files(tmp_path):
     assert saved["test_ind"].ravel().tolist() == (catalog["filter_flags"] == 0).tolist()
     post = saved["model_posteriors"]
     assert post.shape == (Q, 2) and np.allclose(post.sum(axis=1), 1)
+
+
+def _rank_worker(rank, world, port, base, q):
+    import os
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from gp_dla_detection_amd import process as PRw
+        devs = L.load().gpdla_device_count()
+        PRw.run_process_qsos(base, "dr12q", "dr9q_minus_concordance", "dr9q_concordance",
+                             " prior_catalog.in_dr9 & prior_catalog.los_inds(dla_catalog_name)", "dr12q", "dr12q",
+                             "(catalog.filter_flags == 0)", device=rank % devs, rank=rank, world=world)
+        q.put(rank)
+    finally:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_run_process_qsos_two_ranks(tmp_path):
+    """One process per GPU (ranks share the device on a one-GPU box): the sharded run writes the
+    same processed_qsos file as the single-process run."""
+    import socket
+
+    import torch.multiprocessing as mp
+    single, multi = tmp_path / "single", tmp_path / "multi"
+    for d in (single, multi):
+        write_reference_tree(d, Q=6, S=48, k=8)
+    args = ("dr12q", "dr9q_minus_concordance", "dr9q_concordance",
+            " prior_catalog.in_dr9 & prior_catalog.los_inds(dla_catalog_name)", "dr12q", "dr12q",
+            "(catalog.filter_flags == 0)")
+    PR.run_process_qsos(str(single), *args)
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_rank_worker, args=(r, 2, port, str(multi), q)) for r in range(2)]
+    for pr in procs:
+        pr.start()
+    assert sorted(q.get(timeout=240) for _ in range(2)) == [0, 1]
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    a = M.loadmat73(str(single / "dr12q" / "processed" / "processed_qsos_dr12q.mat"))
+    b = M.loadmat73(str(multi / "dr12q" / "processed" / "processed_qsos_dr12q.mat"))
+    for k in a:
+        if isinstance(a[k], str):
+            assert a[k] == b[k]
+        else:
+            np.testing.assert_array_equal(a[k], b[k], err_msg=k)

@@ -1,0 +1,89 @@
+"""Multi-process process_qsos on files (gloo, world size 2, CPU): each rank decodes and evaluates
+only its shard of preloaded_qsos.mat, rank 0 writes processed_qsos_<set>.mat with the sample
+array deferred, and both ranks write their rows into it in place.  The per-spectrum evaluation is
+the CPU oracle here (the checker standing in for the engine, which needs the GPU); the file must
+equal the single-process run's."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from gp_dla_detection_amd import matv73 as M
+from gp_dla_detection_amd import process as PR
+
+
+def oracle_compute(model, samples, packed, params, device):
+    from oracle import gpdla_oracle as O
+    off = packed["offsets"]
+    Q, S = off.size - 1, np.asarray(samples["nhi_samples"]).size
+    out = dict(log_likelihoods_no_dla=np.full(Q, np.nan), log_likelihoods_dla=np.full(Q, np.nan),
+               min_z_dlas=np.full(Q, np.nan), max_z_dlas=np.full(Q, np.nan), num_pixels=np.zeros(Q, np.int32),
+               sample_log_likelihoods_dla=np.full((Q, S), np.nan))
+    for q in range(Q):
+        a, b = off[q], off[q + 1]
+        r = O.process_spectrum(packed["wavelengths"][a:b], packed["flux"][a:b], packed["noise_variance"][a:b],
+                               packed["pixel_mask"][a:b].astype(bool), packed["z_qsos"][q], model,
+                               samples["offset_samples"], samples["nhi_samples"])
+        out["log_likelihoods_no_dla"][q] = r["log_likelihood_no_dla"]
+        out["log_likelihoods_dla"][q] = r["log_likelihood_dla"]
+        out["min_z_dlas"][q], out["max_z_dlas"][q] = r["min_z_dla"], r["max_z_dla"]
+        out["num_pixels"][q] = r["n"]
+        out["sample_log_likelihoods_dla"][q] = r["sample_log_likelihoods_dla"]
+    return out
+
+
+ARGS = ("dr12q", "dr9q_minus_concordance", "dr9q_concordance",
+        " prior_catalog.in_dr9 & prior_catalog.los_inds(dla_catalog_name)", "dr12q", "dr12q",
+        "(catalog.filter_flags == 0)")
+
+
+def _worker(rank, world, port, base, q):
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        out = PR.run_process_qsos(base, *ARGS, rank=rank, world=world, compute=oracle_compute)
+        q.put((rank, sorted(out)))
+    finally:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.timeout(600)
+def test_world2_file_equals_single_process(tmp_path):
+    from test_matv73 import write_reference_tree
+    single, multi = tmp_path / "single", tmp_path / "multi"
+    for d in (single, multi):
+        write_reference_tree(d, Q=5, S=24, k=8)
+    PR.run_process_qsos(str(single), *ARGS, compute=oracle_compute)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, str(multi), q)) for r in range(2)]
+    for pr in procs:
+        pr.start()
+    got = dict(q.get(timeout=500) for _ in range(2))
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    assert "p_dlas" in got[0] and "sample_log_likelihoods_dla" in got[1]
+    a = M.loadmat73(str(single / "dr12q" / "processed" / "processed_qsos_dr12q.mat"))
+    b = M.loadmat73(str(multi / "dr12q" / "processed" / "processed_qsos_dr12q.mat"))
+    assert sorted(a) == sorted(b)
+    for k in a:
+        if isinstance(a[k], str):
+            assert a[k] == b[k]
+        else:
+            np.testing.assert_array_equal(a[k], b[k], err_msg=k)
+    assert np.isfinite(b["sample_log_likelihoods_dla"]).all()
