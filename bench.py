@@ -115,11 +115,11 @@ WORKLOADS = {
 PROFILE_SUMMARY = ROOT / "profiles" / "r1g_summary.json"
 
 
-def profiled_traffic(Q: int, S: int, k: int):
+def profiled_traffic(Q: int, S: int, k: int, path: str = "fused"):
     """HBM bytes per likelihood launch from the committed PMC profile of the default workload
     (2 x FETCH_SIZE + WRITE_SIZE, gfx950 correction per MI355X_MICROARCH.md; includes
     Infinity-Cache hits).  None for other workloads or if no summary is present."""
-    if (Q, S, k) != (1024, 10000, 20) or not PROFILE_SUMMARY.exists():
+    if (Q, S, k) != (1024, 10000, 20) or path != "fused" or not PROFILE_SUMMARY.exists():
         return None, None
     d = json.loads(PROFILE_SUMMARY.read_text())
     for ent in d["kernels"]:
@@ -155,6 +155,9 @@ def main():
     ap.add_argument("--spectra", type=int, default=None, help="override: spectra per GPU (c2/c5)")
     ap.add_argument("--samples", type=int, default=None, help="override: DLA samples")
     ap.add_argument("--k", type=int, default=None, help="override: rank")
+    ap.add_argument("--path", choices=["auto", "fused", "fused_i8", "panel_gemm"], default="auto",
+                    help="likelihood path (Engine path=): auto = fused fp64 kernel for the compiled ranks, "
+                         "fused_i8 = the int8 Ozaki contraction (k=20), panel_gemm = weights + dgemm + LDL^T")
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU-baseline work (0 = skip)")
     args = ap.parse_args()
 
@@ -207,8 +210,13 @@ def main():
     o_s = L.DeviceArray(dev, (Q, S), np.float64)
     o_n = L.DeviceArray(dev, Q, np.int32)
 
-    eng = Engine(model, samples, set_parameters(k=args.k), device=dev)
-    path = "fused" if args.k in (4, 8, 10, 12, 16, 20, 24) else "panel-GEMM"
+    eng = Engine(model, samples, set_parameters(k=args.k), device=dev, path=args.path)
+    if args.path == "fused_i8":
+        path = "fused-int8"
+    elif args.path == "panel_gemm" or args.k not in (4, 8, 10, 12, 16, 20, 24):
+        path = "panel-GEMM"
+    else:
+        path = "fused"
 
     def step():
         eng.process_device(packed["offsets"], t["wavelengths"].ptr, t["flux"].ptr, t["noise_variance"].ptr,
@@ -252,7 +260,7 @@ def main():
     achieved_tf = flops_launch / (avg_ms * 1e-3) / 1e12
     eff_gbs = effective_bytes_per_eval(n_mean, args.k) * evals_per_launch / (avg_ms * 1e-3) / 1e9
 
-    traffic, traffic_src = profiled_traffic(Q, S, args.k)
+    traffic, traffic_src = profiled_traffic(Q, S, args.k, path)
     result = {
         "metric": "(spectrum x DLA-sample) log-evidence evals/sec",
         "value": value,
@@ -273,8 +281,9 @@ def main():
         "roofline": {"bound": "mfma", "achieved": achieved_tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved_tf / FP64_PEAK_TFLOPS, "traffic": traffic,
                      "traffic_source": traffic_src,
-                     "kernel": (f"likelihood_kernel<{args.k}>" if path == "fused"
-                                else "weights_kernel + rocBLAS dgemm + ldl_reg_kernel (per batch)"),
+                     "kernel": {"fused": f"likelihood_kernel<{args.k}>",
+                                "fused-int8": f"likelihood_i8_kernel<{args.k}>"}.get(
+                                    path, "weights_kernel + rocBLAS dgemm + ldl_reg_kernel (per batch)"),
                      "avg_launch_ms": avg_ms,
                      "flops_per_eval": algorithmic_flops_per_eval(n_mean, args.k),
                      "evals_per_launch": evals_per_launch},

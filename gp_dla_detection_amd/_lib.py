@@ -25,6 +25,7 @@ ABSORPTION_UNMASKED = 1
 PATH_AUTO = 0
 PATH_FUSED = 1
 PATH_PANEL_GEMM = 2
+PATH_FUSED_I8 = 3
 
 dp = C.POINTER(C.c_double)
 i64p = C.POINTER(C.c_int64)

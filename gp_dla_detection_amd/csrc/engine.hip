@@ -103,6 +103,7 @@ struct gpdla_engine {
   int K = 0;
   int64_t S = 0;
   bool gemm = false;                 // panel-GEMM path (gemm_path.hip + rocBLAS) instead of fused
+  bool i8 = false;                   // fused path with the int8 Ozaki contraction (kernels_i8.hip)
   rocblas_handle blas = nullptr;
   gpdla_params params{};
   hipStream_t own_stream = nullptr;
@@ -137,6 +138,10 @@ struct gpdla_engine {
          *d_U = nullptr, *d_q1p = nullptr, *d_ldp = nullptr;
   size_t cap_pm = 0, cap_srow = 0, cap_wg = 0, cap_wu = 0, cap_G = 0, cap_U = 0, cap_q1p = 0,
          cap_ldp = 0;
+  // int8 fused path workspaces
+  uint8_t* d_pi8 = nullptr;
+  double *d_psc = nullptr, *d_pent = nullptr;
+  size_t cap_pi8 = 0, cap_psc = 0, cap_pent = 0;
 
   // pinned host metadata (reused after meta_ready completes)
   int64_t* h_meta = nullptr;
@@ -183,7 +188,8 @@ int validate_params(const gpdla_params* p) {
   if (!(p->max_lambda > p->min_lambda) || !(p->pixel_spacing > 0) || !(p->lya_wavelength > 0))
     return set_error(GPDLA_EINVAL, "invalid wavelength parameters");
   if (p->max_batch_spectra < 0) return set_error(GPDLA_EINVAL, "max_batch_spectra < 0");
-  if (p->path != GPDLA_PATH_AUTO && p->path != GPDLA_PATH_FUSED && p->path != GPDLA_PATH_PANEL_GEMM)
+  if (p->path != GPDLA_PATH_AUTO && p->path != GPDLA_PATH_FUSED && p->path != GPDLA_PATH_PANEL_GEMM &&
+      p->path != GPDLA_PATH_FUSED_I8)
     return set_error(GPDLA_EINVAL, "path=%d", p->path);
   return GPDLA_OK;
 }
@@ -224,7 +230,8 @@ void gpdla_engine_destroy(gpdla_engine* e) {
                   e->d_status, e->d_meta, e->d_wl, e->d_flux, e->d_noise, e->d_mask, e->d_z,
                   e->d_info, e->d_panel, e->d_lam, e->d_smap, e->d_scratch, e->d_sll,
                   e->d_llnull, e->d_lldla, e->d_zmin, e->d_zmax, e->d_npix, e->d_pm, e->d_srow,
-                  e->d_wg, e->d_wu, e->d_G, e->d_U, e->d_q1p, e->d_ldp};
+                  e->d_wg, e->d_wu, e->d_G, e->d_U, e->d_q1p, e->d_ldp, e->d_pi8, e->d_psc,
+                  e->d_pent};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (e->h_meta) (void)hipHostFree(e->h_meta);
@@ -243,6 +250,10 @@ int gpdla_engine_create(int32_t device, const gpdla_model* model, const gpdla_sa
   if ((rc = validate_params(params))) return rc;
   const bool fused_ok = rank_supported(model->k);
   const bool use_gemm = params->path == GPDLA_PATH_PANEL_GEMM || (params->path == GPDLA_PATH_AUTO && !fused_ok);
+  const bool use_i8 = params->path == GPDLA_PATH_FUSED_I8;
+  if (use_i8 && (!i8_supported(model->k) || params->num_lines != 3))
+    return set_error(GPDLA_EUNSUPPORTED, "int8 fused path needs k=20 and num_lines=3 (k=%d, num_lines=%d)",
+                     model->k, params->num_lines);
   if (!use_gemm && !fused_ok)
     return set_error(GPDLA_EUNSUPPORTED, "rank k=%d not compiled for the fused path (4 8 10 12 16 20 24)", model->k);
   if (use_gemm && (model->k < 1 || model->k > kGemmMaxK))
@@ -261,6 +272,7 @@ int gpdla_engine_create(int32_t device, const gpdla_model* model, const gpdla_sa
   e->K = model->k;
   e->S = samples->num_samples;
   e->gemm = use_gemm;
+  e->i8 = use_i8;
   e->params = *params;
   e->num_rest = model->num_rest;
   e->c0 = std::exp(model->log_c_0);     // process_qsos.m:84-86
@@ -398,8 +410,8 @@ int gpdla_engine_process(gpdla_engine* e, const gpdla_spectra* sp, const gpdla_r
   const int64_t sc_max = std::min<int64_t>(e->S + 1, 16384);  // panel-GEMM sample chunk
   const int64_t blocks_x = (e->S + 1 + kSamplesPerBlock - 1) / kSamplesPerBlock;
 
-  // pinned metadata for every batch of this call: per batch (QB+1) + 3*QB int64
-  const size_t per_batch = (size_t)(QB + 1) + 3 * (size_t)QB;
+  // pinned metadata for every batch of this call: per batch (QB+1) + 4*QB int64
+  const size_t per_batch = (size_t)(QB + 1) + 4 * (size_t)QB;
   const int64_t nbatch = (Q + QB - 1) / QB;
   HIP_TRY(hipEventSynchronize(e->meta_done));
   if (e->cap_hmeta < per_batch * nbatch) {
@@ -417,7 +429,8 @@ int gpdla_engine_process(gpdla_engine* e, const gpdla_spectra* sp, const gpdla_r
     int64_t* h_sb = hm + (QB + 1);
     int64_t* h_lb = h_sb + QB;
     int64_t* h_cap = h_lb + QB;
-    int64_t slots = 0, lams = 0, cap_max = 0;
+    int64_t* h_cb = h_cap + QB;  // int8 path: first chunk of each spectrum
+    int64_t slots = 0, lams = 0, cap_max = 0, chunks = 0, lpix_max = 0;
     for (int64_t q = 0; q < nq; ++q) {
       h_off[q] = sp->offsets[q0 + q] - sp->offsets[q0];
       const int64_t lpix = sp->offsets[q0 + q + 1] - sp->offsets[q0 + q];
@@ -425,6 +438,9 @@ int gpdla_engine_process(gpdla_engine* e, const gpdla_spectra* sp, const gpdla_r
       h_sb[q] = slots;
       h_lb[q] = lams;
       h_cap[q] = cap;
+      h_cb[q] = chunks;
+      chunks += ((lpix + 3) / 4 + 15) / 16;  // >= ceil(L / 16) chunks of 16 steps per segment
+      lpix_max = std::max(lpix_max, lpix);
       cap_max = std::max(cap_max, cap);
       slots += cap;
       lams += cap + 8;
@@ -450,6 +466,13 @@ int gpdla_engine_process(gpdla_engine* e, const gpdla_spectra* sp, const gpdla_r
       if ((rc = grow(&e->d_ldp, &e->cap_ldp, (size_t)(kWeightParts * sc_max)))) return rc;
     } else {
       if ((rc = grow(&e->d_scratch, &e->cap_scr, (size_t)blocks_x * nq * kSamplesPerBlock * es))) return rc;
+    }
+    // int8 contraction for this batch (exactness bound on the slot count, else the fp64 kernel)
+    const bool batch_i8 = e->i8 && lpix_max <= kI8MaxSlots;
+    if (batch_i8) {
+      if ((rc = grow(&e->d_pi8, &e->cap_pi8, (size_t)chunks * i8_chunk_bytes(e->K)))) return rc;
+      if ((rc = grow(&e->d_psc, &e->cap_psc, (size_t)chunks * 64 * 8))) return rc;
+      if ((rc = grow(&e->d_pent, &e->cap_pent, (size_t)nq * 2 * i8_entries(e->K)))) return rc;
     }
     if ((rc = grow(&e->d_smap, &e->cap_smap, (size_t)slots))) return rc;
     HIP_TRY(hipMemcpyAsync(e->d_meta, hm, per_batch * sizeof(int64_t), hipMemcpyHostToDevice, st));
@@ -534,6 +557,18 @@ int gpdla_engine_process(gpdla_engine* e, const gpdla_spectra* sp, const gpdla_r
     la.scratch = e->d_scratch;
     la.sample_ll = o_sll; la.ld = ld; la.ll_null = o_null; la.status = e->d_status;
 
+    ConvertI8Args ca{};
+    LikelihoodI8Args li{};
+    if (batch_i8) {
+      ca.q_count = (int32_t)nq; ca.info = e->d_info; ca.panel = e->d_panel; ca.lam_pad = e->d_lam;
+      ca.chunk_base = pa.slot_cap + QB; ca.panel_i8 = e->d_pi8; ca.scal = e->d_psc; ca.ent = e->d_pent;
+      li.q_count = (int32_t)nq; li.info = e->d_info; li.panel_i8 = e->d_pi8; li.scal = e->d_psc;
+      li.ent = e->d_pent; li.chunk_base = ca.chunk_base; li.lam_pad = e->d_lam;
+      li.offsets = e->d_off; li.nhi = e->d_nhi; li.perm = e->d_perm; li.S = e->S;
+      li.lines = la.lines; li.scratch = e->d_scratch;
+      li.sample_ll = o_sll; li.ld = ld; li.ll_null = o_null; li.status = e->d_status;
+    }
+
     ReduceArgs ra{};
     ra.q_count = (int32_t)nq; ra.info = e->d_info; ra.sample_ll = o_sll; ra.ld = ld; ra.S = e->S;
     ra.ll_dla = o_dla; ra.zmin = o_zmin; ra.zmax = o_zmax; ra.num_pixels = o_npix;
@@ -541,10 +576,13 @@ int gpdla_engine_process(gpdla_engine* e, const gpdla_spectra* sp, const gpdla_r
     TimedLaunch t0{}, t1{}, t2{};
     if ((rc = record_start(e, &t0, 0))) return rc;
     HIP_TRY(launch_prep(e->gemm ? 0 : e->K, pa, st));
+    if (batch_i8) HIP_TRY(launch_convert_i8(e->K, ca, st));
     HIP_TRY(hipEventRecord(t0.stop, st));
     e->pending.push_back(t0);
     if ((rc = record_start(e, &t1, 1))) return rc;
-    if (!e->gemm) {
+    if (batch_i8) {
+      HIP_TRY(launch_likelihood_i8(e->K, li, st));
+    } else if (!e->gemm) {
       HIP_TRY(launch_likelihood(e->K, la, st));
     } else if ((rc = run_panel_gemm(e, nq, h_sb, h_lb, h_cap, sc_max, o_sll, ld, o_null, st))) {
       return rc;

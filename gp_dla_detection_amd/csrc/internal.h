@@ -189,6 +189,70 @@ struct LikelihoodArgs {
   int32_t* status;
 };
 
+// ---- int8 Ozaki-sliced fused path (kernels_i8.hip; ranks with i8_supported(K))
+//
+// The Gram/u contraction sum_slot w(sample, slot) P(slot, entry) runs on v_mfma_i32_16x16x64_i8
+// exactly in integers: per slot the weights are w~ = a^2/d (omega^2+sigma^2) in [0, 1] (Gram) and
+// a r/d / beta in [-1, 1] (u, beta a static per-slot bound), quantised as X_A = rint(w~ 2^30); the
+// panel entries P~ = M_r M_c / (omega^2+sigma^2) and M_i beta as X_B = rint(P~ / s_e 2^30) with a
+// per-entry power-of-two scale s_e.  X_A + 2^31 is split into 4 bytes (XOR 0x80 -> signed digits,
+// offset 0x808080 per slot), X_B into 4 balanced signed base-256 digits; the 13 digit pairs of
+// level i + j <= 4 accumulate exactly in int32 per level, and the epilogue forms
+//   sum_slot X_A X_B = sum_l 2^(8(6-l)) C_l + 0x808080 * colsum_e
+// in fp64.  See DESIGN.md section 4 for the error budget.
+template <int K>
+struct I8Layout {
+  static constexpr int kNGram = K * (K + 1) / 2;
+  static constexpr int kGT = (kNGram + 15) / 16;     // Gram tiles (16 entries each)
+  static constexpr int kUT = (K + 15) / 16;          // u tiles
+  static constexpr int kTiles = kGT + kUT;
+  static constexpr int kEnt = 16 * kTiles;           // entries incl. padding (<= 256)
+  static constexpr int kUBase = 16 * kGT;            // entry of u_0
+  static constexpr int kChunkSlots = 64;             // 4 segments x 16 steps (MFMA K = 64)
+  static constexpr int kPlaneBytes = kEnt * 64;      // one digit plane of a chunk
+  static constexpr int kChunkBytes = 4 * kPlaneBytes;
+  static constexpr int kScal = 8;                    // doubles per slot record
+  static constexpr int kScalBytes = kChunkSlots * kScal * 8;
+};
+constexpr int kI8MaxSlots = 30000;  // int32 level sums stay exact up to 4 * 32767 * 2^14 < 2^31
+
+struct ConvertI8Args {
+  int32_t q_count;
+  const SpecInfo* info;
+  const double* panel;           // fused f64 layout (prep_kernel<K>)
+  const double* lam_pad;
+  const int64_t* chunk_base;     // device, [q_count]: first i8 chunk of each spectrum
+  uint8_t* panel_i8;             // [chunks][4 planes][kEnt][64 B] (16 B granules swizzled)
+  double* scal;                  // [chunks][64][8]: lam(+6), y, noise, mu, om2, gscale, uscale, 0
+  double* ent;                   // [q_count][2][kEnt]: s_e, colsum_e
+};
+
+struct LikelihoodI8Args {
+  int32_t q_count;
+  const SpecInfo* info;
+  const uint8_t* panel_i8;
+  const double* scal;
+  const double* ent;
+  const int64_t* chunk_base;
+  const double* lam_pad;
+  const double* offsets;
+  const double* nhi;
+  const int32_t* perm;
+  int64_t S;
+  LineArgs lines;
+  double* scratch;               // [grid blocks][64][Layout<K>::kES]
+  double* sample_ll;
+  int64_t ld;
+  double* ll_null;
+  int32_t* status;
+};
+
+bool i8_supported(int K);
+int i8_chunk_bytes(int K);
+int i8_entries(int K);
+hipError_t launch_convert_i8(int K, const ConvertI8Args& a, hipStream_t s);
+hipError_t launch_likelihood_i8(int K, const LikelihoodI8Args& a, hipStream_t s);
+
 struct ReduceArgs {
   int32_t q_count;
   const SpecInfo* info;

@@ -216,81 +216,6 @@ __global__ __launch_bounds__(256) void prep_kernel(PrepArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// Per-sample augmented LDL^T in registers, one quad of lanes per sample.
-//   srow (Layout<K>::kES doubles): Gram entries (r, c), r <= c, at gram_index(r, c); u_i at
-//   4*kGT + i; sum r^2/d, prod-d mantissa and exponent at 4*kTiles + {0,1,2}.
-//   Lane jq owns Gram columns c = 4jj + jq (rows 0..4jj+3) and u rows i = 4m + jq; pivot rows are
-//   broadcast inside the quad with DPP.  [B u; u' q1] with B = I + M'D^-1 M
-//   (log_mvnpdf_low_rank.m:22-24) is factored as L D L': log det B = sum log D_p and
-//   r'K^-1 r = q1 - u'B^-1 u is the last pivot (log_mvnpdf_low_rank.m:26-32).
-// ---------------------------------------------------------------------------------------------
-template <int K>
-__device__ inline double ldl_log_likelihood(const double* srow, int jq, int n, bool& bad_out) {
-  using Lay = Layout<K>;
-  constexpr int kTiles = Lay::kTiles;
-  constexpr int kGT = Lay::kGT;
-  constexpr int NJJ = (K + 3) / 4;
-  double A[NJJ][4 * NJJ];
-  double U[NJJ];
-#pragma unroll
-  for (int jj = 0; jj < NJJ; ++jj) {
-    const int c = 4 * jj + jq;
-#pragma unroll
-    for (int i = 0; i < 4 * jj + 4; ++i) {
-      double v = 0.0;
-      if (i <= c && c < K) {
-        v = srow[gram_index<K>(i, c)];
-        if (i == c) v += 1.0;  // B = I + M' D^-1 M (log_mvnpdf_low_rank.m:23)
-      }
-      A[jj][i] = v;
-    }
-    U[jj] = (c < K) ? srow[4 * kGT + c] : 0.0;
-  }
-  double quad = srow[4 * kTiles];
-  const double dm = srow[4 * kTiles + 1];
-  const double de = srow[4 * kTiles + 2];
-  double pb = 1.0;
-  int eb = 0;
-  bool bad = false;
-#pragma unroll
-  for (int p = 0; p < K; ++p) {
-    const double Dp = quad_bcast(A[p >> 2][p], p & 3);
-    bad |= !(Dp > 0.0) || !(Dp < INFINITY);
-    const double invD = 1.0 / Dp;
-    pb *= Dp;
-    if ((p & 3) == 3) {
-      int ex;
-      pb = frexp(pb, &ex);
-      eb += ex;
-    }
-    const double up = quad_bcast(U[p >> 2], p & 3);
-    const double upinv = up * invD;
-    double rowp[K];
-#pragma unroll
-    for (int i = p + 1; i < K; ++i) rowp[i] = quad_bcast(A[i >> 2][p], i & 3);
-#pragma unroll
-    for (int jj = p >> 2; jj < NJJ; ++jj) {
-      const double sc = A[jj][p] * invD;
-#pragma unroll
-      for (int i = p + 1; i < 4 * jj + 4 && i < K; ++i) A[jj][i] = fma(-rowp[i], sc, A[jj][i]);
-    }
-#pragma unroll
-    for (int mm = 0; mm < NJJ; ++mm) {
-      if (4 * mm + 3 > p) {
-        const bool cnd = (4 * mm + jq) > p;
-        U[mm] = cnd ? fma(-A[mm][p], upinv, U[mm]) : U[mm];
-      }
-    }
-    quad = fma(-up, upinv, quad);
-  }
-  const double logdet_b = log(pb) + eb * kLn2;
-  const double logdet_d = log(dm) + de * kLn2;
-  const double ll = -0.5 * (quad + (logdet_d + logdet_b) + n * kLog2Pi);  // log_mvnpdf_low_rank.m:30-32
-  bad_out = bad || !(fabs(ll) < INFINITY);
-  return bad_out ? NAN : ll;
-}
-
-// ---------------------------------------------------------------------------------------------
 // likelihood: for one spectrum and 64 samples (4 waves x 16), sweep all slots:
 //   per lane (sample s = lane & 15, segment g = lane >> 4): Voigt raw profile at the leading
 //   padded wavelength, 7-tap convolution from a register window, DLA-modulated pixel terms

@@ -24,7 +24,8 @@ def _model_struct(model: dict, keep: list) -> L.Model:
                    log_beta=float(np.ravel(model["log_beta"])[0]))
 
 
-_PATHS = {"auto": L.PATH_AUTO, "fused": L.PATH_FUSED, "panel_gemm": L.PATH_PANEL_GEMM}
+_PATHS = {"auto": L.PATH_AUTO, "fused": L.PATH_FUSED, "panel_gemm": L.PATH_PANEL_GEMM,
+          "fused_i8": L.PATH_FUSED_I8}
 
 
 def _params_struct(p: Parameters, max_batch_spectra: int = 0, path: str = "auto") -> L.Params:

@@ -53,6 +53,10 @@ extern "C" {
 #define GPDLA_PATH_AUTO 0
 #define GPDLA_PATH_FUSED 1
 #define GPDLA_PATH_PANEL_GEMM 2
+/* Fused sweep with the Gram/u contraction on the int8 matrix cores (Ozaki digit slicing, exact
+ * integer accumulation, fp64 everywhere else); k = 20 with num_lines = 3.  Spectra with more than
+ * 30,000 pixels fall back to the fp64 fused kernel.  Agrees with the fp64 path to ~1e-10 relative. */
+#define GPDLA_PATH_FUSED_I8 3
 
 /* Learned null model (learned_qso_model_<set>.mat, read at process_qsos.m:30-35).  Host memory. */
 typedef struct gpdla_model {

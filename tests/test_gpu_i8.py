@@ -1,0 +1,115 @@
+"""GPU parity of the int8 Ozaki-contraction fused path (GPDLA_PATH_FUSED_I8, kernels_i8.hip)
+against the oracle's golden fixtures and against the fp64 fused kernel.
+
+Tolerance: the north-star bound |got - ref| <= 1e-6 * max(|ref|, 1), plus a tighter 1e-8 bar for
+this path (its only approximations are the 2^-31/2^-32 weight and panel quantisation and the dropped
+digit levels >= 4; the numpy emulation tools/emulate_i8.py measures ~7e-10 on the bench data)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+from conftest import tol_ok  # noqa: E402
+from gp_dla_detection_amd import _lib as L  # noqa: E402
+from gp_dla_detection_amd import synthetic as syn  # noqa: E402
+from gp_dla_detection_amd.engine import Engine  # noqa: E402
+from gp_dla_detection_amd.parameters import set_parameters  # noqa: E402
+
+I8_TOL = 1e-8
+KEYS = ("log_likelihoods_no_dla", "sample_log_likelihoods_dla", "log_likelihoods_dla")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def require_device():
+    assert L.load().gpdla_device_count() > 0, "no HIP device: GPU tests must run on the MI355X box"
+
+
+def _rel_err(got, ref):
+    got, ref = np.asarray(got, float), np.asarray(ref, float)
+    both_nan = np.isnan(got) & np.isnan(ref)
+    err = np.abs(got - ref) / np.maximum(np.abs(ref), 1.0)
+    return float(np.max(np.where(both_nan, 0.0, err)))
+
+
+def _run(model, samples, packed, path, **kw):
+    with Engine(model, samples, set_parameters(k=model["M"].shape[1], **kw), path=path) as eng:
+        return eng.process(packed)
+
+
+@pytest.mark.parametrize("mode", ["reference", "unmasked"])
+def test_i8_matches_golden(golden_dir, mode):
+    g = np.load(golden_dir / "process.npz")
+    model = {k: g[k] for k in ("rest_wavelengths", "mu", "M", "log_omega", "log_c_0", "log_tau_0", "log_beta")}
+    samples = dict(offset_samples=g["offset_samples"], nhi_samples=g["nhi_samples"])
+    packed = {k: g[k] for k in ("offsets", "wavelengths", "flux", "noise_variance", "pixel_mask", "z_qsos")}
+    out = _run(model, samples, packed, "fused_i8", absorption_mode=mode)
+    for key, gkey in (("log_likelihoods_no_dla", "log_likelihood_no_dla"),
+                      ("sample_log_likelihoods_dla", "sample_log_likelihoods_dla"),
+                      ("log_likelihoods_dla", "log_likelihood_dla")):
+        ref = g[f"{mode}_{gkey}"]
+        assert np.all(tol_ok(out[key], ref)), (key, _rel_err(out[key], ref))
+        assert _rel_err(out[key], ref) < I8_TOL, (key, _rel_err(out[key], ref))
+    np.testing.assert_array_equal(out["num_pixels"], g[f"{mode}_n"])
+
+
+def test_i8_equals_fp64_at_bench_shape():
+    """configs[1] shape (n = 800, k = 20, S = 10^4) on a few spectra: the int8 path against the
+    fp64 fused kernel, the calc_cddf.py:246 invariant, and run-to-run determinism."""
+    model = syn.make_model(k=20)
+    samples = syn.make_samples(10000)
+    packed = syn.pack_spectra(syn.make_spectra(model, 6))
+    ref = _run(model, samples, packed, "fused")
+    with Engine(model, samples, set_parameters(k=20), path="fused_i8") as eng:
+        out = eng.process(packed)
+        out2 = eng.process(packed)
+    for key in KEYS:
+        np.testing.assert_array_equal(out[key], out2[key])
+        assert _rel_err(out[key], ref[key]) < I8_TOL, (key, _rel_err(out[key], ref[key]))
+    sll, lld = out["sample_log_likelihoods_dla"], out["log_likelihoods_dla"]
+    tot = np.exp(sll - (lld[:, None] + np.log(sll.shape[1]))).sum(axis=1)
+    np.testing.assert_allclose(tot, 1.0, atol=1e-12)
+    print("i8 vs fp64 max rel err:", {k: _rel_err(out[k], ref[k]) for k in KEYS})
+
+
+def test_i8_dr12q_shapes_and_masks():
+    """Ragged n (269..1250) with 5% masked pixels, both absorption modes, S not a multiple of 64."""
+    model = syn.make_model(k=20)
+    samples = syn.make_samples(333)
+    packed = syn.pack_spectra(syn.make_dr12q_like_spectra(model, 24, seed=5, mask_fraction=0.05))
+    for mode in ("reference", "unmasked"):
+        ref = _run(model, samples, packed, "fused", absorption_mode=mode)
+        out = _run(model, samples, packed, "fused_i8", absorption_mode=mode)
+        for key in KEYS:
+            assert _rel_err(out[key], ref[key]) < I8_TOL, (mode, key, _rel_err(out[key], ref[key]))
+
+
+def test_i8_edge_cases():
+    """Tiny spectra (n = 1..33: a single chunk, mostly padding), an unusable spectrum (NaN outputs)."""
+    model = syn.make_model(k=20, seed=3)
+    samples = syn.make_samples(67)
+    base = syn.make_spectrum(model, 0, z_qso=2.8, n_target=None, mask_fraction=0.1)
+    spectra = []
+    for npx in (1, 2, 3, 5, 9, 33, 64, 65):
+        sl = slice(100, 100 + npx)
+        s = {k: (v[sl] if isinstance(v, np.ndarray) else v) for k, v in base.items()}
+        s["pixel_mask"] = np.zeros(npx, dtype=bool)
+        spectra.append(s)
+    empty = dict(base)
+    empty["z_qso"] = 9.5
+    spectra.append(empty)
+    packed = syn.pack_spectra(spectra)
+    ref = _run(model, samples, packed, "fused")
+    out = _run(model, samples, packed, "fused_i8")
+    for key in KEYS:
+        assert _rel_err(out[key][:-1], ref[key][:-1]) < I8_TOL, (key, _rel_err(out[key][:-1], ref[key][:-1]))
+        assert np.all(np.isnan(out[key][-1]))
+
+
+def test_i8_unsupported_configurations_rejected():
+    model = syn.make_model(k=16)
+    samples = syn.make_samples(8)
+    with pytest.raises(L.GpdlaError):
+        Engine(model, samples, set_parameters(k=16), path="fused_i8")
+    model = syn.make_model(k=20)
+    with pytest.raises(L.GpdlaError):
+        Engine(model, samples, set_parameters(k=20, num_lines=4), path="fused_i8")
