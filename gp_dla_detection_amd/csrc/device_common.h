@@ -20,6 +20,12 @@
 #ifndef GPDLA_FAST_EXP
 #define GPDLA_FAST_EXP 1
 #endif
+#ifndef GPDLA_RCP_STEPS
+#define GPDLA_RCP_STEPS 1
+#endif
+#ifndef GPDLA_BATCHED_PROFILE
+#define GPDLA_BATCHED_PROFILE 1
+#endif
 #ifndef GPDLA_LDL_REGISTERS
 #define GPDLA_LDL_REGISTERS 1
 #endif
@@ -41,6 +47,17 @@ __device__ inline double rcp_nr(double d) {
   r = fma(r, e, r);
   e = fma(-d, r, 1.0);
   return fma(r, e, r);
+}
+
+// 1/d in the per-pixel sweeps (d = omega^2 a^2 + sigma^2 > 0, finite): v_rcp_f64 (~2^-26) and one
+// Newton step (error ~2^-52, i.e. within a couple of ulp; the sums over n pixels are insensitive)
+__device__ inline double rcp_sweep(double d) {
+#if GPDLA_RCP_STEPS == 1
+  const double r = __builtin_amdgcn_rcp(d);
+  return fma(r, fma(-d, r, 1.0), r);
+#else
+  return rcp_nr(d);
+#endif
 }
 
 // exp(v) for v <= 0 (v = N * total, voigt.c:291): v = (64 m + j) ln2/64 + r, |r| <= ln2/128,

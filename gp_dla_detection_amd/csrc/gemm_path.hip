@@ -86,7 +86,7 @@ __global__ __launch_bounds__(256) void weights_kernel(WeightsArgs a) {
     const double r = fma(-mu, ab, y);  // process_qsos.m:191-197, log_mvnpdf_low_rank.m:11-15
     const double a2 = ab * ab;
     const double d = fma(om2, a2, noise);
-    const double dinv = rcp_nr(d);
+    const double dinv = rcp_sweep(d);
     const double rd = r * dinv;
     q1 = fma(r, rd, q1);
     pm *= d;

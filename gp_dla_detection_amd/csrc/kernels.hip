@@ -343,6 +343,60 @@ __global__ __launch_bounds__(256, (K <= 20 ? GPDLA_WAVES_PER_EU : 1)) void likel
     double* cur = lds + (c & 1) * kBuf;
     if (c + 1 < nchunks)
       stage_chunk<K>(panel, Ls, c + 1, lds_base + (uint32_t)(((c + 1) & 1) * kBuf * 8), wave_s, voff);
+#if GPDLA_BATCHED_PROFILE
+    // raw profiles of the chunk's 4 steps first: branch-free damping wings (one basic block, so
+    // the 4 chains interleave), a rare core fix-up for lanes with |x| < kCoreX (raw_profile3's
+    // order: bit-identical), then the 4 table exps
+    double rwv[kChunkSteps];
+    if constexpr (NL == 3) {
+      double tot[kChunkSteps], lamc[kChunkSteps];
+      uint32_t cm = 0;
+#pragma unroll
+      for (int tt = 0; tt < kChunkSteps; ++tt) {
+        lamc[tt] = cur[(tt * 4 + g) * kRowS + Lay::kLam];
+        tot[tt] = 0.0;
+      }
+      // line-outer order (same per-step summation order): one line's 9 coefficients live at a
+      // time, re-read from LDS per line (opaque zero offset) rather than hoisted
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        int zoff;
+        asm volatile("s_mov_b32 %0, 0" : "=s"(zoff));
+        const double* wl = wing_lds + zoff + j * kWingStride;
+#pragma unroll
+        for (int tt = 0; tt < kChunkSteps; ++tt) {
+          const double x = fma(lamc[tt], afac[j], -kC2);
+          cm |= (fabs(x) < kCoreX ? 1u : 0u) << tt;
+          tot[tt] -= wing_eval(wl, x);
+        }
+      }
+      if (cm) {
+#pragma unroll
+        for (int tt = 0; tt < kChunkSteps; ++tt) {
+          if (cm & (1u << tt)) {
+            double t = 0.0;
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+              const double x = fma(lamc[tt], afac[j], -kC2);
+              const double ax = fabs(x);
+              double f = wing_eval(wing_lds + j * kWingStride, x);
+              if (ax < kCoreX) f = core_eval(core_lds + j * kCoreTable, ax);
+              t -= f;
+            }
+            tot[tt] = t;
+          }
+        }
+      }
+#pragma unroll
+      for (int tt = 0; tt < kChunkSteps; ++tt) {
+#if GPDLA_FAST_EXP
+        rwv[tt] = exp_tab64(N * tot[tt], exp_lds);
+#else
+        rwv[tt] = exp(N * tot[tt]);
+#endif
+      }
+    }
+#endif
 #pragma unroll
     for (int tt = 0; tt < kChunkSteps; ++tt) {
       const double* row = cur + (tt * 4 + g) * kRowS;
@@ -357,9 +411,19 @@ __global__ __launch_bounds__(256, (K <= 20 ? GPDLA_WAVES_PER_EU : 1)) void likel
       }
       // Per-step opaque zero: the wing coefficients are re-read from LDS (broadcast) every step
       // instead of being hoisted into registers for the whole chunk.
+#if GPDLA_BATCHED_PROFILE
+      double w6;
+      if constexpr (NL == 3) {
+        w6 = rwv[tt];
+        (void)lam;
+      } else {
+        w6 = raw(lam, wing_lds);
+      }
+#else
       int zoff;
       asm volatile("s_mov_b32 %0, 0" : "=s"(zoff));
       const double w6 = raw(lam, wing_lds + zoff);
+#endif
       // instrumental broadening, voigt.c:297-299 (zero-initialised accumulator, taps in order)
       double ab = w0 * kInstrumentProfile[0];
       ab = fma(w1, kInstrumentProfile[1], ab);
@@ -375,7 +439,7 @@ __global__ __launch_bounds__(256, (K <= 20 ? GPDLA_WAVES_PER_EU : 1)) void likel
       const double r = fma(-mu, ab, y);
       const double a2 = ab * ab;
       const double d = fma(om2, a2, noise);
-      const double dinv = rcp_nr(d);
+      const double dinv = rcp_sweep(d);
       const double rd = r * dinv;
       const double wg = a2 * dinv;
       const double wu = ab * rd;

@@ -12,9 +12,8 @@ VARIANTS = {
     "f0_w1": dict(GPDLA_SCHED_FENCE=0, GPDLA_WAVES_PER_EU=1),
     "epi_lds": dict(GPDLA_LDS_EPILOGUE=1),
     "epi_global": dict(GPDLA_LDS_EPILOGUE=0),
-    "i8_f0_r0": dict(I8_SLOT_FENCE=0, I8_WING_RELOAD=0),
-    "i8_f0_r1": dict(I8_SLOT_FENCE=0, I8_WING_RELOAD=1),
-    "i8_f1_r1": dict(I8_SLOT_FENCE=1, I8_WING_RELOAD=1),
+    "rcp1": dict(GPDLA_RCP_STEPS=1),
+    "rcp2": dict(GPDLA_RCP_STEPS=2),
 }
 if __name__ == "__main__":
     names = sys.argv[1:] or list(VARIANTS)
