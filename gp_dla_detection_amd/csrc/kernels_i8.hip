@@ -255,8 +255,9 @@ __global__ __launch_bounds__(256, 1) void likelihood_i8_kernel(LikelihoodI8Args 
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
-  // damping-wing coefficients read as uniform global data (scalar loads -> SGPR operands)
-  const double* __restrict__ wing_g = a.lines.buf + kLineBufWing;
+  // damping-wing coefficients from LDS (broadcast reads, lgkmcnt): vector loads from global
+  // memory here would wait on vmcnt behind the next chunk's LDS-DMA and serialise it with compute
+  const double* wing_g = wing_lds;
   auto raw = [&](double lam) { return raw_profile3(lam, afac, N, core_lds, wing_lds, exp_lds); };
   double w0 = raw(lw[0]), w1 = raw(lw[1]), w2 = raw(lw[2]);
   double w3 = raw(lw[3]), w4 = raw(lw[4]), w5 = raw(lw[5]);
@@ -310,20 +311,32 @@ __global__ __launch_bounds__(256, 1) void likelihood_i8_kernel(LikelihoodI8Args 
         }
       }
     }
-    // (3) exp (table lookups of the 16 slots overlap), 7-tap convolution, pixel terms, weights
-    uint32_t xg[16], xu[16];
+    // (3) the 16 table exps (their LDS lookups in flight together)
+    double rw[16];
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
-      const double2 r01 = *reinterpret_cast<const double2*>(rec + e * I::kScal);
-      const double2 r23 = *reinterpret_cast<const double2*>(rec + e * I::kScal + 2);
-      const double2 r45 = *reinterpret_cast<const double2*>(rec + e * I::kScal + 4);
-      const double us = rec[e * I::kScal + 6];
-      const double y = r01.y, noise = r23.x, mu = r23.y, om2 = r45.x, gs = r45.y;
 #if GPDLA_FAST_EXP
-      const double w6 = exp_tab64(N * tot[e], exp_lds);  // voigt.c:291
+      rw[e] = exp_tab64(N * tot[e], exp_lds);  // voigt.c:291
 #else
-      const double w6 = exp(N * tot[e]);
+      rw[e] = exp(N * tot[e]);
 #endif
+    }
+    // (4) 7-tap convolution, pixel terms, weights; slot records prefetched one slot ahead
+    uint32_t xg[16], xu[16];
+    double2 n01 = *reinterpret_cast<const double2*>(rec + 0);
+    double2 n23 = *reinterpret_cast<const double2*>(rec + 2);
+    double2 n45 = *reinterpret_cast<const double2*>(rec + 4);
+    double nus = rec[6];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const double y = n01.y, noise = n23.x, mu = n23.y, om2 = n45.x, gs = n45.y, us = nus;
+      if (e + 1 < 16) {
+        n01 = *reinterpret_cast<const double2*>(rec + (e + 1) * I::kScal);
+        n23 = *reinterpret_cast<const double2*>(rec + (e + 1) * I::kScal + 2);
+        n45 = *reinterpret_cast<const double2*>(rec + (e + 1) * I::kScal + 4);
+        nus = rec[(e + 1) * I::kScal + 6];
+      }
+      const double w6 = rw[e];
       double ab = w0 * kInstrumentProfile[0];  // voigt.c:297-299
       ab = fma(w1, kInstrumentProfile[1], ab);
       ab = fma(w2, kInstrumentProfile[2], ab);
