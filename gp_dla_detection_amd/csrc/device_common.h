@@ -23,6 +23,12 @@
 #ifndef GPDLA_RCP_STEPS
 #define GPDLA_RCP_STEPS 1
 #endif
+#ifndef GPDLA_MAGIC_RINT
+#define GPDLA_MAGIC_RINT 1
+#endif
+#ifndef GPDLA_SHARED_RCP
+#define GPDLA_SHARED_RCP 1
+#endif
 #ifndef GPDLA_BATCHED_PROFILE
 #define GPDLA_BATCHED_PROFILE 1
 #endif
@@ -68,7 +74,16 @@ __device__ inline double exp_tab64(double v, const double* __restrict__ tab) {
   constexpr double kLhi = 0.010830424695086549;           // ln2/64 to 33 bits (k*kLhi exact)
   constexpr double kLlo = 1.162596423439437e-12;           // ln2/64 - kLhi
   v = fmax(v, -1100.0);                                    // keeps k in int range; exp(-1100) = 0
+#if GPDLA_MAGIC_RINT
+  // k = rint(v 64/ln2) by the 1.5 2^52 shifter: the fma rounds at the units place, the low
+  // mantissa word is k as a two's-complement int (no f64 <-> int conversion instructions)
+  const double kd = fma(v, kInvL, 0x1.8p52);
+  const int ki = __double2loint(kd);
+  const double k = kd - 0x1.8p52;
+#else
   const double k = __builtin_rint(v * kInvL);
+  const int ki = (int)k;
+#endif
   double r = fma(-k, kLhi, v);
   r = fma(-k, kLlo, r);
   double p = fma(r, 1.0 / 120.0, 1.0 / 24.0);
@@ -76,8 +91,22 @@ __device__ inline double exp_tab64(double v, const double* __restrict__ tab) {
   p = fma(p, r, 0.5);
   p = fma(p, r, 1.0);
   p = fma(p, r, 1.0);
-  const int ki = (int)k;
   return __builtin_ldexp(p * tab[ki & 63], ki >> 6);
+}
+
+// T_j = 1/x_j^2 of the three Lyman lines with ONE v_rcp_f64 (+ Newton step) on x0^2 x1^2 x2^2
+// (< 1e26 over the spectral range) instead of three.  Lanes with a tiny x (line cores) may get
+// inf/NaN here; their line sums are recomputed by the core fix-up.
+__device__ inline void wing_T3(double x0, double x1, double x2, double& T0, double& T1, double& T2) {
+  const double a0 = x0 * x0, a1 = x1 * x1, a2 = x2 * x2;
+  const double p01 = a0 * a1;
+  const double q = p01 * a2;
+  double R = __builtin_amdgcn_rcp(q);
+  R = fma(R, fma(-q, R, 1.0), R);
+  const double r01 = R * a2;  // 1 / (a0 a1)
+  T0 = a1 * r01;
+  T1 = a0 * r01;
+  T2 = p01 * R;
 }
 
 template <int SRC>

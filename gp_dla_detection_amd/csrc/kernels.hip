@@ -356,6 +356,16 @@ __global__ __launch_bounds__(256, (K <= 20 ? GPDLA_WAVES_PER_EU : 1)) void likel
         lamc[tt] = cur[(tt * 4 + g) * kRowS + Lay::kLam];
         tot[tt] = 0.0;
       }
+#if GPDLA_SHARED_RCP
+      double Tj[3][kChunkSteps];
+#pragma unroll
+      for (int tt = 0; tt < kChunkSteps; ++tt) {
+        const double x0 = fma(lamc[tt], afac[0], -kC2), x1 = fma(lamc[tt], afac[1], -kC2),
+                     x2 = fma(lamc[tt], afac[2], -kC2);
+        cm |= ((fabs(x0) < kCoreX) | (fabs(x1) < kCoreX) | (fabs(x2) < kCoreX) ? 1u : 0u) << tt;
+        wing_T3(x0, x1, x2, Tj[0][tt], Tj[1][tt], Tj[2][tt]);
+      }
+#endif
       // line-outer order (same per-step summation order): one line's 9 coefficients live at a
       // time, re-read from LDS per line (opaque zero offset) rather than hoisted
 #pragma unroll
@@ -365,9 +375,13 @@ __global__ __launch_bounds__(256, (K <= 20 ? GPDLA_WAVES_PER_EU : 1)) void likel
         const double* wl = wing_lds + zoff + j * kWingStride;
 #pragma unroll
         for (int tt = 0; tt < kChunkSteps; ++tt) {
+#if GPDLA_SHARED_RCP
+          tot[tt] -= wing_poly(wl, Tj[j][tt]);
+#else
           const double x = fma(lamc[tt], afac[j], -kC2);
           cm |= (fabs(x) < kCoreX ? 1u : 0u) << tt;
           tot[tt] -= wing_eval(wl, x);
+#endif
         }
       }
       if (cm) {

@@ -283,12 +283,22 @@ __global__ __launch_bounds__(256, 1) void likelihood_i8_kernel(LikelihoodI8Args 
     for (int e = 0; e < 16; ++e) {
       const double lam = rec[e * I::kScal];
       double t = 0.0;
+#if GPDLA_SHARED_RCP
+      const double x0 = fma(lam, afac[0], -kC2), x1 = fma(lam, afac[1], -kC2), x2 = fma(lam, afac[2], -kC2);
+      cm |= ((fabs(x0) < kCoreX) | (fabs(x1) < kCoreX) | (fabs(x2) < kCoreX) ? 1u : 0u) << e;
+      double T0, T1, T2;
+      wing_T3(x0, x1, x2, T0, T1, T2);
+      t -= wing_poly(wing_g, T0);
+      t -= wing_poly(wing_g + kWingStride, T1);
+      t -= wing_poly(wing_g + 2 * kWingStride, T2);
+#else
 #pragma unroll
       for (int j = 0; j < 3; ++j) {
         const double x = fma(lam, afac[j], -kC2);
         cm |= (fabs(x) < kCoreX ? 1u : 0u) << e;
         t -= wing_eval(wing_g + j * kWingStride, x);
       }
+#endif
       tot[e] = t;
     }
     // (2) rare fix-up (z-sorted samples: a few % of wave-chunks): the core polynomial for the

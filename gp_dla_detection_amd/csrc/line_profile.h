@@ -55,6 +55,15 @@ GPDLA_HD double wing_eval(const double* __restrict__ c, double x) {
   return T * f;
 }
 
+// Damping wing from a precomputed T = 1/x^2 (the batched sweeps share one reciprocal between
+// the three lines, wing_T3 in device_common.h).
+GPDLA_HD double wing_poly(const double* __restrict__ c, double T) {
+  double f = c[kWingDeg];
+#pragma unroll
+  for (int n = kWingDeg - 1; n >= 0; --n) f = fma(f, T, c[n]);
+  return T * f;
+}
+
 GPDLA_HD double core_eval(const double* __restrict__ core, double ax) {
   int p = (int)(ax * (1.0 / kPieceW));
   p = p > kPieces - 1 ? kPieces - 1 : p;

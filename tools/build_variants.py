@@ -12,8 +12,9 @@ VARIANTS = {
     "f0_w1": dict(GPDLA_SCHED_FENCE=0, GPDLA_WAVES_PER_EU=1),
     "epi_lds": dict(GPDLA_LDS_EPILOGUE=1),
     "epi_global": dict(GPDLA_LDS_EPILOGUE=0),
-    "rcp1": dict(GPDLA_RCP_STEPS=1),
-    "rcp2": dict(GPDLA_RCP_STEPS=2),
+    "m1s1": dict(GPDLA_MAGIC_RINT=1, GPDLA_SHARED_RCP=1),
+    "m1s0": dict(GPDLA_MAGIC_RINT=1, GPDLA_SHARED_RCP=0),
+    "m0s0": dict(GPDLA_MAGIC_RINT=0, GPDLA_SHARED_RCP=0),
 }
 if __name__ == "__main__":
     names = sys.argv[1:] or list(VARIANTS)
