@@ -23,6 +23,13 @@
 #ifndef GPDLA_RCP_STEPS
 #define GPDLA_RCP_STEPS 1
 #endif
+// far-wing fast path: fp64 kernel off (A/B +1.4% time: spills at 256 VGPRs), int8 kernel on (-0.9%)
+#ifndef GPDLA_FAR_WING
+#define GPDLA_FAR_WING 0
+#endif
+#ifndef GPDLA_I8_FAR_WING
+#define GPDLA_I8_FAR_WING 1
+#endif
 #ifndef GPDLA_MAGIC_RINT
 #define GPDLA_MAGIC_RINT 1
 #endif

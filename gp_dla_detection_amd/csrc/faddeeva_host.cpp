@@ -175,6 +175,39 @@ void fit_wing_line(int j, double* wing) {
   for (int n = 0; n < kWingStride; ++n) wing[n] = n < N ? (double)t[n] : 0.0;
 }
 
+// Far-wing polynomial of line j on T in (0, kFarT] (|x| >= kFarX), degree kFarDeg.
+void fit_far_line(int j, double* far) {
+  long double scale, y;
+  line_scale(j, &scale, &y);
+  const long double Tmax = 1.0L / ((long double)kFarX * kFarX);
+  const int N = kFarDeg + 1;
+  std::vector<long double> fv(N);
+  for (int k = 0; k < N; ++k) {
+    const long double T = Tmax * (std::cos(kPiL * (k + 0.5L) / N) + 1.0L) / 2.0L;
+    fv[k] = scale * faddeeva_w(1.0L / std::sqrt(T), y).real() / T;
+  }
+  const std::vector<long double> t = shift_to_T(cheb_fit_monomial(fv), 2.0L / Tmax, -1.0L);
+  for (int n = 0; n < kFarStride; ++n) far[n] = n < N ? (double)t[n] : 0.0;
+}
+
+// Max relative error of the far-wing polynomial (|x| from kFarX geometrically out to 2e6).
+double far_profile_error(int j) {
+  std::vector<double> far(kFarStride);
+  fit_far_line(j, far.data());
+  long double scale, y;
+  line_scale(j, &scale, &y);
+  double maxrel = 0;
+  for (int i = 0; i <= 12000; ++i) {
+    const double x = kFarX * std::pow(1.00025, i);
+    const double T = 1.0 / (x * x);
+    const double got = far_poly(far.data(), T);
+    const long double ref = scale * faddeeva_w((long double)x, y).real();
+    const double rel = (double)std::fabs((got - ref) / ref);
+    if (rel > maxrel) maxrel = rel;
+  }
+  return maxrel;
+}
+
 // Core table of line j (kPieces x kCoreStride, polynomial in u = |x| - centre).
 void fit_core_table(int j, double* core) {
   long double scale, y;

@@ -262,11 +262,13 @@ __global__ __launch_bounds__(256, (K <= 20 ? GPDLA_WAVES_PER_EU : 1)) void likel
   constexpr int kBuf = 4 * kChunkSteps * kRowS;
   static_assert(kWavesPerBlock == 4, "stage_chunk: one wave per segment");
   constexpr int kWingLds = 4 * ((3 * kWingStride + 3) / 4);
-  constexpr int kCoreLds = NL == 3 ? 3 * kCoreTable + kWingLds + 64 : 1;
+  constexpr int kFarLds = 4 * ((3 * kFarStride + 3) / 4);
+  constexpr int kCoreLds = NL == 3 ? 3 * kCoreTable + kWingLds + 64 + kFarLds : 1;
   __shared__ __attribute__((aligned(16))) double lds[2 * kBuf + kCoreLds];
   double* core_lds = lds + 2 * kBuf;
   double* wing_lds = core_lds + 3 * kCoreTable;
   double* exp_lds = wing_lds + kWingLds;
+  double* far_lds = exp_lds + 64;
 
   // XCD-aware block order: the dispatcher deals consecutive blocks round-robin over the 8 XCDs,
   // so block b runs on XCD b % 8.  Virtual index v gives each XCD one contiguous eighth of the
@@ -302,6 +304,7 @@ __global__ __launch_bounds__(256, (K <= 20 ? GPDLA_WAVES_PER_EU : 1)) void likel
     for (int i = threadIdx.x; i < 3 * kCoreTable; i += 256) core_lds[i] = a.lines.buf[i];
     if (threadIdx.x < 64) exp_lds[threadIdx.x] = a.lines.buf[kLineBufExp2 + threadIdx.x];
     if (threadIdx.x < 3 * kWingStride) wing_lds[threadIdx.x] = a.lines.buf[kLineBufWing + threadIdx.x];
+    if (threadIdx.x < 3 * kFarStride) far_lds[threadIdx.x] = a.lines.buf[kLineBufFar + threadIdx.x];
   }
 
   // ---- per-lane sample constants (MFMA A-operand layout: sample = lane & 15, segment = lane >> 4)
@@ -365,6 +368,21 @@ __global__ __launch_bounds__(256, (K <= 20 ? GPDLA_WAVES_PER_EU : 1)) void likel
         cm |= ((fabs(x0) < kCoreX) | (fabs(x1) < kCoreX) | (fabs(x2) < kCoreX) ? 1u : 0u) << tt;
         wing_T3(x0, x1, x2, Tj[0][tt], Tj[1][tt], Tj[2][tt]);
       }
+#endif
+#if GPDLA_SHARED_RCP && GPDLA_FAR_WING
+      // a wave whose 4 steps are all >= kFarX from every line centre (most chunks) takes the
+      // degree-4 far-wing polynomials (NaN T of core lanes fails the test)
+      bool ok = true;
+#pragma unroll
+      for (int tt = 0; tt < kChunkSteps; ++tt)
+        ok = ok && (Tj[0][tt] <= kFarT) && (Tj[1][tt] <= kFarT) && (Tj[2][tt] <= kFarT);
+      if (__all(ok)) {
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+#pragma unroll
+          for (int tt = 0; tt < kChunkSteps; ++tt) tot[tt] -= far_poly(far_lds + j * kFarStride, Tj[j][tt]);
+        }
+      } else
 #endif
       // line-outer order (same per-step summation order): one line's 9 coefficients live at a
       // time, re-read from LDS per line (opaque zero offset) rather than hoisted

@@ -39,6 +39,12 @@ constexpr int kCoreStride = 16;  // kCoreDeg + 1
 constexpr int kCoreTable = kPieces * kCoreStride;  // doubles per line
 constexpr int kWingDeg = 8;      // wing polynomial degree in T
 constexpr int kWingStride = 10;  // doubles per line (kWingDeg + 1, padded to 16-byte pairs)
+// far wing |x| >= kFarX (T <= 1e-4): the same function, degree kFarDeg (the batched sweeps take it
+// when a whole wave's chunk is that far from every line centre)
+constexpr double kFarX = 100.0;
+constexpr double kFarT = 1.0 / (kFarX * kFarX);
+constexpr int kFarDeg = 4;
+constexpr int kFarStride = 6;
 
 GPDLA_HD double wing_eval(const double* __restrict__ c, double x) {
   const double x2 = x * x;
@@ -52,6 +58,13 @@ GPDLA_HD double wing_eval(const double* __restrict__ c, double x) {
   double f = c[kWingDeg];
 #pragma unroll
   for (int n = kWingDeg - 1; n >= 0; --n) f = fma(f, T, c[n]);
+  return T * f;
+}
+
+GPDLA_HD double far_poly(const double* __restrict__ c, double T) {
+  double f = c[kFarDeg];
+#pragma unroll
+  for (int n = kFarDeg - 1; n >= 0; --n) f = fma(f, T, c[n]);
   return T * f;
 }
 

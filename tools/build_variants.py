@@ -15,6 +15,8 @@ VARIANTS = {
     "m1s1": dict(GPDLA_MAGIC_RINT=1, GPDLA_SHARED_RCP=1),
     "m1s0": dict(GPDLA_MAGIC_RINT=1, GPDLA_SHARED_RCP=0),
     "m0s0": dict(GPDLA_MAGIC_RINT=0, GPDLA_SHARED_RCP=0),
+    "far1": dict(GPDLA_FAR_WING=1),
+    "far0": dict(GPDLA_FAR_WING=0),
 }
 if __name__ == "__main__":
     names = sys.argv[1:] or list(VARIANTS)
