@@ -365,7 +365,7 @@ __global__ __launch_bounds__(256, (K <= 20 ? GPDLA_WAVES_PER_EU : 1)) void likel
       for (int tt = 0; tt < kChunkSteps; ++tt) {
         const double x0 = fma(lamc[tt], afac[0], -kC2), x1 = fma(lamc[tt], afac[1], -kC2),
                      x2 = fma(lamc[tt], afac[2], -kC2);
-        cm |= ((fabs(x0) < kCoreX) | (fabs(x1) < kCoreX) | (fabs(x2) < kCoreX) ? 1u : 0u) << tt;
+        cm |= (((fabs(x0) < kCoreX) | (fabs(x1) < kCoreX) | (fabs(x2) < kCoreX)) ? 1u : 0u) << tt;
         wing_T3(x0, x1, x2, Tj[0][tt], Tj[1][tt], Tj[2][tt]);
       }
 #endif

@@ -315,7 +315,7 @@ __global__ __launch_bounds__(256, 1) void likelihood_i8_kernel(LikelihoodI8Args 
       double t = 0.0;
 #if GPDLA_SHARED_RCP
       const double x0 = fma(lam, afac[0], -kC2), x1 = fma(lam, afac[1], -kC2), x2 = fma(lam, afac[2], -kC2);
-      cm |= ((fabs(x0) < kCoreX) | (fabs(x1) < kCoreX) | (fabs(x2) < kCoreX) ? 1u : 0u) << e;
+      cm |= (((fabs(x0) < kCoreX) | (fabs(x1) < kCoreX) | (fabs(x2) < kCoreX)) ? 1u : 0u) << e;
       double T0, T1, T2;
       wing_T3(x0, x1, x2, T0, T1, T2);
       t -= wing_poly(wing_g, T0);
