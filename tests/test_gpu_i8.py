@@ -113,3 +113,23 @@ def test_i8_unsupported_configurations_rejected():
     model = syn.make_model(k=20)
     with pytest.raises(L.GpdlaError):
         Engine(model, samples, set_parameters(k=20, num_lines=4), path="fused_i8")
+
+
+def test_i8_long_spectrum_batch_falls_back_to_fp64():
+    """A batch holding a spectrum longer than kI8MaxSlots (30,000 pixels: the int32 level sums stay
+    exact only below that) runs on the fp64 kernel: bit-identical to path='fused'."""
+    model = syn.make_model(k=20)
+    samples = syn.make_samples(64)
+    base = syn.make_spectrum(model, 1)
+    lo, hi = np.log10(base["wavelengths"][0]), np.log10(base["wavelengths"][-1])
+    lam = 10.0 ** np.linspace(lo, hi, 30500)
+    rng = np.random.default_rng(7)
+    long_spec = dict(wavelengths=lam, flux=np.interp(lam, base["wavelengths"], base["flux"]),
+                     noise_variance=rng.uniform(0.01, 0.09, lam.size), pixel_mask=np.zeros(lam.size, bool),
+                     z_qso=base["z_qso"])
+    packed = syn.pack_spectra([base, long_spec])
+    ref = _run(model, samples, packed, "fused")
+    out = _run(model, samples, packed, "fused_i8")
+    for key in KEYS:
+        np.testing.assert_array_equal(out[key], ref[key])
+    assert out["num_pixels"][1] > 30000
