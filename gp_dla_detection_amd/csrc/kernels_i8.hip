@@ -44,6 +44,9 @@ __device__ inline double u_bound(double y, double mu, double noise) {
 constexpr int kI8Levels = 4;
 #ifndef I8_SLOT_FENCE
 #define I8_SLOT_FENCE 0
+#endif
+#ifndef I8_PIPELINE
+#define I8_PIPELINE 1
 #endif  // digit levels i + j = 0..3 kept (10 of the 16 pairs)
 
 // ---------------------------------------------------------------------------------------------
@@ -229,14 +232,30 @@ __global__ __launch_bounds__(256, 1) void likelihood_i8_kernel(LikelihoodI8Args 
   constexpr int kBPieces = I::kChunkBytes / 1024 / kWavesPerBlock;  // per wave
   static_assert(I::kChunkBytes % (1024 * kWavesPerBlock) == 0, "B chunk splits into whole pieces");
   static_assert(I::kScalBytes == 1024 * kWavesPerBlock, "one record piece per wave");
-  auto stage = [&](int c, int buf) {
+  auto stage_b = [&](int c, int buf) {
     const uint8_t* bsrc = a.panel_i8 + (cb + c) * (int64_t)I::kChunkBytes + wave_s * kBPieces * 1024;
     dma_pieces(bsrc, ldsb_base + (uint32_t)(buf * I::kChunkBytes + wave_s * kBPieces * 1024), kBPieces, voff);
+  };
+  auto stage_rec = [&](int c, int buf) {
     const uint8_t* ssrc = reinterpret_cast<const uint8_t*>(a.scal + (cb + c) * kSBuf) + wave_s * 1024;
     dma_pieces(ssrc, ldss_base + (uint32_t)(buf * kSBuf * 8 + wave_s * 1024), 1, voff);
   };
+  auto stage = [&](int c, int buf) {
+    stage_b(c, buf);
+    stage_rec(c, buf);
+  };
 
+#if I8_PIPELINE
+  // software pipeline: iteration c computes chunk c's weights while its MFMAs contract chunk c-1
+  // (digits kept from the previous iteration, B planes in buffer (c-1)&1; B(c) is staged into
+  // buffer c&1 during iteration c).  Iteration 0 contracts an all-zero "chunk -1" (buffer 1).
+  static_assert(I::kTiles == 16, "one tile per slot of the 16-slot stage");
+  stage_rec(0, 0);
+  for (int i = threadIdx.x; i < I::kChunkBytes / 16; i += 256)
+    reinterpret_cast<uint4*>(ldsb + I::kChunkBytes)[i] = make_uint4(0u, 0u, 0u, 0u);
+#else
   stage(0, 0);
+#endif
   for (int i = threadIdx.x; i < 3 * kCoreTable; i += 256) core_lds[i] = a.lines.buf[i];
   if (threadIdx.x < 64) exp_lds[threadIdx.x] = a.lines.buf[kLineBufExp2 + threadIdx.x];
   if (threadIdx.x < 3 * kWingStride) wing_lds[threadIdx.x] = a.lines.buf[kLineBufWing + threadIdx.x];
@@ -273,9 +292,27 @@ __global__ __launch_bounds__(256, 1) void likelihood_i8_kernel(LikelihoodI8Args 
   double q1 = 0.0, pm = 1.0;
   int pe = 0;
 
+#if I8_PIPELINE
+  v4i Apg[4], Apu[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) Apg[i] = Apu[i] = (v4i){0, 0, 0, 0};
+#endif
   for (int c = 0; c < nch; ++c) {
     const int cur = c & 1;
+#if I8_PIPELINE
+    if (c + 1 < nch) stage_rec(c + 1, cur ^ 1);
+    stage_b(c, cur);
+    const uint8_t* bp = ldsb + (cur ^ 1) * I::kChunkBytes;  // B planes of chunk c - 1
+    auto load_bp = [&](int t, v4i (&Bt)[4]) {
+      const int ent = 16 * t + (lane & 15);
+      const int boff = ent * 64 + 16 * (g ^ ((ent >> 2) & 3));
+#pragma unroll
+      for (int j = 0; j < 4; ++j) Bt[j] = *reinterpret_cast<const v4i*>(bp + j * I::kPlaneBytes + boff);
+    };
+    v4i Bq[4];
+#else
     if (c + 1 < nch) stage(c + 1, cur ^ 1);
+#endif
     // ---- weights of this lane's 16 slots (fp64), quantised to X_A + 2^31, digits XOR 0x80
     const double* rec = ldss + cur * kSBuf + (16 * g) * I::kScal;
     // (1) line sums of the 16 slots, branch-free damping wings (one basic block: the scheduler
@@ -367,8 +404,28 @@ __global__ __launch_bounds__(256, 1) void likelihood_i8_kernel(LikelihoodI8Args 
     double2 n23 = *reinterpret_cast<const double2*>(rec + 2);
     double2 n45 = *reinterpret_cast<const double2*>(rec + 4);
     double nus = rec[6];
+#if I8_PIPELINE
+    load_bp(0, Bq);
+#endif
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
+#if I8_PIPELINE
+      {  // tile e of chunk c - 1 (its 10 MFMAs run beside this slot's VALU work)
+        const v4i B0 = Bq[0], B1 = Bq[1], B2 = Bq[2], B3 = Bq[3];
+        if (e + 1 < 16) load_bp(e + 1, Bq);
+        const v4i* A = e < I::kGT ? Apg : Apu;
+        acc[0][e] = MFMA_I8(A[0], B0, acc[0][e]);
+        acc[1][e] = MFMA_I8(A[0], B1, acc[1][e]);
+        acc[1][e] = MFMA_I8(A[1], B0, acc[1][e]);
+        acc[2][e] = MFMA_I8(A[0], B2, acc[2][e]);
+        acc[2][e] = MFMA_I8(A[1], B1, acc[2][e]);
+        acc[2][e] = MFMA_I8(A[2], B0, acc[2][e]);
+        acc[3][e] = MFMA_I8(A[0], B3, acc[3][e]);
+        acc[3][e] = MFMA_I8(A[1], B2, acc[3][e]);
+        acc[3][e] = MFMA_I8(A[2], B1, acc[3][e]);
+        acc[3][e] = MFMA_I8(A[3], B0, acc[3][e]);
+      }
+#endif
       const double y = n01.y, noise = n23.x, mu = n23.y, om2 = n45.x, gs = n45.y, us = nus;
       if (e + 1 < 16) {
         n01 = *reinterpret_cast<const double2*>(rec + (e + 1) * I::kScal);
@@ -405,14 +462,30 @@ __global__ __launch_bounds__(256, 1) void likelihood_i8_kernel(LikelihoodI8Args 
       pm = frexp(pm, &ex);
       pe += ex;
     }
+#if I8_PIPELINE
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      Apg[i] = digit_plane(xg, i);
+      Apu[i] = digit_plane(xu, i);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA (rec c+1, B c) landed
+    __syncthreads();
+  }
+  // drain: contract the last chunk
+  {
+    const v4i* Ag = Apg;
+    const v4i* Au = Apu;
+    const uint8_t* bb = ldsb + ((nch - 1) & 1) * I::kChunkBytes;
+#else
     v4i Ag[4], Au[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       Ag[i] = digit_plane(xg, i);
       Au[i] = digit_plane(xu, i);
     }
-    // ---- exact int8 contraction: the 10 digit pairs of level i + j <= 3 per tile
     const uint8_t* bb = ldsb + cur * I::kChunkBytes;
+#endif
+    // ---- exact int8 contraction: the 10 digit pairs of level i + j <= 3 per tile
     auto load_b = [&](int t, v4i (&Bt)[4]) {
       const int ent = 16 * t + (lane & 15);
       const int boff = ent * 64 + 16 * (g ^ ((ent >> 2) & 3));
@@ -440,8 +513,10 @@ __global__ __launch_bounds__(256, 1) void likelihood_i8_kernel(LikelihoodI8Args 
       acc[3][t] = MFMA_I8(A[3], B0, acc[3][t]);
       __builtin_amdgcn_sched_barrier(0);  // keep one tile's B digits live at a time
     }
+#if !I8_PIPELINE
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA for chunk c+1 landed
     __syncthreads();                                   // ... and everyone's; buffer c free again
+#endif
   }
 
   // ---- combine the 4 segments of each sample (lanes l, l^16, l^32, l^48)

@@ -17,6 +17,8 @@ VARIANTS = {
     "m0s0": dict(GPDLA_MAGIC_RINT=0, GPDLA_SHARED_RCP=0),
     "far1": dict(GPDLA_FAR_WING=1),
     "far0": dict(GPDLA_FAR_WING=0),
+    "i8pipe1": dict(I8_PIPELINE=1),
+    "i8pipe0": dict(I8_PIPELINE=0),
 }
 if __name__ == "__main__":
     names = sys.argv[1:] or list(VARIANTS)
