@@ -3,11 +3,11 @@
 Quantises the per-slot weights and panel entries exactly as convert_i8_kernel / likelihood_i8_kernel
 do, forms the digit-pair level sums in int64 (exact, like the int32 MFMA accumulators), and reports
 the log-likelihood error vs the fp64 restatement for the kept levels (<= 3 or <= 4).
-Experiment support only (imports the oracle as the checker)."""
+Test infrastructure (imports the oracle as the checker; lives under tests/ for that reason)."""
 import sys
 from pathlib import Path
 import numpy as np
-sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+sys.path.insert(0, str(Path(__file__).resolve().parents[2]))
 from oracle import gpdla_oracle as O
 from gp_dla_detection_amd import synthetic as syn
 
