@@ -23,26 +23,27 @@ def digits_balanced(X):
     return ds[::-1]  # d0 (most significant) .. d3
 
 
-def digits_offset(XA):
-    U = (XA + 2 ** 31).astype(np.int64)
-    return [((U >> (8 * (3 - i))) & 255) - 128 for i in range(4)]
-
-
-def contract(wt, Pt, maxlevel):
-    """sum_slot wt[slot] Pt[slot, e] via the int8 scheme; wt in [-1, 1], Pt any."""
+def contract(wt, Pt, maxlevel, signed):
+    """sum_slot wt[slot] Pt[slot, e] as kernels_i8.hip computes it: weights quantised to
+    X_A = rint(w (2^32 - 256)) (Gram, w in [0, 1]) or rint(w (2^31 - 256)) + 2^31 (u, w in [-1, 1])
+    read as 4 offset bytes; panel entries X_B = rint(P / s_e), s_e = max|P_e| / (127 2^24), in 4
+    balanced base-256 digits; digit pairs of level i + j <= maxlevel summed exactly (int64 here,
+    int32 on the GPU); + the offset term c * colsum_e."""
     mx = np.abs(Pt).max(axis=0)
-    ex = np.where(mx > 0, np.frexp(mx)[1], 0)
-    se = np.ldexp(1.0, ex)
-    XB = np.rint(np.ldexp(Pt, 30 - ex)).astype(np.int64)
-    XA = np.rint(wt * 2.0 ** 30).astype(np.int64)
-    dA, dB = digits_offset(XA), digits_balanced(XB)
+    mx = np.where(mx > 0, mx, 1.0)
+    se = mx / (127 * 2.0 ** 24)
+    XB = np.rint(Pt / se).astype(np.int64)
+    sc = (2.0 ** 31 - 256) if signed else (2.0 ** 32 - 256)
+    U = np.rint(wt * sc).astype(np.int64) + (2 ** 31 if signed else 0)
+    dA = [((U >> (8 * (3 - i))) & 255) - 128 for i in range(4)]
+    dB = digits_balanced(XB)
     tot = np.zeros(Pt.shape[1])
     for i in range(4):
         for j in range(4):
             if i + j <= maxlevel:
                 tot += (2.0 ** (8 * (6 - i - j))) * (dA[i][:, None] * dB[j]).sum(axis=0)
-    tot += 8421504.0 * XB.sum(axis=0)
-    return tot * se * 2.0 ** -60
+    tot += (8421504.0 if signed else 2155905152.0) * XB.sum(axis=0)
+    return tot * se / sc
 
 
 def ll_i8(prep, z, nhi, maxlevel):
@@ -56,13 +57,13 @@ def ll_i8(prep, z, nhi, maxlevel):
     iu = np.triu_indices(k)
     P = (M[:, iu[0]] * M[:, iu[1]])
     wt = wg * (om2 + noise)
-    G = contract(wt, P / (om2 + noise)[:, None], maxlevel)
+    G = contract(wt, P / (om2 + noise)[:, None], maxlevel, False)
     f = np.abs(y - mu)
     av = np.where(mu != 0, y / (2 * np.where(mu != 0, mu, 1)), -1)
     f = np.where((av > 0) & (av < 1), np.maximum(f, np.abs(y * av - mu * av * av)), f)
     beta = 1.125 * f / noise
     beta = np.where((beta > 0) & np.isfinite(beta), beta, 1.0)
-    u = contract(wu / beta, M * beta[:, None], maxlevel)
+    u = contract(wu / beta, M * beta[:, None], maxlevel, True)
     B = np.eye(k)
     B[iu] += G
     B = np.triu(B) + np.triu(B, 1).T
