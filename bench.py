@@ -155,7 +155,7 @@ def main():
     ap.add_argument("--spectra", type=int, default=None, help="override: spectra per GPU (c2/c5)")
     ap.add_argument("--samples", type=int, default=None, help="override: DLA samples")
     ap.add_argument("--k", type=int, default=None, help="override: rank")
-    ap.add_argument("--path", choices=["auto", "fused", "fused_i8", "panel_gemm"], default="auto",
+    ap.add_argument("--path", choices=["auto", "fused", "fused_i8", "panel_gemm", "panel_gemm_i8"], default="auto",
                     help="likelihood path (Engine path=): auto = fused fp64 kernel for the compiled ranks, "
                          "fused_i8 = the int8 Ozaki contraction (k=20), panel_gemm = weights + dgemm + LDL^T")
     ap.add_argument("--no-alt", action="store_true",
@@ -215,6 +215,8 @@ def main():
     eng = Engine(model, samples, set_parameters(k=args.k), device=dev, path=args.path)
     if args.path == "fused_i8":
         path = "fused-int8"
+    elif args.path == "panel_gemm_i8":
+        path = "panel-GEMM-int8"
     elif args.path == "panel_gemm" or args.k not in (4, 8, 10, 12, 16, 20, 24):
         path = "panel-GEMM"
     else:
@@ -319,7 +321,8 @@ def main():
                      "frac": achieved_tf / FP64_PEAK_TFLOPS, "traffic": traffic,
                      "traffic_source": traffic_src,
                      "kernel": {"fused": f"likelihood_kernel<{args.k}>",
-                                "fused-int8": f"likelihood_i8_kernel<{args.k}>"}.get(
+                                "fused-int8": f"likelihood_i8_kernel<{args.k}>",
+                                "panel-GEMM-int8": "weights_i8_kernel + gemm_i8_kernel + ldl_reg_kernel (per batch)"}.get(
                                     path, "weights_kernel + rocBLAS dgemm + ldl_reg_kernel (per batch)"),
                      "avg_launch_ms": avg_ms,
                      "flops_per_eval": algorithmic_flops_per_eval(n_mean, args.k),

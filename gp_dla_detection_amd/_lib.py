@@ -26,6 +26,7 @@ PATH_AUTO = 0
 PATH_FUSED = 1
 PATH_PANEL_GEMM = 2
 PATH_FUSED_I8 = 3
+PATH_PANEL_GEMM_I8 = 4
 
 dp = C.POINTER(C.c_double)
 i64p = C.POINTER(C.c_int64)

@@ -8,7 +8,7 @@ from pathlib import Path
 
 PKG = Path(__file__).resolve().parent
 CSRC = PKG / "csrc"
-SOURCES = ["kernels.hip", "kernels_i8.hip", "gemm_path.hip", "engine.hip", "objective.hip", "faddeeva_host.cpp"]
+SOURCES = ["kernels.hip", "kernels_i8.hip", "gemm_path.hip", "gemm_i8.hip", "engine.hip", "objective.hip", "faddeeva_host.cpp"]
 OUT = PKG / "libgpdla.so"
 
 

@@ -73,6 +73,38 @@ __device__ inline double rcp_sweep(double d) {
 #endif
 }
 
+// ---- int8 Ozaki contraction helpers (kernels_i8.hip, gemm_i8.hip)
+typedef int v4i __attribute__((ext_vector_type(4)));
+
+// weight quantisation: Gram X_A = rint(w~ kI8ScaleG) in [0, 2^32) read directly as 4 offset bytes;
+// u X_A = rint(u~ kI8ScaleU) stored as X_A + 2^31.  256 below the power of two keeps rint inside
+// the range when w~ rounds a hair above 1.
+constexpr double kI8ScaleG = 4294967040.0;  // 2^32 - 256
+constexpr double kI8ScaleU = 2147483392.0;  // 2^31 - 256
+
+// Static per-slot bound beta >= |a r / d| over a in [0, 1]: |a (y - mu a)| is a parabola in a
+// (max at a = 1 or at its vertex y / (2 mu)), and d = omega^2 a^2 + sigma^2 >= sigma^2.
+__device__ inline double u_bound(double y, double mu, double noise) {
+  double f = fabs(y - mu);
+  if (mu != 0.0) {
+    const double av = y / (2 * mu);
+    if (av > 0.0 && av < 1.0) f = fmax(f, fabs(y * av - mu * av * av));
+  }
+  const double b = 1.125 * f / noise;
+  return (b > 0.0 && b < INFINITY) ? b : 1.0;
+}
+
+// digit plane i (byte 3 - i of each X) of 16 slots, packed 4 slots per dword in K order
+__device__ inline v4i digit_plane(const uint32_t (&x)[16], int i) {
+  const int sh = 8 * (3 - i);
+  v4i r;
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+    r[m] = (int)(((x[4 * m] >> sh) & 0xffu) | (((x[4 * m + 1] >> sh) & 0xffu) << 8) |
+                 (((x[4 * m + 2] >> sh) & 0xffu) << 16) | (((x[4 * m + 3] >> sh) & 0xffu) << 24));
+  return r;
+}
+
 // exp(v) for v <= 0 (v = N * total, voigt.c:291): v = (64 m + j) ln2/64 + r, |r| <= ln2/128,
 // exp(v) = 2^m * 2^(j/64) * e^r with 2^(j/64) from a 64-entry LDS table (host-rounded from long
 // double) and e^r a degree-5 Taylor polynomial (truncation < 4e-17).  Underflows to +0 like exp.

@@ -140,7 +140,9 @@ struct gpdla_engine {
   size_t cap_pm = 0, cap_srow = 0, cap_wg = 0, cap_wu = 0, cap_G = 0, cap_U = 0, cap_q1p = 0,
          cap_ldp = 0;
   // int8 fused path workspaces
-  uint8_t* d_pi8 = nullptr;
+  uint8_t* d_pi8 = nullptr;          // fused: digit chunks; panel-GEMM: B digit planes per spectrum
+  uint8_t* d_ai8 = nullptr;          // panel-GEMM int8: A digit planes of a sample chunk
+  size_t cap_ai8 = 0;
   double *d_psc = nullptr, *d_pent = nullptr;
   size_t cap_pi8 = 0, cap_psc = 0, cap_pent = 0;
 
@@ -190,7 +192,7 @@ int validate_params(const gpdla_params* p) {
     return set_error(GPDLA_EINVAL, "invalid wavelength parameters");
   if (p->max_batch_spectra < 0) return set_error(GPDLA_EINVAL, "max_batch_spectra < 0");
   if (p->path != GPDLA_PATH_AUTO && p->path != GPDLA_PATH_FUSED && p->path != GPDLA_PATH_PANEL_GEMM &&
-      p->path != GPDLA_PATH_FUSED_I8)
+      p->path != GPDLA_PATH_FUSED_I8 && p->path != GPDLA_PATH_PANEL_GEMM_I8)
     return set_error(GPDLA_EINVAL, "path=%d", p->path);
   return GPDLA_OK;
 }
@@ -232,7 +234,7 @@ void gpdla_engine_destroy(gpdla_engine* e) {
                   e->d_info, e->d_panel, e->d_lam, e->d_smap, e->d_scratch, e->d_sll,
                   e->d_llnull, e->d_lldla, e->d_zmin, e->d_zmax, e->d_npix, e->d_pm, e->d_srow,
                   e->d_wg, e->d_wu, e->d_G, e->d_U, e->d_q1p, e->d_ldp, e->d_pi8, e->d_psc,
-                  e->d_pent};
+                  e->d_pent, e->d_ai8};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (e->h_meta) (void)hipHostFree(e->h_meta);
@@ -250,9 +252,12 @@ int gpdla_engine_create(int32_t device, const gpdla_model* model, const gpdla_sa
   if (rc) return rc;
   if ((rc = validate_params(params))) return rc;
   const bool fused_ok = rank_supported(model->k);
-  const bool use_gemm = params->path == GPDLA_PATH_PANEL_GEMM || (params->path == GPDLA_PATH_AUTO && !fused_ok);
-  const bool use_i8 = params->path == GPDLA_PATH_FUSED_I8;
-  if (use_i8 && (!i8_supported(model->k) || params->num_lines != 3))
+  const bool use_gemm = params->path == GPDLA_PATH_PANEL_GEMM || params->path == GPDLA_PATH_PANEL_GEMM_I8 ||
+                        (params->path == GPDLA_PATH_AUTO && !fused_ok);
+  const bool use_i8 = params->path == GPDLA_PATH_FUSED_I8 || params->path == GPDLA_PATH_PANEL_GEMM_I8;
+  if (params->path == GPDLA_PATH_PANEL_GEMM_I8 && params->num_lines != 3)
+    return set_error(GPDLA_EUNSUPPORTED, "int8 panel-GEMM path needs num_lines=3 (num_lines=%d)", params->num_lines);
+  if (params->path == GPDLA_PATH_FUSED_I8 && (!i8_supported(model->k) || params->num_lines != 3))
     return set_error(GPDLA_EUNSUPPORTED, "int8 fused path needs k=20 and num_lines=3 (k=%d, num_lines=%d)",
                      model->k, params->num_lines);
   if (!use_gemm && !fused_ok)
@@ -345,8 +350,8 @@ int gpdla_engine_set_stream(gpdla_engine* e, void* hip_stream) {
 // Panel-GEMM path for one batch: per spectrum and chunk of samples, weights -> two dgemm ->
 // batched LDL^T (gemm_path.hip).  All on stream st, in order.
 static int run_panel_gemm(gpdla_engine* e, int64_t nq, const int64_t* h_sb, const int64_t* h_lb,
-                          const int64_t* h_cap, int64_t sc_max, double* o_sll, int64_t ld,
-                          double* o_null, hipStream_t st) {
+                          const int64_t* h_cap, const int64_t* h_cb, int64_t sc_max, double* o_sll,
+                          int64_t ld, double* o_null, hipStream_t st) {
   const int K = e->K;
   const int64_t E = (int64_t)K * (K + 1) / 2;
   if (rocblas_set_stream(e->blas, st) != rocblas_status_success)
@@ -355,6 +360,28 @@ static int run_panel_gemm(gpdla_engine* e, int64_t nq, const int64_t* h_sb, cons
   for (int64_t q = 0; q < nq; ++q) {
     for (int64_t s0 = 0; s0 <= e->S; s0 += sc_max) {
       const int32_t sc = (int32_t)std::min<int64_t>(sc_max, e->S + 1 - s0);
+      if (e->i8) {  // int8 Ozaki contraction (gemm_i8.hip): weights digits -> exact GEMM -> Gram, u
+        const int64_t ks = i8_gemm_kstride(h_cap[q]);
+        const int64_t rows = (sc_max + 127) / 128 * 128;
+        WeightsI8Args wi{};
+        wi.info = e->d_info; wi.q = (int32_t)q;
+        wi.srow = e->d_srow + h_sb[q] * 8; wi.lam_pad = e->d_lam + h_lb[q]; wi.kstride = ks;
+        wi.offsets = e->d_off; wi.nhi = e->d_nhi; wi.S = e->S; wi.s0 = s0; wi.sc = sc; wi.rows = rows;
+        wi.lines = make_line_args(e->d_lines); wi.adig = e->d_ai8; wi.q1p = e->d_q1p; wi.ldp = e->d_ldp;
+        HIP_TRY(launch_weights_i8(wi, st));
+        GemmI8Args gi{};
+        gi.info = e->d_info; gi.q = (int32_t)q; gi.k = K; gi.kstride = ks; gi.rows = rows; gi.sc = sc;
+        gi.adig = e->d_ai8; gi.bdig = e->d_pi8 + h_cb[q];
+        gi.ent = e->d_pent + q * 2 * (int64_t)i8_gemm_entries(K); gi.G = e->d_G; gi.U = e->d_U;
+        HIP_TRY(launch_gemm_i8(gi, st));
+        LdlArgs da{};
+        da.info = e->d_info; da.q = (int32_t)q; da.k = K;
+        da.G = e->d_G; da.U = e->d_U; da.q1p = e->d_q1p; da.ldp = e->d_ldp;
+        da.S = e->S; da.s0 = s0; da.sc = sc; da.perm = e->d_perm;
+        da.sample_ll = o_sll ? o_sll + q * ld : nullptr; da.ll_null = o_null + q; da.status = e->d_status;
+        HIP_TRY(launch_ldl_batch(da, st));
+        continue;
+      }
       WeightsArgs wa{};
       wa.info = e->d_info; wa.q = (int32_t)q;
       wa.srow = e->d_srow + h_sb[q] * 8; wa.lam_pad = e->d_lam + h_lb[q]; wa.cap = h_cap[q];
@@ -439,8 +466,13 @@ int gpdla_engine_process(gpdla_engine* e, const gpdla_spectra* sp, const gpdla_r
       h_sb[q] = slots;
       h_lb[q] = lams;
       h_cap[q] = cap;
-      h_cb[q] = chunks;
-      chunks += ((lpix + 3) / 4 + 15) / 16;  // >= ceil(L / 16) chunks of 16 steps per segment
+      if (e->gemm) {  // int8 panel-GEMM: byte base of the spectrum's B digit planes
+        h_cb[q] = chunks;
+        chunks += 4 * (int64_t)i8_gemm_entries(e->K) * i8_gemm_kstride(cap);
+      } else {
+        h_cb[q] = chunks;
+        chunks += ((lpix + 3) / 4 + 15) / 16;  // >= ceil(L / 16) chunks of 16 steps per segment
+      }
       lpix_max = std::max(lpix_max, lpix);
       cap_max = std::max(cap_max, cap);
       slots += cap;
@@ -469,7 +501,13 @@ int gpdla_engine_process(gpdla_engine* e, const gpdla_spectra* sp, const gpdla_r
       if ((rc = grow(&e->d_scratch, &e->cap_scr, (size_t)blocks_x * nq * kSamplesPerBlock * es))) return rc;
     }
     // int8 contraction for this batch (exactness bound on the slot count, else the fp64 kernel)
-    const bool batch_i8 = e->i8 && lpix_max <= kI8MaxSlots;
+    const bool batch_i8 = e->i8 && !e->gemm && lpix_max <= kI8MaxSlots;
+    if (e->i8 && e->gemm) {
+      if ((rc = grow(&e->d_pi8, &e->cap_pi8, (size_t)chunks))) return rc;
+      if ((rc = grow(&e->d_pent, &e->cap_pent, (size_t)nq * 2 * i8_gemm_entries(e->K)))) return rc;
+      if ((rc = grow(&e->d_ai8, &e->cap_ai8,
+                     (size_t)8 * ((sc_max + 127) / 128 * 128) * i8_gemm_kstride(cap_max + 0)))) return rc;
+    }
     if (batch_i8) {
       if ((rc = grow(&e->d_pi8, &e->cap_pi8, (size_t)chunks * i8_chunk_bytes(e->K)))) return rc;
       if ((rc = grow(&e->d_psc, &e->cap_psc, (size_t)chunks * 64 * 8))) return rc;
@@ -578,6 +616,13 @@ int gpdla_engine_process(gpdla_engine* e, const gpdla_spectra* sp, const gpdla_r
     if ((rc = record_start(e, &t0, 0))) return rc;
     HIP_TRY(launch_prep(e->gemm ? 0 : e->K, pa, st));
     if (batch_i8) HIP_TRY(launch_convert_i8(e->K, ca, st));
+    if (e->i8 && e->gemm) {
+      ConvertGemmI8Args cg{};
+      cg.k = e->K; cg.info = e->d_info; cg.panel = e->d_panel; cg.panel_m = e->d_pm; cg.srow = e->d_srow;
+      cg.slot_base = pa.slot_base; cg.slot_cap = pa.slot_cap; cg.bbase = pa.slot_cap + QB;
+      cg.bdig = e->d_pi8; cg.ent = e->d_pent;
+      HIP_TRY(launch_convert_gemm_i8(cg, (int32_t)nq, st));
+    }
     HIP_TRY(hipEventRecord(t0.stop, st));
     e->pending.push_back(t0);
     if ((rc = record_start(e, &t1, 1))) return rc;
@@ -585,7 +630,7 @@ int gpdla_engine_process(gpdla_engine* e, const gpdla_spectra* sp, const gpdla_r
       HIP_TRY(launch_likelihood_i8(e->K, li, st));
     } else if (!e->gemm) {
       HIP_TRY(launch_likelihood(e->K, la, st));
-    } else if ((rc = run_panel_gemm(e, nq, h_sb, h_lb, h_cap, sc_max, o_sll, ld, o_null, st))) {
+    } else if ((rc = run_panel_gemm(e, nq, h_sb, h_lb, h_cap, h_cb, sc_max, o_sll, ld, o_null, st))) {
       return rc;
     }
     HIP_TRY(hipEventRecord(t1.stop, st));

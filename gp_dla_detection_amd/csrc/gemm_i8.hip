@@ -1,0 +1,381 @@
+// Panel-GEMM path with the Gram/u contraction on the int8 matrix cores (path panel_gemm_i8, any
+// rank 1..kGemmMaxK; BASELINE configs[4]: k = 50, 10^5 samples, quoted in fp32).  Same numerics as
+// the fused int8 kernel (kernels_i8.hip), as a GEMM:
+//   convert_gemm_i8_kernel  panel entries P~ (Khatri-Rao / (omega^2 + sigma^2), M beta) -> 4
+//                           balanced base-256 digit planes per entry, K-contiguous, + scales
+//   weights_i8_kernel       Voigt x pixel terms (process_qsos.m:186-197) -> the quantised weights
+//                           w~, u~ as 4 offset-byte digit planes per sample, K-contiguous, and the
+//                           sum r^2/d, sum log d partials of the fp64 weights kernel
+//   gemm_i8_kernel          C[s][e] = sum_slot X_A X_B exactly (10 digit pairs of level <= 3 on
+//                           v_mfma_i32_16x16x64_i8, int32 per level), fp64 epilogue -> Gram / u
+// followed by the fp64 augmented LDL^T of gemm_path.hip (log_mvnpdf_low_rank.m:22-32).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+
+#include "device_common.h"
+#include "internal.h"
+
+namespace gpdla {
+
+namespace {
+
+#define MFMA_I8(A, B, C) __builtin_amdgcn_mfma_i32_16x16x64_i8((A), (B), (C), 0, 0, 0)
+
+// --------------------------------------------------------------------------------------------
+// convert: grid (entries / 64, spectra), 256 threads = 64 entries x 4 segments
+// --------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void convert_gemm_i8_kernel(ConvertGemmI8Args a) {
+  __shared__ double s_mx[4][64];
+  __shared__ long long s_cs[4][64];
+  const int q = blockIdx.y;
+  const SpecInfo inf = a.info[q];
+  if (inf.J == 0) return;
+  const int K = a.k;
+  const int E = K * (K + 1) / 2;
+  const int Ep = 64 * ((E + 63) / 64);
+  const int NE = i8_gemm_entries(K);
+  const int le = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int e = blockIdx.x * 64 + le;
+  const bool is_u = e >= Ep;
+  const int col = is_u ? e - Ep : e;
+  const bool valid = is_u ? col < K : col < E;
+  const int L = inf.L;
+  const int Ls = ((L + kChunkSteps - 1) / kChunkSteps) * kChunkSteps;
+  const int Ls16 = 16 * ((L + 15) / 16);
+  const int64_t sb = a.slot_base[q];
+  const int64_t kstride = i8_gemm_kstride(a.slot_cap[q]);
+  auto value = [&](int t) -> double {
+    if (!valid || t >= L) return 0.0;
+    const int64_t row = sb + (int64_t)g * Ls + t;
+    const double* sr = a.srow + row * 8;
+    const double y = sr[1], noise = sr[2], mu = sr[3], om2 = sr[4];
+    return is_u ? a.panel_m[row * K + col] * u_bound(y, mu, noise) : a.panel[row * E + col] / (om2 + noise);
+  };
+  double mx = 0.0;
+  for (int t = 0; t < L; ++t) mx = fmax(mx, fabs(value(t)));
+  s_mx[g][le] = mx;
+  __syncthreads();
+  mx = fmax(fmax(s_mx[0][le], s_mx[1][le]), fmax(s_mx[2][le], s_mx[3][le]));
+  const double s_e = mx > 0.0 ? mx * (1.0 / (127.0 * 0x1p24)) : 1.0;  // |X_B| <= 127 2^24
+  long long colsum = 0;
+  uint8_t* base = a.bdig + a.bbase[q] + (int64_t)e * kstride + (int64_t)g * Ls16;
+  const int64_t plane = (int64_t)NE * kstride;
+  for (int t0 = 0; t0 < Ls16; t0 += 16) {
+    uint32_t pl[4][4];
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) pl[j][w] = 0u;
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        int X = (int)rint(value(t0 + 4 * w + b) / s_e);
+        colsum += X;
+        const int d3 = ((X + 128) & 255) - 128; X = (X - d3) >> 8;
+        const int d2 = ((X + 128) & 255) - 128; X = (X - d2) >> 8;
+        const int d1 = ((X + 128) & 255) - 128; X = (X - d1) >> 8;
+        pl[0][w] |= (uint32_t)(X & 255) << (8 * b);
+        pl[1][w] |= (uint32_t)(d1 & 255) << (8 * b);
+        pl[2][w] |= (uint32_t)(d2 & 255) << (8 * b);
+        pl[3][w] |= (uint32_t)(d3 & 255) << (8 * b);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      *reinterpret_cast<uint4*>(base + j * plane + t0) = make_uint4(pl[j][0], pl[j][1], pl[j][2], pl[j][3]);
+  }
+  s_cs[g][le] = colsum;
+  __syncthreads();
+  if (g == 0) {
+    const long long cs = s_cs[0][le] + s_cs[1][le] + s_cs[2][le] + s_cs[3][le];
+    a.ent[(int64_t)q * 2 * NE + e] = s_e / (is_u ? kI8ScaleU : kI8ScaleG);
+    a.ent[(int64_t)q * 2 * NE + NE + e] = (is_u ? 8421504.0 : 2155905152.0) * (double)cs;
+  }
+}
+
+// --------------------------------------------------------------------------------------------
+// weights: grid (ceil(sc / 64), 4 quarters), 4 waves = 4 segments, lane = sample.  Each wave walks
+// its quarter of the segment (whole 16-slot groups) with the register sliding window, and stores
+// each 16-slot group as 16 bytes per digit plane (K-contiguous rows: the GEMM's A operand).
+// --------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void weights_i8_kernel(WeightsI8Args a) {
+  constexpr int kWingLds = 4 * ((3 * kWingStride + 3) / 4);
+  __shared__ __attribute__((aligned(16))) double tables[3 * kCoreTable + kWingLds + 64];
+  const SpecInfo inf = a.info[a.q];
+  if (inf.J == 0) return;  // the LDL kernel writes NaN
+  const int lane = threadIdx.x & 63;
+  const int g = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int sl = blockIdx.x * 64 + lane;
+  const bool active = sl < a.sc;
+  const int64_t s = a.s0 + sl;
+  double* core_lds = tables;
+  double* wing_lds = tables + 3 * kCoreTable;
+  double* exp_lds = wing_lds + kWingLds;
+  for (int i = threadIdx.x; i < 3 * kCoreTable; i += 256) core_lds[i] = a.lines.buf[i];
+  if (threadIdx.x < 64) exp_lds[threadIdx.x] = a.lines.buf[kLineBufExp2 + threadIdx.x];
+  if (threadIdx.x < 3 * kWingStride) wing_lds[threadIdx.x] = a.lines.buf[kLineBufWing + threadIdx.x];
+  __syncthreads();
+  const int L = inf.L;
+  const int Ls = ((L + kChunkSteps - 1) / kChunkSteps) * kChunkSteps;
+  const int Ls16 = 16 * ((L + 15) / 16);
+  const int Lq16 = 16 * ((Ls16 / 16 + kWeightQuarters - 1) / kWeightQuarters);
+  const int h = blockIdx.y;
+  const int t0 = min(h * Lq16, Ls16), t1 = min(t0 + Lq16, Ls16);
+  const double off = (s < a.S) ? a.offsets[s] : 0.5;
+  const double N = (s < a.S) ? a.nhi[s] : 0.0;  // null model / idle lanes: absorption exactly 1
+  const double zdla = inf.zmin + (inf.zmax - inf.zmin) * off;  // process_qsos.m:163-165
+  const double zfac = 1.0 / (1 + zdla);
+  double afac[3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) afac[j] = a.lines.buf[kLineBufFac + j] * zfac;
+  auto raw = [&](double lam) { return raw_profile3(lam, afac, N, core_lds, wing_lds, exp_lds); };
+  const double* lamp = a.lam_pad + (int64_t)g * L + t0;  // padded positions g L + t0 + 0..5
+  double w0 = raw(lamp[0]), w1 = raw(lamp[1]), w2 = raw(lamp[2]);
+  double w3 = raw(lamp[3]), w4 = raw(lamp[4]), w5 = raw(lamp[5]);
+  double q1 = 0.0, pm = 1.0;
+  int pe = 0;
+  const int64_t plane = a.rows * a.kstride;
+  uint8_t* ag = a.adig + (int64_t)sl * a.kstride + (int64_t)g * Ls16;
+  uint8_t* au = ag + 4 * plane;
+  for (int tg = t0; tg < t1; tg += 16) {
+    // (1) branch-free damping wings of the group's 16 slots (one shared reciprocal per slot),
+    // (2) rare core fix-up, (3) table exps, (4) convolution, pixel terms, quantised weights --
+    // the staging of likelihood_i8_kernel (kernels_i8.hip), here with lanes = samples
+    double lamv[16], tot[16];
+    uint32_t cm = 0;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int t = tg + e;
+      lamv[e] = t < L ? a.srow[((int64_t)g * Ls + t) * 8] : a.lam_pad[(int64_t)g * L + t + 2 * kWidth];
+    }
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const double x0 = fma(lamv[e], afac[0], -kC2), x1 = fma(lamv[e], afac[1], -kC2),
+                   x2 = fma(lamv[e], afac[2], -kC2);
+      cm |= (((fabs(x0) < kCoreX) | (fabs(x1) < kCoreX) | (fabs(x2) < kCoreX)) ? 1u : 0u) << e;
+      double T0, T1, T2;
+      wing_T3(x0, x1, x2, T0, T1, T2);
+      double t = 0.0;
+      t -= wing_poly(wing_lds, T0);
+      t -= wing_poly(wing_lds + kWingStride, T1);
+      t -= wing_poly(wing_lds + 2 * kWingStride, T2);
+      tot[e] = t;
+    }
+    if (cm) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        if (cm & (1u << e)) {
+          double t = 0.0;
+#pragma unroll
+          for (int j = 0; j < 3; ++j) {
+            const double x = fma(lamv[e], afac[j], -kC2);
+            const double ax = fabs(x);
+            double f = wing_eval(wing_lds + j * kWingStride, x);
+            if (ax < kCoreX) f = core_eval(core_lds + j * kCoreTable, ax);
+            t -= f;
+          }
+          tot[e] = t;
+        }
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 16; ++e) tot[e] = exp_tab64(N * tot[e], exp_lds);  // voigt.c:291
+    uint32_t xg[16], xu[16];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int t = tg + e;
+      double y = 0.0, noise = 1.0, mu = 0.0, om2 = 0.0;  // neutral past the segment
+      if (t < L) {
+        const double* sr = a.srow + ((int64_t)g * Ls + t) * 8;
+        y = sr[1]; noise = sr[2]; mu = sr[3]; om2 = sr[4];
+      }
+      const double w6 = tot[e];
+      double ab = w0 * kInstrumentProfile[0];  // voigt.c:297-299
+      ab = fma(w1, kInstrumentProfile[1], ab);
+      ab = fma(w2, kInstrumentProfile[2], ab);
+      ab = fma(w3, kInstrumentProfile[3], ab);
+      ab = fma(w4, kInstrumentProfile[4], ab);
+      ab = fma(w5, kInstrumentProfile[5], ab);
+      ab = fma(w6, kInstrumentProfile[6], ab);
+      w0 = w1; w1 = w2; w2 = w3; w3 = w4; w4 = w5; w5 = w6;
+      const double r = fma(-mu, ab, y);  // process_qsos.m:191-197, log_mvnpdf_low_rank.m:11-15
+      const double a2 = ab * ab;
+      const double d = fma(om2, a2, noise);
+      const double dinv = rcp_sweep(d);
+      const double rd = r * dinv;
+      q1 = fma(r, rd, q1);
+      pm *= d;
+      xg[e] = (uint32_t)__builtin_rint(a2 * dinv * ((om2 + noise) * kI8ScaleG)) ^ 0x80808080u;
+      xu[e] = (uint32_t)__builtin_rint(fma(ab * rd, kI8ScaleU / u_bound(y, mu, noise), 0x1p31)) ^ 0x80808080u;
+    }
+    {
+      int ex;
+      pm = frexp(pm, &ex);
+      pe += ex;
+    }
+    if (active) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const v4i dg = digit_plane(xg, i), du = digit_plane(xu, i);
+        *reinterpret_cast<v4i*>(ag + i * plane + (tg - 0)) = dg;
+        *reinterpret_cast<v4i*>(au + i * plane + (tg - 0)) = du;
+      }
+    }
+  }
+  if (active) {
+    a.q1p[(int64_t)sl * kWeightParts + g * kWeightQuarters + h] = q1;
+    a.ldp[(int64_t)sl * kWeightParts + g * kWeightQuarters + h] = log(pm) + pe * kLn2;
+  }
+}
+
+// global -> LDS DMA of one 1 KiB piece (64 lanes x 16 B, per-lane global byte offsets)
+__device__ inline void dma_piece(const uint8_t* sbase, uint32_t voffset, uint32_t lds_dst) {
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+  asm volatile("s_nop 4\n\ts_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2"
+               :: "s"(lds_dst), "v"(voffset), "s"(sbase) : "memory", "m0");
+#pragma clang diagnostic pop
+}
+
+// --------------------------------------------------------------------------------------------
+// GEMM: grid (rows / 128 sample tiles, entries / 64 entry tiles), 4 waves; wave w owns samples
+// 32 w .. 32 w + 31 of the tile (2 row tiles) x all 64 entries (4 column tiles).  Per 64-slot K
+// step the block stages A (4 planes x 128 samples x 64 B) and B (4 planes x 64 entries x 64 B)
+// in LDS, 16 B granules XOR-swizzled by row so the MFMA operand reads are bank-conflict free.
+// --------------------------------------------------------------------------------------------
+constexpr int kGTileS = 128, kGTileE = 64;
+
+__global__ __launch_bounds__(256, 2) void gemm_i8_kernel(GemmI8Args a) {
+  __shared__ __attribute__((aligned(16))) uint8_t As[4 * kGTileS * 64];
+  __shared__ __attribute__((aligned(16))) uint8_t Bs[4 * kGTileE * 64];
+  const SpecInfo inf = a.info[a.q];
+  if (inf.J == 0) return;
+  const int K = a.k;
+  const int E = K * (K + 1) / 2;
+  const int Ep = 64 * ((E + 63) / 64);
+  const int NE = i8_gemm_entries(K);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wave_s = __builtin_amdgcn_readfirstlane(wave);
+  const int s_tile = blockIdx.x * kGTileS;
+  const int e_tile = blockIdx.y * kGTileE;
+  const bool u_tile = e_tile >= Ep;
+  const int nks = (16 * ((inf.L + 15) / 16)) / 16;  // 4 Ls16 / 64
+  const int64_t planeA = a.rows * a.kstride, planeB = (int64_t)NE * a.kstride;
+  const uint8_t* A0 = a.adig + (u_tile ? 4 * planeA : 0) + (int64_t)s_tile * a.kstride;
+  const uint8_t* B0 = a.bdig + (int64_t)e_tile * a.kstride;
+  const uint32_t as_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)As;
+  const uint32_t bs_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)Bs;
+  // this lane's piece geometry: row (l >> 2) of a 16-row piece, LDS granule l & 3 holds global
+  // granule (l & 3) ^ ((row >> 2) & 3)
+  const int prow = lane >> 2;
+  v4i acc[4][2][4];
+#pragma unroll
+  for (int l = 0; l < 4; ++l)
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+      for (int ct = 0; ct < 4; ++ct) acc[l][rt][ct] = (v4i){0, 0, 0, 0};
+  const int g = lane >> 4;
+  for (int ks = 0; ks < nks; ++ks) {
+    // A: 32 pieces (plane p = piece / 8, rows 16 (piece % 8) ..), 8 per wave
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int piece = wave_s * 8 + i;
+      const int p = piece >> 3, row = (piece & 7) * 16 + prow;
+      const uint32_t voffset = (uint32_t)((int64_t)row * a.kstride + ks * 64 + 16 * ((lane & 3) ^ ((row >> 2) & 3)));
+      dma_piece(A0 + p * planeA, voffset, as_base + (uint32_t)(piece * 1024));
+    }
+    // B: 16 pieces (plane p = piece / 4, entries 16 (piece % 4) ..), 4 per wave
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int piece = wave_s * 4 + i;
+      const int p = piece >> 2, row = (piece & 3) * 16 + prow;
+      const uint32_t voffset = (uint32_t)((int64_t)row * a.kstride + ks * 64 + 16 * ((lane & 3) ^ ((row >> 2) & 3)));
+      dma_piece(B0 + p * planeB, voffset, bs_base + (uint32_t)(piece * 1024));
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    v4i Ad[2][4];
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt) {
+      const int row = 32 * wave + 16 * rt + (lane & 15);
+#pragma unroll
+      for (int p = 0; p < 4; ++p)
+        Ad[rt][p] = *reinterpret_cast<const v4i*>(As + p * (kGTileS * 64) + row * 64 + 16 * (g ^ ((row >> 2) & 3)));
+    }
+#pragma unroll
+    for (int ct = 0; ct < 4; ++ct) {
+      const int row = 16 * ct + (lane & 15);
+      v4i Bd[4];
+#pragma unroll
+      for (int p = 0; p < 4; ++p)
+        Bd[p] = *reinterpret_cast<const v4i*>(Bs + p * (kGTileE * 64) + row * 64 + 16 * (g ^ ((row >> 2) & 3)));
+#pragma unroll
+      for (int rt = 0; rt < 2; ++rt) {
+        const v4i* Ar = Ad[rt];
+        acc[0][rt][ct] = MFMA_I8(Ar[0], Bd[0], acc[0][rt][ct]);
+        acc[1][rt][ct] = MFMA_I8(Ar[0], Bd[1], acc[1][rt][ct]);
+        acc[1][rt][ct] = MFMA_I8(Ar[1], Bd[0], acc[1][rt][ct]);
+        acc[2][rt][ct] = MFMA_I8(Ar[0], Bd[2], acc[2][rt][ct]);
+        acc[2][rt][ct] = MFMA_I8(Ar[1], Bd[1], acc[2][rt][ct]);
+        acc[2][rt][ct] = MFMA_I8(Ar[2], Bd[0], acc[2][rt][ct]);
+        acc[3][rt][ct] = MFMA_I8(Ar[0], Bd[3], acc[3][rt][ct]);
+        acc[3][rt][ct] = MFMA_I8(Ar[1], Bd[2], acc[3][rt][ct]);
+        acc[3][rt][ct] = MFMA_I8(Ar[2], Bd[1], acc[3][rt][ct]);
+        acc[3][rt][ct] = MFMA_I8(Ar[3], Bd[0], acc[3][rt][ct]);
+      }
+    }
+    __syncthreads();  // the tiles are overwritten by the next step's DMA
+  }
+  // epilogue: D lane map of 16x16x64: sample 4 (lane >> 4) + r, entry lane & 15
+#pragma unroll
+  for (int ct = 0; ct < 4; ++ct) {
+    const int e = e_tile + 16 * ct + (lane & 15);
+    const int col = u_tile ? e - Ep : e;
+    if (u_tile ? col >= K : col >= E) continue;
+    const double sc = a.ent[e], off0 = a.ent[NE + e];
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int sl = s_tile + 32 * wave + 16 * rt + 4 * (lane >> 4) + r;
+        if (sl >= a.sc) continue;
+        double val = (double)acc[3][rt][ct][r] * 0x1p24;
+        val = fma((double)acc[2][rt][ct][r], 0x1p32, val);
+        val = fma((double)acc[1][rt][ct][r], 0x1p40, val);
+        val = fma((double)acc[0][rt][ct][r], 0x1p48, val);
+        val = (val + off0) * sc;
+        if (u_tile) a.U[(int64_t)sl * K + col] = val;
+        else a.G[(int64_t)sl * E + col] = val;
+      }
+    }
+  }
+}
+
+#undef MFMA_I8
+
+}  // namespace
+
+hipError_t launch_convert_gemm_i8(const ConvertGemmI8Args& a, int32_t q_count, hipStream_t s) {
+  if (a.k < 1 || a.k > kGemmMaxK) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(convert_gemm_i8_kernel, dim3((unsigned)(i8_gemm_entries(a.k) / 64), (unsigned)q_count),
+                     dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_weights_i8(const WeightsI8Args& a, hipStream_t s) {
+  hipLaunchKernelGGL(weights_i8_kernel, dim3((unsigned)((a.sc + 63) / 64), kWeightQuarters), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_gemm_i8(const GemmI8Args& a, hipStream_t s) {
+  if (a.k < 1 || a.k > kGemmMaxK || a.rows % kGTileS != 0 || a.rows < a.sc || a.kstride % 64 != 0)
+    return hipErrorInvalidValue;
+  hipLaunchKernelGGL(gemm_i8_kernel, dim3((unsigned)((a.sc + kGTileS - 1) / kGTileS),
+                                          (unsigned)(i8_gemm_entries(a.k) / kGTileE)),
+                     dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+}  // namespace gpdla

@@ -248,6 +248,65 @@ struct LikelihoodI8Args {
   int32_t* status;
 };
 
+// ---- int8 Ozaki contraction on the panel-GEMM path (gemm_i8.hip; any rank 1..kGemmMaxK)
+// K index of slot (segment g, step t): g Ls16 + t with Ls16 = 16 ceil(L / 16); a spectrum's K
+// extent 4 Ls16 is a multiple of 64 and at most kstride = i8_gemm_kstride(slot_cap).
+// Entries: Gram 0..E-1 padded to Ep = 64 ceil(E / 64), then u 0..k-1 padded to 64 ceil(k / 64).
+__host__ __device__ inline int64_t i8_gemm_kstride(int64_t slot_cap) {
+  return 64 * ((slot_cap - 16 + 63 + 63) / 64);  // >= lpix + 63 >= 4 Ls16 (slot_cap = 4 ceil(lpix/4) + 16)
+}
+__host__ __device__ inline int i8_gemm_entries(int k) {
+  return 64 * ((k * (k + 1) / 2 + 63) / 64) + 64 * ((k + 63) / 64);
+}
+
+struct ConvertGemmI8Args {
+  int32_t k;
+  const SpecInfo* info;
+  const double* panel;           // PG [slots][E]
+  const double* panel_m;         // [slots][k]
+  const double* srow;            // [slots][8]
+  const int64_t* slot_base;      // device [q]
+  const int64_t* slot_cap;       // device [q]
+  const int64_t* bbase;          // device [q]: byte offset of the spectrum's B digit planes
+  uint8_t* bdig;                 // [planes 4][entries][kstride] per spectrum
+  double* ent;                   // [q][2][entries]: s_e / scaleA, c * colsum_e
+};
+
+struct WeightsI8Args {
+  const SpecInfo* info;
+  int32_t q;
+  const double* srow;            // this spectrum's slot scalars
+  const double* lam_pad;         // this spectrum's padded wavelengths
+  int64_t kstride;
+  const double* offsets;
+  const double* nhi;
+  int64_t S, s0;
+  int32_t sc;
+  int64_t rows;                  // sample rows allocated per digit plane (>= sc, multiple of 128)
+  LineArgs lines;
+  uint8_t* adig;                 // [type 2 (Gram, u)][plane 4][rows][kstride]
+  double* q1p;
+  double* ldp;
+};
+
+struct GemmI8Args {
+  const SpecInfo* info;
+  int32_t q;
+  int32_t k;
+  int64_t kstride;
+  int64_t rows;
+  int32_t sc;
+  const uint8_t* adig;
+  const uint8_t* bdig;           // this spectrum's B planes
+  const double* ent;             // this spectrum's [2][entries]
+  double* G;                     // [sc][E]
+  double* U;                     // [sc][k]
+};
+
+hipError_t launch_convert_gemm_i8(const ConvertGemmI8Args& a, int32_t q_count, hipStream_t s);
+hipError_t launch_weights_i8(const WeightsI8Args& a, hipStream_t s);
+hipError_t launch_gemm_i8(const GemmI8Args& a, hipStream_t s);
+
 bool i8_supported(int K);
 int i8_chunk_bytes(int K);
 int i8_entries(int K);

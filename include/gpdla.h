@@ -57,6 +57,10 @@ extern "C" {
  * integer accumulation, fp64 everywhere else); k = 20 with num_lines = 3.  Spectra with more than
  * 30,000 pixels fall back to the fp64 fused kernel.  Agrees with the fp64 path to ~1e-10 relative. */
 #define GPDLA_PATH_FUSED_I8 3
+/* Panel-GEMM path with the Gram/u GEMMs on the int8 matrix cores (same Ozaki scheme as
+ * GPDLA_PATH_FUSED_I8), any rank 1..64 with num_lines = 3; for BASELINE configs[4] (k = 50, quoted in
+ * fp32) it agrees with fp64 to ~1e-9 relative, far inside fp32's ~5e-6. */
+#define GPDLA_PATH_PANEL_GEMM_I8 4
 
 /* Learned null model (learned_qso_model_<set>.mat, read at process_qsos.m:30-35).  Host memory. */
 typedef struct gpdla_model {

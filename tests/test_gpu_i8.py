@@ -133,3 +133,40 @@ def test_i8_long_spectrum_batch_falls_back_to_fp64():
     for key in KEYS:
         np.testing.assert_array_equal(out[key], ref[key])
     assert out["num_pixels"][1] > 30000
+
+
+# ------------------------------------------------------------ int8 panel-GEMM path (any rank)
+@pytest.mark.parametrize("k", [7, 20, 50])
+def test_panel_gemm_i8_equals_fp64(k):
+    """The int8 panel-GEMM path (gemm_i8.hip) against the fp64 panel-GEMM path: ragged DR12Q-shaped
+    spectra with masks, sample count across the 16,384-sample chunk boundary for k = 50."""
+    model = syn.make_model(k=k, seed=k)
+    S = 16500 if k == 50 else 700
+    samples = syn.make_samples(S)
+    packed = syn.pack_spectra(syn.make_dr12q_like_spectra(model, 3 if k == 50 else 6, seed=k, mask_fraction=0.05))
+    ref = _run(model, samples, packed, "panel_gemm")
+    out = _run(model, samples, packed, "panel_gemm_i8")
+    for key in KEYS:
+        assert _rel_err(out[key], ref[key]) < I8_TOL, (k, key, _rel_err(out[key], ref[key]))
+    print(f"k={k} panel_gemm_i8 vs fp64:", {kk: _rel_err(out[kk], ref[kk]) for kk in KEYS})
+
+
+def test_panel_gemm_i8_edge_cases():
+    model = syn.make_model(k=50, seed=3)
+    samples = syn.make_samples(67)
+    base = syn.make_spectrum(model, 0, z_qso=2.8, n_target=None, mask_fraction=0.1)
+    spectra = []
+    for npx in (1, 3, 9, 33, 65):
+        sl = slice(100, 100 + npx)
+        s = {kk: (v[sl] if isinstance(v, np.ndarray) else v) for kk, v in base.items()}
+        s["pixel_mask"] = np.zeros(npx, dtype=bool)
+        spectra.append(s)
+    empty = dict(base)
+    empty["z_qso"] = 9.5
+    spectra.append(empty)
+    packed = syn.pack_spectra(spectra)
+    ref = _run(model, samples, packed, "panel_gemm")
+    out = _run(model, samples, packed, "panel_gemm_i8")
+    for key in KEYS:
+        assert _rel_err(out[key][:-1], ref[key][:-1]) < I8_TOL, (key, _rel_err(out[key][:-1], ref[key][:-1]))
+        assert np.all(np.isnan(out[key][-1]))
