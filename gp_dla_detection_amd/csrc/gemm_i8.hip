@@ -411,9 +411,8 @@ hipError_t launch_weights_i8(const WeightsI8Args& a, hipStream_t s) {
 hipError_t launch_gemm_i8(const GemmI8Args& a, hipStream_t s) {
   if (a.k < 1 || a.k > kGemmMaxK || a.rows % kGTileS != 0 || a.rows < a.sc || a.kstride % 64 != 0)
     return hipErrorInvalidValue;
-  hipLaunchKernelGGL(gemm_i8_kernel, dim3((unsigned)((a.sc + kGTileS - 1) / kGTileS),
-                                          (unsigned)(i8_gemm_entries(a.k) / kGTileE)),
-                     dim3(256), 0, s, a);
+  const dim3 grid((unsigned)((a.sc + kGTileS - 1) / kGTileS), (unsigned)(i8_gemm_entries(a.k) / kGTileE));
+  hipLaunchKernelGGL(gemm_i8_kernel, grid, dim3(256), 0, s, a);
   return hipGetLastError();
 }
 
