@@ -139,7 +139,9 @@ __global__ __launch_bounds__(256) void weights_i8_kernel(WeightsI8Args a) {
   double q1 = 0.0, pm = 1.0;
   int pe = 0;
   const int64_t plane = a.rows * a.kstride;
-  uint8_t* ag = a.adig + (int64_t)sl * a.kstride + (int64_t)g * Ls16;
+  // A planes are stored [16-slot group][sample][16 B]: a lane's 16-byte store per group sits next to
+  // its neighbours' (coalesced rows of 1 KiB per wave)
+  uint8_t* ag = a.adig + (int64_t)sl * 16 + (int64_t)(g * Ls16 / 16) * a.rows * 16;
   uint8_t* au = ag + 4 * plane;
   for (int tg = t0; tg < t1; tg += 16) {
 #if GPDLA_WI8_STAGED
@@ -257,8 +259,8 @@ __global__ __launch_bounds__(256) void weights_i8_kernel(WeightsI8Args a) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const v4i dg = digit_plane(xg, i), du = digit_plane(xu, i);
-        *reinterpret_cast<v4i*>(ag + i * plane + (tg - 0)) = dg;
-        *reinterpret_cast<v4i*>(au + i * plane + (tg - 0)) = du;
+        *reinterpret_cast<v4i*>(ag + i * plane + (int64_t)(tg / 16) * a.rows * 16) = dg;
+        *reinterpret_cast<v4i*>(au + i * plane + (int64_t)(tg / 16) * a.rows * 16) = du;
       }
     }
   }
@@ -301,7 +303,7 @@ __global__ __launch_bounds__(256, 2) void gemm_i8_kernel(GemmI8Args a) {
   const bool u_tile = e_tile >= Ep;
   const int nks = (16 * ((inf.L + 15) / 16)) / 16;  // 4 Ls16 / 64
   const int64_t planeA = a.rows * a.kstride, planeB = (int64_t)NE * a.kstride;
-  const uint8_t* A0 = a.adig + (u_tile ? 4 * planeA : 0) + (int64_t)s_tile * a.kstride;
+  const uint8_t* A0 = a.adig + (u_tile ? 4 * planeA : 0) + (int64_t)s_tile * 16;
   const uint8_t* B0 = a.bdig + (int64_t)e_tile * a.kstride;
   const uint32_t as_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)As;
   const uint32_t bs_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)Bs;
@@ -322,7 +324,7 @@ __global__ __launch_bounds__(256, 2) void gemm_i8_kernel(GemmI8Args a) {
     for (int i = 0; i < 8; ++i) {
       const int piece = wave_s * 8 + i;
       const int p = piece >> 3, row = (piece & 7) * 16 + prow;
-      const uint32_t voffset = (uint32_t)((int64_t)row * a.kstride + ks * 64 + 16 * ((lane & 3) ^ ((row >> 2) & 3)));
+      const uint32_t voffset = (uint32_t)((int64_t)(ks * 4 + ((lane & 3) ^ ((row >> 2) & 3))) * a.rows * 16 + row * 16);
       dma_piece(A0 + p * planeA, voffset, as_base + (uint32_t)(piece * 1024));
     }
     // B: 16 pieces (plane p = piece / 4, entries 16 (piece % 4) ..), 4 per wave
