@@ -22,6 +22,9 @@ namespace gpdla {
 namespace {
 
 #define MFMA_I8(A, B, C) __builtin_amdgcn_mfma_i32_16x16x64_i8((A), (B), (C), 0, 0, 0)
+#ifndef GPDLA_GEMM_I8_REGPF
+#define GPDLA_GEMM_I8_REGPF 1
+#endif
 #ifndef GPDLA_WI8_STAGED
 #define GPDLA_WI8_STAGED 0
 #endif
@@ -318,6 +321,35 @@ __global__ __launch_bounds__(256, 2) void gemm_i8_kernel(GemmI8Args a) {
 #pragma unroll
       for (int ct = 0; ct < 4; ++ct) acc[l][rt][ct] = (v4i){0, 0, 0, 0};
   const int g = lane >> 4;
+#if GPDLA_GEMM_I8_REGPF
+  // register prefetch: each wave loads its 12 pieces of step ks + 1 into VGPRs while step ks's
+  // MFMAs run, then stores them to LDS after the barrier (double buffering without a second tile)
+  auto load_pieces = [&](int ks, v4i (&reg)[12]) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int piece = wave_s * 8 + i;
+      const int p = piece >> 3, row = (piece & 7) * 16 + prow;
+      const int64_t off = (int64_t)(ks * 4 + ((lane & 3) ^ ((row >> 2) & 3))) * a.rows * 16 + row * 16;
+      reg[i] = *reinterpret_cast<const v4i*>(A0 + p * planeA + off);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int piece = wave_s * 4 + i;
+      const int p = piece >> 2, row = (piece & 3) * 16 + prow;
+      const int64_t off = (int64_t)row * a.kstride + ks * 64 + 16 * ((lane & 3) ^ ((row >> 2) & 3));
+      reg[8 + i] = *reinterpret_cast<const v4i*>(B0 + p * planeB + off);
+    }
+  };
+  v4i pf[12];
+  load_pieces(0, pf);
+  for (int ks = 0; ks < nks; ++ks) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) *reinterpret_cast<v4i*>(As + (wave_s * 8 + i) * 1024 + lane * 16) = pf[i];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) *reinterpret_cast<v4i*>(Bs + (wave_s * 4 + i) * 1024 + lane * 16) = pf[8 + i];
+    __syncthreads();
+    if (ks + 1 < nks) load_pieces(ks + 1, pf);
+#else
   for (int ks = 0; ks < nks; ++ks) {
     // A: 32 pieces (plane p = piece / 8, rows 16 (piece % 8) ..), 8 per wave
 #pragma unroll
@@ -337,6 +369,7 @@ __global__ __launch_bounds__(256, 2) void gemm_i8_kernel(GemmI8Args a) {
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+#endif
     v4i Ad[2][4];
 #pragma unroll
     for (int rt = 0; rt < 2; ++rt) {

@@ -19,6 +19,8 @@ VARIANTS = {
     "far0": dict(GPDLA_FAR_WING=0),
     "i8pipe1": dict(I8_PIPELINE=1),
     "i8pipe0": dict(I8_PIPELINE=0),
+    "gemm_pf1": dict(GPDLA_GEMM_I8_REGPF=1),
+    "gemm_pf0": dict(GPDLA_GEMM_I8_REGPF=0),
 }
 if __name__ == "__main__":
     names = sys.argv[1:] or list(VARIANTS)
