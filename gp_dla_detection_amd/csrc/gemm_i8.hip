@@ -25,9 +25,6 @@ namespace {
 #ifndef GPDLA_GEMM_I8_REGPF
 #define GPDLA_GEMM_I8_REGPF 1
 #endif
-#ifndef GPDLA_WI8_STAGED
-#define GPDLA_WI8_STAGED 0
-#endif
 
 // --------------------------------------------------------------------------------------------
 // convert: grid (entries / 64, spectra), 256 threads = 64 entries x 4 segments
@@ -147,78 +144,6 @@ __global__ __launch_bounds__(256) void weights_i8_kernel(WeightsI8Args a) {
   uint8_t* ag = a.adig + (int64_t)sl * 16 + (int64_t)(g * Ls16 / 16) * a.rows * 16;
   uint8_t* au = ag + 4 * plane;
   for (int tg = t0; tg < t1; tg += 16) {
-#if GPDLA_WI8_STAGED
-    // (1) branch-free damping wings of the group's 16 slots (one shared reciprocal per slot),
-    // (2) rare core fix-up, (3) table exps, (4) convolution, pixel terms, quantised weights --
-    // the staging of likelihood_i8_kernel (kernels_i8.hip), here with lanes = samples
-    double lamv[16], tot[16];
-    uint32_t cm = 0;
-#pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      const int t = tg + e;
-      lamv[e] = t < L ? a.srow[((int64_t)g * Ls + t) * 8] : a.lam_pad[(int64_t)g * L + t + 2 * kWidth];
-    }
-#pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      const double x0 = fma(lamv[e], afac[0], -kC2), x1 = fma(lamv[e], afac[1], -kC2),
-                   x2 = fma(lamv[e], afac[2], -kC2);
-      cm |= (((fabs(x0) < kCoreX) | (fabs(x1) < kCoreX) | (fabs(x2) < kCoreX)) ? 1u : 0u) << e;
-      double T0, T1, T2;
-      wing_T3(x0, x1, x2, T0, T1, T2);
-      double t = 0.0;
-      t -= wing_poly(wing_lds, T0);
-      t -= wing_poly(wing_lds + kWingStride, T1);
-      t -= wing_poly(wing_lds + 2 * kWingStride, T2);
-      tot[e] = t;
-    }
-    if (cm) {
-#pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        if (cm & (1u << e)) {
-          double t = 0.0;
-#pragma unroll
-          for (int j = 0; j < 3; ++j) {
-            const double x = fma(lamv[e], afac[j], -kC2);
-            const double ax = fabs(x);
-            double f = wing_eval(wing_lds + j * kWingStride, x);
-            if (ax < kCoreX) f = core_eval(core_lds + j * kCoreTable, ax);
-            t -= f;
-          }
-          tot[e] = t;
-        }
-      }
-    }
-#pragma unroll
-    for (int e = 0; e < 16; ++e) tot[e] = exp_tab64(N * tot[e], exp_lds);  // voigt.c:291
-    uint32_t xg[16], xu[16];
-#pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      const int t = tg + e;
-      double y = 0.0, noise = 1.0, mu = 0.0, om2 = 0.0;  // neutral past the segment
-      if (t < L) {
-        const double* sr = a.srow + ((int64_t)g * Ls + t) * 8;
-        y = sr[1]; noise = sr[2]; mu = sr[3]; om2 = sr[4];
-      }
-      const double w6 = tot[e];
-      double ab = w0 * kInstrumentProfile[0];  // voigt.c:297-299
-      ab = fma(w1, kInstrumentProfile[1], ab);
-      ab = fma(w2, kInstrumentProfile[2], ab);
-      ab = fma(w3, kInstrumentProfile[3], ab);
-      ab = fma(w4, kInstrumentProfile[4], ab);
-      ab = fma(w5, kInstrumentProfile[5], ab);
-      ab = fma(w6, kInstrumentProfile[6], ab);
-      w0 = w1; w1 = w2; w2 = w3; w3 = w4; w4 = w5; w5 = w6;
-      const double r = fma(-mu, ab, y);  // process_qsos.m:191-197, log_mvnpdf_low_rank.m:11-15
-      const double a2 = ab * ab;
-      const double d = fma(om2, a2, noise);
-      const double dinv = rcp_sweep(d);
-      const double rd = r * dinv;
-      q1 = fma(r, rd, q1);
-      pm *= d;
-      xg[e] = (uint32_t)__builtin_rint(a2 * dinv * ((om2 + noise) * kI8ScaleG)) ^ 0x80808080u;
-      xu[e] = (uint32_t)__builtin_rint(fma(ab * rd, kI8ScaleU / u_bound(y, mu, noise), 0x1p31)) ^ 0x80808080u;
-    }
-#else
     // per slot as the fp64 weights kernel (its core branch is coherent: a block's 64 samples are
     // consecutive in z), 16 slots' quantised weights collected for the digit planes
     uint32_t xg[16], xu[16];
@@ -252,7 +177,6 @@ __global__ __launch_bounds__(256) void weights_i8_kernel(WeightsI8Args a) {
       xu[e] = (uint32_t)__builtin_rint(fma(ab * rd, kI8ScaleU / u_bound(y, mu, noise), 0x1p31)) ^ 0x80808080u;
       asm volatile("" : "+v"(xg[e]), "+v"(xu[e]), "+v"(q1), "+v"(pm));  // no sinking across slots
     }
-#endif
     {
       int ex;
       pm = frexp(pm, &ex);

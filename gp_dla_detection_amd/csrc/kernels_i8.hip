@@ -22,9 +22,6 @@ namespace gpdla {
 namespace {
 
 constexpr int kI8Levels = 4;
-#ifndef I8_SLOT_FENCE
-#define I8_SLOT_FENCE 0
-#endif
 #ifndef I8_PIPELINE
 #define I8_PIPELINE 1
 #endif  // digit levels i + j = 0..3 kept (10 of the 16 pairs)
@@ -422,9 +419,6 @@ __global__ __launch_bounds__(256, 1) void likelihood_i8_kernel(LikelihoodI8Args 
       pm *= d;
       xg[e] = (uint32_t)__builtin_rint(wg * gs) ^ 0x80808080u;
       xu[e] = (uint32_t)__builtin_rint(fma(wu, us, 0x1p31)) ^ 0x80808080u;
-#if I8_SLOT_FENCE
-      asm volatile("" : "+v"(xg[e]), "+v"(xu[e]), "+v"(q1), "+v"(pm));
-#endif
     }
     {
       int ex;
