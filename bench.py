@@ -302,6 +302,8 @@ def main():
     eff_gbs = effective_bytes_per_eval(n_mean, args.k) * evals_per_launch / (avg_ms * 1e-3) / 1e9
 
     traffic, traffic_src = profiled_traffic(Q, S, args.k, path)
+    # batched LDL^T kernel of the panel paths (gemm_path.hip launch_ldl_batch)
+    ldl_name = "ldl_cyc_kernel" if args.k >= 32 else "ldl_reg_kernel"
     result = {
         "metric": "(spectrum x DLA-sample) log-evidence evals/sec",
         "value": value,
@@ -325,8 +327,8 @@ def main():
                      "traffic_source": traffic_src,
                      "kernel": {"fused": f"likelihood_kernel<{args.k}>",
                                 "fused-int8": f"likelihood_i8_kernel<{args.k}>",
-                                "panel-GEMM-int8": "weights_i8_kernel + gemm_i8_kernel + ldl_reg_kernel (per batch)"}.get(
-                                    path, "weights_kernel + rocBLAS dgemm + ldl_reg_kernel (per batch)"),
+                                "panel-GEMM-int8": f"weights_i8_kernel + gemm_i8_kernel + {ldl_name} (per batch)"}.get(
+                                    path, f"weights_kernel + rocBLAS dgemm + {ldl_name} (per batch)"),
                      "avg_launch_ms": avg_ms,
                      "flops_per_eval": algorithmic_flops_per_eval(n_mean, args.k),
                      "evals_per_launch": evals_per_launch},

@@ -42,6 +42,9 @@
 #ifndef GPDLA_LDL_REGISTERS
 #define GPDLA_LDL_REGISTERS 1
 #endif
+#ifndef GPDLA_LDL_CYCLIC
+#define GPDLA_LDL_CYCLIC 1
+#endif
 
 namespace gpdla {
 

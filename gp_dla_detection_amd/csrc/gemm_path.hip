@@ -315,6 +315,128 @@ __global__ __launch_bounds__(256) void ldl_reg_kernel(LdlArgs a) {
   emit(ll);
 }
 
+// 2-D block-cyclic form of the same augmented LDL^T for the larger ranks (k + 1 <= 8 NS, NS =
+// ceil((KMAX + 1) / 8)): one wave per sample, lane (ra, cb) = (lane >> 3, lane & 7) holds
+// A(ra + 8r, cb + 8c) for the register slots r >= c -- every lower-triangle entry exactly once,
+// plus upper entries in the diagonal slots that are never read.  At pivot p the 8 lanes of
+// column class p & 7 publish column p (rows > p; rows <= p as zeros) to a 64-double LDS line;
+// every lane reads its row and column multipliers from that line (8 distinct addresses per read,
+// consecutive doubles: conflict-free) and updates its live slots r >= c >= p / 8.  Slot blocks
+// left of the pivot are skipped at compile time, so a lane issues ~Σ_p (NS - p/8)(NS - p/8 + 1)/2
+// FMAs (666 at k = 50) where the lane-per-column form issues Σ_p (KB - 1 - p) (1,325), and all 64
+// lanes hold live entries until the last column block.
+template <int KMAX>
+__global__ __launch_bounds__(256) void ldl_cyc_kernel(LdlArgs a) {
+  constexpr int NS = (KMAX + 1 + 7) / 8;
+  constexpr int N8 = 8 * NS;
+  constexpr int kStage = KMAX * (KMAX + 1) / 2 + KMAX;  // packed Gram + u of the largest rank
+  __shared__ __attribute__((aligned(16))) double colp_all[4][2][N8];  // double-buffered by pivot parity
+  __shared__ __attribute__((aligned(16))) double stage_all[4][kStage];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  double* stage = stage_all[wave];
+  const int sl = blockIdx.x * 4 + wave;
+  if (sl >= a.sc) return;  // wave-uniform
+  const int K = a.k;
+  const int64_t s = a.s0 + sl;
+  const SpecInfo inf = a.info[a.q];
+  auto emit = [&](double ll) {
+    if (lane != 0) return;
+    if (s == a.S) *a.ll_null = ll;
+    else if (a.sample_ll) a.sample_ll[a.perm[s]] = ll;
+  };
+  if (inf.J == 0) {
+    emit(NAN);
+    return;
+  }
+  const int64_t E = (int64_t)K * (K + 1) / 2;
+  const double* Gs = a.G + (int64_t)sl * E;
+  const double* Us = a.U + (int64_t)sl * K;
+  const double* q = a.q1p + (int64_t)sl * kWeightParts;
+  const double* l4 = a.ldp + (int64_t)sl * kWeightParts;
+  {  // coalesced copy of the packed Gram and u into this wave's LDS slice (all loads in flight first)
+    constexpr int kIt = (kStage + 63) / 64;
+    double tmp[kIt];
+#pragma unroll
+    for (int it = 0; it < kIt; ++it) {
+      const int t = it * 64 + lane;
+      tmp[it] = t < E ? Gs[t] : (t < E + K ? Us[t - E] : 0.0);
+    }
+#pragma unroll
+    for (int it = 0; it < kIt; ++it) {
+      const int t = it * 64 + lane;
+      if (t < E + K) stage[t] = tmp[it];
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  const int ra = lane >> 3, cb = lane & 7;
+  double A[NS][NS];
+#pragma unroll
+  for (int r = 0; r < NS; ++r) {
+#pragma unroll
+    for (int c = 0; c <= r; ++c) {
+      const int i = ra + 8 * r, j = cb + 8 * c;
+      double v = 0.0;
+      if (i <= K && j <= K && i >= j) {
+        if (i < K) v = stage[j * K - j * (j - 1) / 2 + (i - j)] + (i == j ? 1.0 : 0.0);  // B = I + Gram
+        else if (j < K) v = stage[E + j];                                                  // row k: u'
+        else v = sum_parts(q);                                                             // sum r^2 / d
+      }
+      A[r][c] = v;
+    }
+  }
+  double pb = 1.0;  // prod D_p = pb 2^eb (frexp-renormalised, one log at the end)
+  int eb = 0;
+  bool bad = false;
+  // column blocks unrolled (register slots compile-time per block), the 8 pivots of a block not
+#pragma unroll
+  for (int c0 = 0; c0 < NS; ++c0) {
+#pragma unroll 1
+    for (int pp = 0; pp < 8; ++pp) {
+      const int p = 8 * c0 + pp;
+      if (p >= K) break;
+      double* colp = colp_all[wave][p & 1];
+      if (cb == pp) {  // column p: rows ra + 8r, r >= c0; rows <= p published as zeros
+#pragma unroll
+        for (int r = c0; r < NS; ++r) colp[ra + 8 * r] = (r > c0 || ra + 8 * r > p) ? A[r][c0] : 0.0;
+      }
+      __builtin_amdgcn_wave_barrier();
+      const double d = readlane_d(A[c0][c0], (pp << 3) | pp);  // A(p, p)
+      bad |= !(d > 0.0);
+      pb *= d;
+      if ((p & 3) == 3) {
+        int ex;
+        pb = frexp(pb, &ex);
+        eb += ex;
+      }
+      const double invd = rcp_nr(d);
+      double R[NS], F[NS];
+#pragma unroll
+      for (int r = c0; r < NS; ++r) {
+        R[r] = colp[ra + 8 * r];          // A(i, p), zero for i <= p
+        F[r] = colp[cb + 8 * r] * invd;   // A(j, p) / D_p, zero for j <= p
+      }
+#pragma unroll
+      for (int r = c0; r < NS; ++r) {
+#pragma unroll
+        for (int c = c0; c <= r; ++c) A[r][c] = fma(-R[r], F[c], A[r][c]);  // A(i,j) -= A(i,p) A(j,p) / D_p
+      }
+    }
+  }
+  double diag = 0.0;  // A(k, k) = r'D^-1 r - u'B^-1 u, at lane (k & 7, k & 7), slot (k / 8, k / 8)
+#pragma unroll
+  for (int r = 0; r < NS; ++r)
+    if (r == (K >> 3)) diag = A[r][r];
+  const double quad = readlane_d(diag, ((K & 7) << 3) | (K & 7));
+  const double logdet_d = sum_parts(l4);
+  const double logdet_b = log(pb) + eb * kLn2;
+  double ll = -0.5 * (quad + (logdet_d + logdet_b) + inf.n * kLog2Pi);  // log_mvnpdf_low_rank.m:30-32
+  if (bad || !(fabs(ll) < INFINITY)) {
+    ll = NAN;
+    if (lane == 0) atomicOr(a.status, 1);
+  }
+  emit(ll);
+}
+
 }  // namespace
 
 hipError_t launch_weights(const WeightsArgs& a, hipStream_t s) {
@@ -329,6 +451,17 @@ hipError_t launch_weights(const WeightsArgs& a, hipStream_t s) {
 hipError_t launch_ldl_batch(const LdlArgs& a, hipStream_t s) {
   if (a.k < 1 || a.k > kGemmMaxK) return hipErrorInvalidValue;
   const dim3 grid((unsigned)((a.sc + 3) / 4)), blk(256);
+#if GPDLA_LDL_CYCLIC
+  // 2-D block-cyclic register path for k >= 32 (configs[4]: k = 50)
+  if (a.k >= 32 && a.k <= 63) {
+    if (a.k <= 39) hipLaunchKernelGGL(ldl_cyc_kernel<39>, grid, blk, 0, s, a);
+    else if (a.k <= 47) hipLaunchKernelGGL(ldl_cyc_kernel<47>, grid, blk, 0, s, a);
+    else if (a.k <= 51) hipLaunchKernelGGL(ldl_cyc_kernel<51>, grid, blk, 0, s, a);
+    else if (a.k <= 55) hipLaunchKernelGGL(ldl_cyc_kernel<55>, grid, blk, 0, s, a);
+    else hipLaunchKernelGGL(ldl_cyc_kernel<63>, grid, blk, 0, s, a);
+    return hipGetLastError();
+  }
+#endif
 #if GPDLA_LDL_REGISTERS
   // register path: column j of the augmented (k+1) x (k+1) matrix in lane j (k <= 63)
   if (a.k <= 15) hipLaunchKernelGGL(ldl_reg_kernel<16>, grid, blk, 0, s, a);

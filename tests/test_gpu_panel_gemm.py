@@ -73,6 +73,25 @@ def test_rank50_matches_oracle():
         assert _rel_err(out["log_likelihoods_dla"][q], ref["log_likelihood_dla"]) < 1e-9
 
 
+@pytest.mark.parametrize("k", [31, 32, 39, 40, 47, 48, 51, 52, 55, 56, 63])
+def test_high_rank_ldl_buckets_match_oracle(k):
+    """Every rank bucket of the batched LDL^T kernels around and above the block-cyclic switch at
+    k = 32 (buckets of ldl_cyc_kernel: k <= 39, 47, 51, 55, 63), fp64 and int8 panel paths."""
+    model = syn.make_model(k=k, seed=100 + k)
+    samples = syn.make_samples(40)
+    spectra = syn.make_dr12q_like_spectra(model, 2, seed=200 + k, mask_fraction=0.05)
+    refs = _oracle(spectra, model, samples)
+    for path, tol in (("panel_gemm", 1e-9), ("panel_gemm_i8", 1e-7)):
+        with Engine(model, samples, set_parameters(k=k), path=path) as eng:
+            out = eng.process(syn.pack_spectra(spectra))
+        for q, ref in enumerate(refs):
+            for key, rkey in (("sample_log_likelihoods_dla", "sample_log_likelihoods_dla"),
+                              ("log_likelihoods_no_dla", "log_likelihood_no_dla"),
+                              ("log_likelihoods_dla", "log_likelihood_dla")):
+                err = _rel_err(out[key][q], ref[rkey])
+                assert err < tol, (path, k, key, err)
+
+
 def test_sample_chunk_boundaries():
     """S + 1 = 16685 spans two 16384-sample chunks; compare with the fused path (k = 8)."""
     model = syn.make_model(k=8, seed=8)
