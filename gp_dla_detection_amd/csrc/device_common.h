@@ -45,6 +45,9 @@
 #ifndef GPDLA_LDL_CYCLIC
 #define GPDLA_LDL_CYCLIC 1
 #endif
+#ifndef GPDLA_LDL_GATHER
+#define GPDLA_LDL_GATHER 0
+#endif
 
 namespace gpdla {
 

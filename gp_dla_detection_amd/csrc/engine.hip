@@ -15,6 +15,11 @@
 #include "../../include/gpdla.h"
 #include "internal.h"
 
+// panel-GEMM paths: run the batched LDL^T on a second stream, overlapped with the next chunk
+#ifndef GPDLA_LDL_OVERLAP
+#define GPDLA_LDL_OVERLAP 1
+#endif
+
 using namespace gpdla;
 
 namespace {
@@ -109,6 +114,10 @@ struct gpdla_engine {
   gpdla_params params{};
   hipStream_t own_stream = nullptr;
   hipStream_t stream = nullptr;
+  // panel-GEMM paths: the batched LDL^T of sample chunk c runs on ldl_stream while the weights and
+  // GEMM of chunk c + 1 run on `stream` (Gram/u/partials double-buffered by chunk parity)
+  hipStream_t ldl_stream = nullptr;
+  hipEvent_t ev_prod[2] = {nullptr, nullptr}, ev_ldl[2] = {nullptr, nullptr};
 
   // resident model / samples / line data
   double *d_rest = nullptr, *d_mu = nullptr, *d_M = nullptr, *d_logom = nullptr;
@@ -240,6 +249,11 @@ void gpdla_engine_destroy(gpdla_engine* e) {
   if (e->h_meta) (void)hipHostFree(e->h_meta);
   if (e->blas) (void)rocblas_destroy_handle(e->blas);
   if (e->meta_done) (void)hipEventDestroy(e->meta_done);
+  for (int b = 0; b < 2; ++b) {
+    if (e->ev_prod[b]) (void)hipEventDestroy(e->ev_prod[b]);
+    if (e->ev_ldl[b]) (void)hipEventDestroy(e->ev_ldl[b]);
+  }
+  if (e->ldl_stream) (void)hipStreamDestroy(e->ldl_stream);
   if (e->own_stream) (void)hipStreamDestroy(e->own_stream);
   delete e;
 }
@@ -293,6 +307,14 @@ int gpdla_engine_create(int32_t device, const gpdla_model* model, const gpdla_sa
     return fail(set_error(GPDLA_EDEVICE, "hipEventCreate failed"));
   if (e->gemm && rocblas_create_handle(&e->blas) != rocblas_status_success)
     return fail(set_error(GPDLA_EDEVICE, "rocblas_create_handle failed"));
+  if (e->gemm && e->i8 && GPDLA_LDL_OVERLAP) {  // int8 path: +5.5%; dgemm path: -0.4% (A/B), off
+    if (hipStreamCreateWithFlags(&e->ldl_stream, hipStreamNonBlocking) != hipSuccess)
+      return fail(set_error(GPDLA_EDEVICE, "hipStreamCreate failed"));
+    for (int b = 0; b < 2; ++b)
+      if (hipEventCreateWithFlags(&e->ev_prod[b], hipEventDisableTiming) != hipSuccess ||
+          hipEventCreateWithFlags(&e->ev_ldl[b], hipEventDisableTiming) != hipSuccess)
+        return fail(set_error(GPDLA_EDEVICE, "hipEventCreate failed"));
+  }
 
   const size_t G = model->num_rest, K = model->k;
   std::vector<double> Mrow(G * K);
@@ -348,7 +370,10 @@ int gpdla_engine_set_stream(gpdla_engine* e, void* hip_stream) {
 }
 
 // Panel-GEMM path for one batch: per spectrum and chunk of samples, weights -> two dgemm ->
-// batched LDL^T (gemm_path.hip).  All on stream st, in order.
+// batched LDL^T (gemm_path.hip).  Weights and GEMM run on stream st in order; with an LDL stream
+// the LDL^T of chunk c runs there (after chunk c's GEMM) while st proceeds with chunk c + 1, the
+// chunk's Gram, u and partials in buffer c & 1 (chunk c + 2 waits for chunk c's LDL^T); st joins
+// the LDL stream at the end, so work queued on st afterwards sees every output.
 static int run_panel_gemm(gpdla_engine* e, int64_t nq, const int64_t* h_sb, const int64_t* h_lb,
                           const int64_t* h_cap, const int64_t* h_cb, int64_t sc_max, double* o_sll,
                           int64_t ld, double* o_null, hipStream_t st) {
@@ -357,9 +382,36 @@ static int run_panel_gemm(gpdla_engine* e, int64_t nq, const int64_t* h_sb, cons
   if (rocblas_set_stream(e->blas, st) != rocblas_status_success)
     return set_error(GPDLA_EDEVICE, "rocblas_set_stream failed");
   const double one = 1.0, zero = 0.0;
+  hipStream_t ls = e->ldl_stream ? e->ldl_stream : st;
+  int64_t chunk = 0;
+  double *G = e->d_G, *U = e->d_U, *q1p = e->d_q1p, *ldp = e->d_ldp;
+  // before the chunk's producers: pick its buffer, wait for the LDL^T that last read it
+  auto begin_chunk = [&]() -> hipError_t {
+    const int b = (int)(chunk & 1);
+    const int64_t sw = e->ldl_stream ? b : 0;
+    G = e->d_G + sw * E * sc_max; U = e->d_U + sw * K * sc_max;
+    q1p = e->d_q1p + sw * kWeightParts * sc_max; ldp = e->d_ldp + sw * kWeightParts * sc_max;
+    if (e->ldl_stream && chunk >= 2) return hipStreamWaitEvent(st, e->ev_ldl[b], 0);
+    return hipSuccess;
+  };
+  // after the chunk's producers: hand the chunk to the LDL stream
+  auto to_ldl = [&]() -> hipError_t {
+    if (!e->ldl_stream) return hipSuccess;
+    const int b = (int)(chunk & 1);
+    hipError_t r = hipEventRecord(e->ev_prod[b], st);
+    if (r == hipSuccess) r = hipStreamWaitEvent(ls, e->ev_prod[b], 0);
+    return r;
+  };
+  auto end_chunk = [&]() -> hipError_t {
+    hipError_t r = hipSuccess;
+    if (e->ldl_stream) r = hipEventRecord(e->ev_ldl[chunk & 1], ls);
+    ++chunk;
+    return r;
+  };
   for (int64_t q = 0; q < nq; ++q) {
     for (int64_t s0 = 0; s0 <= e->S; s0 += sc_max) {
       const int32_t sc = (int32_t)std::min<int64_t>(sc_max, e->S + 1 - s0);
+      HIP_TRY(begin_chunk());
       if (e->i8) {  // int8 Ozaki contraction (gemm_i8.hip): weights digits -> exact GEMM -> Gram, u
         const int64_t ks = i8_gemm_kstride(h_cap[q]);
         const int64_t rows = (sc_max + 127) / 128 * 128;
@@ -367,19 +419,21 @@ static int run_panel_gemm(gpdla_engine* e, int64_t nq, const int64_t* h_sb, cons
         wi.info = e->d_info; wi.q = (int32_t)q;
         wi.srow = e->d_srow + h_sb[q] * 8; wi.lam_pad = e->d_lam + h_lb[q]; wi.kstride = ks;
         wi.offsets = e->d_off; wi.nhi = e->d_nhi; wi.S = e->S; wi.s0 = s0; wi.sc = sc; wi.rows = rows;
-        wi.lines = make_line_args(e->d_lines); wi.adig = e->d_ai8; wi.q1p = e->d_q1p; wi.ldp = e->d_ldp;
+        wi.lines = make_line_args(e->d_lines); wi.adig = e->d_ai8; wi.q1p = q1p; wi.ldp = ldp;
         HIP_TRY(launch_weights_i8(wi, st));
         GemmI8Args gi{};
         gi.info = e->d_info; gi.q = (int32_t)q; gi.k = K; gi.kstride = ks; gi.rows = rows; gi.sc = sc;
         gi.adig = e->d_ai8; gi.bdig = e->d_pi8 + h_cb[q];
-        gi.ent = e->d_pent + q * 2 * (int64_t)i8_gemm_entries(K); gi.G = e->d_G; gi.U = e->d_U;
+        gi.ent = e->d_pent + q * 2 * (int64_t)i8_gemm_entries(K); gi.G = G; gi.U = U;
         HIP_TRY(launch_gemm_i8(gi, st));
+        HIP_TRY(to_ldl());
         LdlArgs da{};
         da.info = e->d_info; da.q = (int32_t)q; da.k = K;
-        da.G = e->d_G; da.U = e->d_U; da.q1p = e->d_q1p; da.ldp = e->d_ldp;
+        da.G = G; da.U = U; da.q1p = q1p; da.ldp = ldp;
         da.S = e->S; da.s0 = s0; da.sc = sc; da.perm = e->d_perm;
         da.sample_ll = o_sll ? o_sll + q * ld : nullptr; da.ll_null = o_null + q; da.status = e->d_status;
-        HIP_TRY(launch_ldl_batch(da, st));
+        HIP_TRY(launch_ldl_batch(da, ls));
+        HIP_TRY(end_chunk());
         continue;
       }
       WeightsArgs wa{};
@@ -387,26 +441,32 @@ static int run_panel_gemm(gpdla_engine* e, int64_t nq, const int64_t* h_sb, cons
       wa.srow = e->d_srow + h_sb[q] * 8; wa.lam_pad = e->d_lam + h_lb[q]; wa.cap = h_cap[q];
       wa.offsets = e->d_off; wa.nhi = e->d_nhi; wa.S = e->S; wa.s0 = s0; wa.sc = sc;
       wa.num_lines = e->params.num_lines; wa.lines = make_line_args(e->d_lines);
-      wa.wg = e->d_wg; wa.wu = e->d_wu; wa.q1p = e->d_q1p; wa.ldp = e->d_ldp;
+      wa.wg = e->d_wg; wa.wu = e->d_wu; wa.q1p = q1p; wa.ldp = ldp;
       HIP_TRY(launch_weights(wa, st));
       // Gram (E x sc) = PG (E x cap, the slot-major Khatri-Rao rows) * Wg^T (Wg stored [cap][sc])
       rocblas_status bs = rocblas_dgemm(e->blas, rocblas_operation_none, rocblas_operation_transpose,
                                         (rocblas_int)E, sc, (rocblas_int)h_cap[q], &one,
                                         e->d_panel + h_sb[q] * E, (rocblas_int)E, e->d_wg, sc, &zero,
-                                        e->d_G, (rocblas_int)E);
+                                        G, (rocblas_int)E);
       if (bs == rocblas_status_success)
         bs = rocblas_dgemm(e->blas, rocblas_operation_none, rocblas_operation_transpose, K, sc,
                            (rocblas_int)h_cap[q], &one, e->d_pm + h_sb[q] * K, K, e->d_wu, sc, &zero,
-                           e->d_U, K);
+                           U, K);
       if (bs != rocblas_status_success)
         return set_error(GPDLA_EDEVICE, "rocblas_dgemm failed: %s", rocblas_status_to_string(bs));
+      HIP_TRY(to_ldl());
       LdlArgs da{};
       da.info = e->d_info; da.q = (int32_t)q; da.k = K;
-      da.G = e->d_G; da.U = e->d_U; da.q1p = e->d_q1p; da.ldp = e->d_ldp;
+      da.G = G; da.U = U; da.q1p = q1p; da.ldp = ldp;
       da.S = e->S; da.s0 = s0; da.sc = sc; da.perm = e->d_perm;
       da.sample_ll = o_sll ? o_sll + q * ld : nullptr; da.ll_null = o_null + q; da.status = e->d_status;
-      HIP_TRY(launch_ldl_batch(da, st));
+      HIP_TRY(launch_ldl_batch(da, ls));
+      HIP_TRY(end_chunk());
     }
+  }
+  if (e->ldl_stream && chunk > 0) {  // st joins the LDL stream
+    HIP_TRY(hipEventRecord(e->ev_ldl[(chunk - 1) & 1], ls));
+    HIP_TRY(hipStreamWaitEvent(st, e->ev_ldl[(chunk - 1) & 1], 0));
   }
   return GPDLA_OK;
 }
@@ -493,10 +553,11 @@ int gpdla_engine_process(gpdla_engine* e, const gpdla_spectra* sp, const gpdla_r
       if ((rc = grow(&e->d_srow, &e->cap_srow, (size_t)slots * 8))) return rc;
       if ((rc = grow(&e->d_wg, &e->cap_wg, (size_t)(cap_max * sc_max)))) return rc;
       if ((rc = grow(&e->d_wu, &e->cap_wu, (size_t)(cap_max * sc_max)))) return rc;
-      if ((rc = grow(&e->d_G, &e->cap_G, (size_t)(E * sc_max)))) return rc;
-      if ((rc = grow(&e->d_U, &e->cap_U, (size_t)(e->K * sc_max)))) return rc;
-      if ((rc = grow(&e->d_q1p, &e->cap_q1p, (size_t)(kWeightParts * sc_max)))) return rc;
-      if ((rc = grow(&e->d_ldp, &e->cap_ldp, (size_t)(kWeightParts * sc_max)))) return rc;
+      const size_t nbuf = e->ldl_stream ? 2 : 1;  // chunk-parity buffers when the LDL^T overlaps
+      if ((rc = grow(&e->d_G, &e->cap_G, nbuf * (size_t)(E * sc_max)))) return rc;
+      if ((rc = grow(&e->d_U, &e->cap_U, nbuf * (size_t)(e->K * sc_max)))) return rc;
+      if ((rc = grow(&e->d_q1p, &e->cap_q1p, nbuf * (size_t)(kWeightParts * sc_max)))) return rc;
+      if ((rc = grow(&e->d_ldp, &e->cap_ldp, nbuf * (size_t)(kWeightParts * sc_max)))) return rc;
     } else {
       if ((rc = grow(&e->d_scratch, &e->cap_scr, (size_t)blocks_x * nq * kSamplesPerBlock * es))) return rc;
     }

@@ -331,9 +331,13 @@ __global__ __launch_bounds__(256) void ldl_cyc_kernel(LdlArgs a) {
   constexpr int N8 = 8 * NS;
   constexpr int kStage = KMAX * (KMAX + 1) / 2 + KMAX;  // packed Gram + u of the largest rank
   __shared__ __attribute__((aligned(16))) double colp_all[4][2][N8];  // double-buffered by pivot parity
-  __shared__ __attribute__((aligned(16))) double stage_all[4][kStage];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#if !GPDLA_LDL_GATHER
+  __shared__ __attribute__((aligned(16))) double stage_all[4][kStage];
   double* stage = stage_all[wave];
+#else
+  (void)kStage;
+#endif
   const int sl = blockIdx.x * 4 + wave;
   if (sl >= a.sc) return;  // wave-uniform
   const int K = a.k;
@@ -353,6 +357,9 @@ __global__ __launch_bounds__(256) void ldl_cyc_kernel(LdlArgs a) {
   const double* Us = a.U + (int64_t)sl * K;
   const double* q = a.q1p + (int64_t)sl * kWeightParts;
   const double* l4 = a.ldp + (int64_t)sl * kWeightParts;
+#if GPDLA_LDL_GATHER
+  auto entry = [&](int64_t t) { return t < E ? Gs[t] : Us[t - E]; };
+#else
   {  // coalesced copy of the packed Gram and u into this wave's LDS slice (all loads in flight first)
     constexpr int kIt = (kStage + 63) / 64;
     double tmp[kIt];
@@ -368,6 +375,8 @@ __global__ __launch_bounds__(256) void ldl_cyc_kernel(LdlArgs a) {
     }
   }
   __builtin_amdgcn_wave_barrier();
+  auto entry = [&](int64_t t) { return stage[t]; };
+#endif
   const int ra = lane >> 3, cb = lane & 7;
   double A[NS][NS];
 #pragma unroll
@@ -377,8 +386,8 @@ __global__ __launch_bounds__(256) void ldl_cyc_kernel(LdlArgs a) {
       const int i = ra + 8 * r, j = cb + 8 * c;
       double v = 0.0;
       if (i <= K && j <= K && i >= j) {
-        if (i < K) v = stage[j * K - j * (j - 1) / 2 + (i - j)] + (i == j ? 1.0 : 0.0);  // B = I + Gram
-        else if (j < K) v = stage[E + j];                                                  // row k: u'
+        if (i < K) v = entry(j * K - j * (j - 1) / 2 + (i - j)) + (i == j ? 1.0 : 0.0);  // B = I + Gram
+        else if (j < K) v = entry(E + j);                                                  // row k: u'
         else v = sum_parts(q);                                                             // sum r^2 / d
       }
       A[r][c] = v;

@@ -21,6 +21,11 @@ VARIANTS = {
     "i8pipe0": dict(I8_PIPELINE=0),
     "gemm_pf1": dict(GPDLA_GEMM_I8_REGPF=1),
     "gemm_pf0": dict(GPDLA_GEMM_I8_REGPF=0),
+    "ldl_reg": dict(GPDLA_LDL_CYCLIC=0),
+    "ldl_cyc_stage": dict(GPDLA_LDL_CYCLIC=1, GPDLA_LDL_GATHER=0),
+    "ldl_cyc_gather": dict(GPDLA_LDL_CYCLIC=1, GPDLA_LDL_GATHER=1),
+    "ldl_ovl0": dict(GPDLA_LDL_OVERLAP=0),
+    "ldl_ovl1": dict(GPDLA_LDL_OVERLAP=1),
 }
 if __name__ == "__main__":
     names = sys.argv[1:] or list(VARIANTS)
