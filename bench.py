@@ -30,12 +30,19 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 FP64_PEAK_TFLOPS = 78.6     # MI355X FP64 (vector and matrix), datasheet
+I8_PEAK_TOPS = 5000.0       # MI355X dense int8 MFMA (2x the ~2.5 PF dense BF16 rate; MI355X_MICROARCH.md)
 HBM_PEAK_GBS = 8000.0       # MI355X HBM3E, datasheet
 
 
 def algorithmic_flops_per_eval(n: int, k: int) -> float:
     """packed Gram + projection + per-pixel scalars + Cholesky + solve."""
     return n * k * (k + 1) + 2 * n * k + 10 * n + k ** 3 / 3 + 2 * k ** 2
+
+
+def i8_ops_per_eval(n: float, k: int) -> float:
+    """int8 MFMA ops of the exact Gram/u contraction: 10 digit pairs
+    (levels <= 3) x n slots x (k(k+1)/2 Gram + k u entries), 2 ops per multiply-add."""
+    return 2 * 10 * n * (k * (k + 1) / 2 + k)
 
 
 def effective_bytes_per_eval(n: int, k: int, w: int = 8) -> float:
@@ -324,6 +331,18 @@ def main():
                    "likelihood_path": path, "parallelism": f"spectrum-shard x{world}"},
         "roofline": {"bound": "mfma", "achieved": achieved_tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved_tf / FP64_PEAK_TFLOPS, "traffic": traffic,
+                     **({} if path != "panel-GEMM-int8" else {
+                         # the contraction runs on the int8 matrix cores: price it against their
+                         # dense peak (2x BF16 per clock, MI355X_MICROARCH.md); the fp64-equivalent
+                         # TFLOP/s above is the algorithmic fp64 work / time and may exceed the FP64 peak
+                         "bound": "mfma-i8", "unit": "TOPS", "peak": I8_PEAK_TOPS,
+                         "achieved": i8_ops_per_eval(n_mean, args.k) * evals_per_launch / (avg_ms * 1e-3) / 1e12,
+                         "frac": i8_ops_per_eval(n_mean, args.k) * evals_per_launch / (avg_ms * 1e-3) / 1e12
+                                 / I8_PEAK_TOPS,
+                         "i8_ops_per_eval": i8_ops_per_eval(n_mean, args.k),
+                         "fp64_equivalent_tflops": achieved_tf,
+                         "note": "int8 ops over the whole batch time (weights + int8 GEMM + LDL^T overlapped); "
+                                 "gemm_i8_kernel alone runs ~3x this rate (profiles/r1l_summary.md)"}),
                      "traffic_source": traffic_src,
                      "kernel": {"fused": f"likelihood_kernel<{args.k}>",
                                 "fused-int8": f"likelihood_i8_kernel<{args.k}>",
