@@ -335,14 +335,14 @@ def main():
                          # the contraction runs on the int8 matrix cores: price it against their
                          # dense peak (2x BF16 per clock, MI355X_MICROARCH.md); the fp64-equivalent
                          # TFLOP/s above is the algorithmic fp64 work / time and may exceed the FP64 peak
-                         "bound": "mfma-i8", "unit": "TOPS", "peak": I8_PEAK_TOPS,
+                         "bound": "mfma", "mfma_dtype": "i8", "unit": "TOPS", "peak": I8_PEAK_TOPS,
                          "achieved": i8_ops_per_eval(n_mean, args.k) * evals_per_launch / (avg_ms * 1e-3) / 1e12,
                          "frac": i8_ops_per_eval(n_mean, args.k) * evals_per_launch / (avg_ms * 1e-3) / 1e12
                                  / I8_PEAK_TOPS,
                          "i8_ops_per_eval": i8_ops_per_eval(n_mean, args.k),
                          "fp64_equivalent_tflops": achieved_tf,
                          "note": "int8 ops over the whole batch time (weights + int8 GEMM + LDL^T overlapped); "
-                                 "gemm_i8_kernel alone runs ~3x this rate (profiles/r1l_summary.md)"}),
+                                 "gemm_i8_kernel alone runs ~2.2x this rate, ~1,700 TOPS (profiles/r1l_summary.md)"}),
                      "traffic_source": traffic_src,
                      "kernel": {"fused": f"likelihood_kernel<{args.k}>",
                                 "fused-int8": f"likelihood_i8_kernel<{args.k}>",

@@ -137,7 +137,9 @@ int gpdla_engine_process(gpdla_engine* engine, const gpdla_spectra* spectra,
                          const gpdla_results* results);
 /* Wait for enqueued work; returns GPDLA_ENUMERIC if any pivot was non-positive since the last call. */
 int gpdla_engine_synchronize(gpdla_engine* engine);
-/* Use an external hipStream_t (NULL restores the engine's own stream). */
+/* Use an external hipStream_t (NULL restores the engine's own stream).  All work of a process call
+ * is ordered on that stream: the int8 panel-GEMM path also runs its batched LDL^T on an internal
+ * second stream, joined back (hipStreamWaitEvent) before the call's later kernels and its copies. */
 int gpdla_engine_set_stream(gpdla_engine* engine, void* hip_stream);
 int gpdla_engine_get_stats(gpdla_engine* engine, gpdla_stats* stats);
 int gpdla_engine_reset_stats(gpdla_engine* engine);
