@@ -126,6 +126,10 @@ def profiled_traffic(Q: int, S: int, k: int, path: str = "fused"):
     """HBM bytes per likelihood launch from the committed PMC profile of the default workload
     (2 x FETCH_SIZE + WRITE_SIZE, gfx950 correction per MI355X_MICROARCH.md; includes
     Infinity-Cache hits).  None for other workloads or if no summary is present."""
+    c5 = ROOT / "profiles" / "r1l_c5_traffic.json"
+    if (Q, S, k) == (128, 100000, 50) and path == "panel-GEMM-int8" and c5.exists():
+        # configs[4]: per batch (the engine launch bench times), summed over its kernels
+        return json.loads(c5.read_text())["hbm_bytes_per_batch"], f"{c5.relative_to(ROOT)} (rocprofv3 PMC)"
     if (Q, S, k) != (1024, 10000, 20) or path != "fused" or not PROFILE_SUMMARY.exists():
         return None, None
     d = json.loads(PROFILE_SUMMARY.read_text())
