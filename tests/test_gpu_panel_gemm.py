@@ -93,7 +93,7 @@ def test_high_rank_ldl_buckets_match_oracle(k):
 
 
 def test_sample_chunk_boundaries():
-    """S + 1 = 16685 spans two 16384-sample chunks; compare with the fused path (k = 8)."""
+    """S + 1 = 16685 spans two sample chunks (<= 16384 each); compare with the fused path (k = 8)."""
     model = syn.make_model(k=8, seed=8)
     samples = syn.make_samples(16684)
     packed = syn.pack_spectra(syn.make_dr12q_like_spectra(model, 2, seed=9, mask_fraction=0.05))
