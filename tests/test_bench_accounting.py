@@ -1,0 +1,42 @@
+"""CPU checks of bench.py's work and traffic accounting (DESIGN.md sections 8, 10):
+the per-eval flop / byte / int8-op formulas at the BASELINE configs, and the lookup of the
+committed PMC traffic for configs[1] (fused fp64) and configs[4] (int8 panel-GEMM)."""
+import importlib.util
+import json
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+
+
+@pytest.fixture(scope="module")
+def bench():
+    spec = importlib.util.spec_from_file_location("bench_under_test", ROOT / "bench.py")
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def test_flops_and_bytes_per_eval(bench):
+    # ~3.79e5 flop and 160,072 B per eval at n = 800, k = 20 (fp64)
+    assert bench.algorithmic_flops_per_eval(800, 20) == pytest.approx(379466.667, rel=1e-6)
+    assert bench.effective_bytes_per_eval(800, 20) == 160072
+    # k = 50 (configs[4]): ~2.17e6 flop
+    assert bench.algorithmic_flops_per_eval(800, 50) == pytest.approx(2174666.667, rel=1e-6)
+
+
+def test_i8_ops_per_eval(bench):
+    # 10 digit pairs x n slots x (1275 Gram + 50 u entries) x 2 ops at k = 50
+    assert bench.i8_ops_per_eval(800, 50) == 2 * 10 * 800 * 1325
+
+
+def test_profiled_traffic_lookup(bench):
+    t, src = bench.profiled_traffic(1024, 10000, 20, "fused")
+    assert t is not None and t > 0 and "r1k_summary" in src
+    t5, src5 = bench.profiled_traffic(128, 100000, 50, "panel-GEMM-int8")
+    want = json.loads((ROOT / "profiles" / "r1l_c5_traffic.json").read_text())["hbm_bytes_per_batch"]
+    assert t5 == want and "r1l_c5_traffic" in src5
+    # other workloads / paths: no profiled number is claimed
+    assert bench.profiled_traffic(128, 100000, 50, "panel-GEMM") == (None, None)
+    assert bench.profiled_traffic(64, 10000, 20, "fused") == (None, None)
