@@ -119,7 +119,7 @@ WORKLOADS = {
 
 
 # rocprofv3 summary of this workload (tools/profile.sh + tools/summarize_profile.py), committed
-PROFILE_SUMMARY = ROOT / "profiles" / "r1k_summary.json"
+PROFILE_SUMMARY = ROOT / "profiles" / "r1m_summary.json"
 
 
 def profiled_traffic(Q: int, S: int, k: int, path: str = "fused"):
