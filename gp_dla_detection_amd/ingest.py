@@ -204,9 +204,17 @@ def preload_qsos(z_qsos, plates, mjds, fiber_ids, filter_flags, file_loader, log
 
 def run_preload_qsos(base_directory: str, release: str) -> dict:
     """The script on files: catalog.mat (z_qsos, plates, mjds, fiber_ids, filter_flags) and the
-    spectra under <base>/<release>/spectra -> preloaded_qsos.mat; filter_flags appended back to
-    catalog.mat (preload_qsos.m:77-83)."""
-    from .matv73 import loadmat, savemat73
+    spectra under <base>/<release>/spectra -> preloaded_qsos.mat; filter_flags saved back into
+    catalog.mat with ``'-append'`` (preload_qsos.m:77-83), i.e. only that variable changes.
+
+    The existing filter_flags dataset is overwritten in place when its storage allows it
+    (matv73.update_variable).  Otherwise catalog.mat is rewritten only if a load + save round trip
+    is lossless (no MATLAB objects such as the containers.Map variables build_catalogs.m writes,
+    no classes the reader does not know); if it is not, catalog.mat is left untouched, the flags
+    go to ``catalog_filter_flags.mat`` beside it and a warning names the file."""
+    import warnings
+
+    from .matv73 import loadmat, rewrite_blockers, savemat73, update_variable
     from .process import processed_directory
     d = processed_directory(base_directory, release)
     cat = loadmat(f"{d}/catalog.mat")
@@ -216,7 +224,18 @@ def run_preload_qsos(base_directory: str, release: str) -> dict:
                        lambda p, m, f: read_spec(spec_filename(spectra_dir, p, m, f)))
     flags = out.pop("filter_flags")
     savemat73(f"{d}/preloaded_qsos.mat", {k: (np.float64(v) if np.isscalar(v) else v) for k, v in out.items()})
-    cat["filter_flags"] = flags.reshape(-1, 1)
-    savemat73(f"{d}/catalog.mat", cat)                                                    # '-append'
+    cpath = f"{d}/catalog.mat"
     out["filter_flags"] = flags
+    out["filter_flags_path"] = cpath
+    if update_variable(cpath, "filter_flags", flags):                                    # '-append'
+        return out
+    blockers = rewrite_blockers(cpath)
+    if not blockers:
+        cat["filter_flags"] = flags.reshape(-1, 1)
+        savemat73(cpath, cat)
+        return out
+    side = f"{d}/catalog_filter_flags.mat"
+    savemat73(side, {"filter_flags": flags.reshape(-1, 1)})
+    warnings.warn(f"catalog.mat not rewritten ({'; '.join(blockers)}): filter_flags saved to {side}")
+    out["filter_flags_path"] = side
     return out

@@ -855,6 +855,76 @@ def loadmat73(path: str, variable_names=None) -> dict:
         r.close()
 
 
+_KNOWN_CLASSES = set(_MATLAB_CLASS.values()) | {"char", "logical", "cell", "struct", "double"}
+
+
+def rewrite_blockers(path: str) -> list[str]:
+    """Why a load + ``savemat73`` round trip of this v7.3 file would lose data: MATLAB objects
+    (``containers.Map`` and other MCOS classes are stored as opaque uint32 handles into the
+    ``#subsystem#`` group, which this reader does not decode) or classes it does not know.
+    Empty if every top-level variable decodes to what was written."""
+    r = _Reader(path)
+    try:
+        links = r.group_links(r.root_ohdr)
+        out = []
+        if "#subsystem#" in links:
+            out.append("#subsystem# group (MATLAB objects)")
+        for name, addr in links.items():
+            if name.startswith("#") or r.is_group(addr):
+                continue
+            attrs = r._attributes(r.messages(addr))
+            cls = attrs.get("MATLAB_class")
+            cls = cls.decode() if isinstance(cls, bytes) else cls
+            if "MATLAB_object_decode" in attrs or (cls is not None and cls not in _KNOWN_CLASSES):
+                out.append(f"{name}: MATLAB_class {cls!r}")
+        return out
+    finally:
+        r.close()
+
+
+def update_variable(path: str, name: str, value) -> bool:
+    """``save(path, name, '-append')`` for a numeric variable that already exists with the same
+    class and element count in contiguous, unfiltered storage: the new values are written over
+    the old bytes in place and nothing else in the file changes.  Returns False (file untouched)
+    when that is not possible."""
+    r = _Reader(path)
+    try:
+        links = r.group_links(r.root_ohdr)
+        if name not in links or r.is_group(links[name]):
+            return False
+        msgs = r.messages(links[name])
+        dims = dt = layout = None
+        for t, body in msgs:
+            if t == 0x01:
+                dims = r._dataspace(body)
+            elif t == 0x03:
+                dt, kind = r._datatype(body)
+                if kind not in ("int", "float"):
+                    return False
+            elif t == 0x08:
+                layout = body
+            elif t == 0x0B:
+                return False                      # filtered (compressed) storage
+        if layout is None or dims is None or dt is None or layout[0] not in (3, 4) or layout[1] != 1:
+            return False
+        addr, size = struct.unpack("<QQ", layout[2:18])
+        val = np.asarray(value)
+        n = int(np.prod(dims)) if dims else 1
+        if addr == UNDEF or val.size != n or size != n * dt.itemsize:
+            return False
+        conv = val.astype(dt.newbyteorder("="))
+        if not np.array_equal(conv, val):         # would not survive the class conversion
+            return False
+        off = r.base + addr
+    finally:
+        r.close()
+    mm = np.memmap(path, dtype=dt, mode="r+", offset=off, shape=(n,))
+    mm[:] = conv.ravel(order="F")                 # MATLAB column-major == C order over HDF5 dims
+    mm.flush()
+    del mm
+    return True
+
+
 def is_matv73(path: str) -> bool:
     with open(path, "rb") as f:
         head = f.read(128)
@@ -873,4 +943,5 @@ def loadmat(path: str, variable_names=None) -> dict:
     return {k: v for k, v in d.items() if not k.startswith("__")}
 
 
-__all__ = ["LazyArray", "Region", "MatFile", "savemat73", "open_region", "loadmat73", "loadmat", "is_matv73"]
+__all__ = ["LazyArray", "Region", "MatFile", "savemat73", "open_region", "loadmat73", "loadmat", "is_matv73",
+           "update_variable", "rewrite_blockers"]

@@ -176,23 +176,6 @@ def processed_directory(base_directory: str, release: str) -> str:
     return f"{base_directory}/{release}/processed"
 
 
-class _MatStruct:
-    """Attribute access over a loaded .mat dict so the reference's index expressions
-    (README.md:242-253, e.g. ``prior_catalog.in_dr9 & prior_catalog.los_inds(dla_catalog_name)``)
-    evaluate as written; a containers.Map variable (stored as a struct, matv73.py) is called
-    with its key."""
-
-    def __init__(self, d: dict):
-        self._d = d
-
-    def __getattr__(self, name):
-        v = self._d[name]
-        if isinstance(v, dict):
-            return _MatMap(v)
-        v = np.asarray(v)
-        return v.ravel() if v.ndim == 2 and 1 in v.shape else v
-
-
 class _MatMap:
     def __init__(self, d: dict):
         self._d = d
@@ -208,15 +191,15 @@ class _MatMap:
 
 def evaluate_index(expr, **names) -> np.ndarray:
     """``if (ischar(ind)) ind = eval(ind); end`` (process_qsos.m:7-9,53-55).  A boolean/integer
-    array passes through; a callable gets the named structs; a string is evaluated as the
-    reference's MATLAB index expression (``&``, ``|``, ``==``, ``~``, field access and Map
-    lookup) in a namespace holding only those structs."""
+    array passes through; a callable gets the named structs; a string is parsed as the
+    reference's MATLAB index expression (``&``, ``|``, ``~``, ``==``, ``~=``, field access and
+    containers.Map lookup, README.md:242-253) by the restricted evaluator in index_expr.py --
+    never by Python's ``eval``."""
     if callable(expr):
         return np.asarray(expr(**names))
     if isinstance(expr, str):
-        py = expr.replace("~=", "!=")
-        ns = {k: _MatStruct(v) if isinstance(v, dict) else v for k, v in names.items()}
-        return np.asarray(eval(py, {"__builtins__": {}}, ns))
+        from .index_expr import evaluate_index_string
+        return evaluate_index_string(expr, **names)
     return np.asarray(expr)
 
 
@@ -351,6 +334,10 @@ def run_process_qsos(base_directory: str, training_release: str, training_set_na
     region = [None]
     if rank == 0:
         merged = merge_shards(tidx.size, shards, gathered)
+        # GPDLA_ENUMERIC on any rank (its likelihoods are NaN): keep every rank's report
+        warns = [f"rank {r}: {g['numeric_warning']}" for r, g in enumerate(gathered) if g.get("numeric_warning")]
+        if warns:
+            merged["numeric_warning"] = "; ".join(warns)
         out = _finish(merged, z_all, prior, params, meta)
         out["test_ind"] = tind
         if save:

@@ -164,19 +164,21 @@ def prepare_training_data(spectra, z_qsos, max_noise_variance: float = P.MAX_NOI
 
 
 def pairwise_pca(X, k: int):
-    """pca(X, 'numcomponents', k, 'rows', 'pairwise'): eigenvectors / eigenvalues of the
-    covariance whose (a, b) entry uses the rows where both columns are present (centred over
-    those rows, normalised by count - 1)."""
+    """pca(X, 'numcomponents', k, 'rows', 'pairwise') (learn_qso_model.m:82-85): MATLAB's pca
+    centres each column by its nanmean and then takes the NON-centred pairwise covariance
+    (its ncnancov): C(a, b) = sum over the rows where both columns are present of x_a x_b,
+    divided by (that row count - 1).  Entries with fewer than two common rows are 0 here."""
     X = np.asarray(X, dtype=np.float64)
     m = ~np.isnan(X)
-    Z = np.where(m, X, 0.0)
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore", RuntimeWarning)
+        Xc = X - np.nanmean(X, axis=0)    # no-op on the already centred training fluxes (:70-71)
+    Z = np.where(m, Xc, 0.0)
     Mf = m.astype(np.float64)
-    N = Mf.T @ Mf
-    Sa = Z.T @ Mf                         # Sa[a, b] = sum over common rows of x_a
-    Sab = Z.T @ Z
+    N = Mf.T @ Mf                         # common-row counts
     with np.errstate(invalid="ignore", divide="ignore"):
-        cov = (Sab - Sa * Sa.T / N) / (N - 1)
-    cov = np.nan_to_num(cov)
+        cov = (Z.T @ Z) / (N - 1)
+    cov = np.where(N > 1, cov, 0.0)
     cov = 0.5 * (cov + cov.T)
     lat, vec = np.linalg.eigh(cov)
     order = np.argsort(lat)[::-1][:k]

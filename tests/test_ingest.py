@@ -103,6 +103,47 @@ def test_run_preload_qsos_tree(tmp_path):
     assert pre["all_flux"].shape == (2, 1) and float(pre["min_num_pixels"][0, 0]) == 200
 
 
+def _spectra_tree(tmp_path):
+    spectra = tmp_path / "dr12q" / "spectra"
+    for plate, mjd, fiber in ((4000, 55000, 12), (4001, 55001, 7)):
+        d = spectra / str(plate)
+        d.mkdir(parents=True)
+        shutil.copy(GOLDEN / "speclite_fixture.fits", d / f"spec-{plate}-{mjd}-{fiber:04d}.fits")
+    proc = tmp_path / "dr12q" / "processed"
+    proc.mkdir(parents=True)
+    return proc
+
+
+def test_run_preload_qsos_appends_in_place(tmp_path):
+    """preload_qsos.m:82-83 save(..., 'filter_flags', '-append'): a MATLAB catalog.mat with
+    containers.Map objects (libhdf5-written fixture) keeps every byte except filter_flags' data."""
+    proc = _spectra_tree(tmp_path)
+    shutil.copy(GOLDEN / "catalog_mcos.mat", proc / "catalog.mat")
+    before = (proc / "catalog.mat").read_bytes()
+    assert M.rewrite_blockers(str(proc / "catalog.mat"))          # the Maps cannot round-trip
+    out = I.run_preload_qsos(str(tmp_path), "dr12q")
+    assert out["filter_flags"].tolist() == [8, 2] and out["filter_flags_path"].endswith("catalog.mat")
+    after = (proc / "catalog.mat").read_bytes()
+    diff = [i for i in range(len(before)) if before[i] != after[i]]
+    assert len(before) == len(after) and len(diff) == 1           # the one flag byte that changed
+    cat = M.loadmat73(str(proc / "catalog.mat"))
+    assert cat["filter_flags"].ravel().tolist() == [8, 2] and cat["filter_flags"].dtype == np.uint8
+
+
+def test_run_preload_qsos_never_rewrites_objects(tmp_path, monkeypatch):
+    """When filter_flags cannot be overwritten in place and the file holds MATLAB objects, the
+    catalog is left untouched and the flags go to a sidecar file."""
+    proc = _spectra_tree(tmp_path)
+    shutil.copy(GOLDEN / "catalog_mcos.mat", proc / "catalog.mat")
+    before = (proc / "catalog.mat").read_bytes()
+    monkeypatch.setattr(M, "update_variable", lambda *a, **k: False)
+    with pytest.warns(UserWarning, match="not rewritten"):
+        out = I.run_preload_qsos(str(tmp_path), "dr12q")
+    assert (proc / "catalog.mat").read_bytes() == before
+    side = M.loadmat73(out["filter_flags_path"])
+    assert side["filter_flags"].ravel().tolist() == [8, 2]
+
+
 def test_own_fits_writer_roundtrip(tmp_path):
     """The test-side writer (tests/fits_writer.py) produces files the reader reads back exactly."""
     from fits_writer import write_speclite

@@ -198,8 +198,16 @@ def test_index_expressions_from_readme():
     assert got.tolist() == [False, False, True, False]
     mask = np.array([True, False])
     assert PR.evaluate_index(mask) is not None and PR.evaluate_index(mask).tolist() == [True, False]
-    with pytest.raises(Exception):
-        PR.evaluate_index("__import__('os')", catalog=prior_catalog)
+    got = PR.evaluate_index("catalog.in_dr9 | (catalog.filter_flags ~= 0) && ~false", catalog=prior_catalog)
+    assert got.tolist() == [True, True, False, True]
+    from gp_dla_detection_amd.index_expr import IndexExpressionError
+    # nothing reaches Python's eval: builtins, dunder chains, unknown names and calls are refused
+    for bad in ("__import__('os')", "().__class__.__base__.__subclasses__()",
+                "catalog.__class__", "catalog._d", "open('x')", "catalog.filter_flags(1)",
+                "catalog.in_dr9; 1", "lambda: 0", "catalog.in_dr9 + [1]", "catalog.nope == 0",
+                "catalog.los_inds('missing')"):
+        with pytest.raises(IndexExpressionError):
+            PR.evaluate_index(bad, catalog=prior_catalog)
 
 
 def write_reference_tree(base, Q=5, S=64, k=8, seed=3):

@@ -40,15 +40,24 @@ ARGS = ("dr12q", "dr9q_minus_concordance", "dr9q_concordance",
         "(catalog.filter_flags == 0)")
 
 
-def _worker(rank, world, port, base, q):
+def warning_compute(model, samples, packed, params, device):
+    """The oracle, plus the engine's GPDLA_ENUMERIC report on rank 1 only."""
+    import torch.distributed as dist
+    out = oracle_compute(model, samples, packed, params, device)
+    if dist.get_rank() == 1:
+        out["numeric_warning"] = "non-positive pivot or non-finite likelihood (outputs NaN)"
+    return out
+
+
+def _worker(rank, world, port, base, q, compute=oracle_compute):
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        out = PR.run_process_qsos(base, *ARGS, rank=rank, world=world, compute=oracle_compute)
-        q.put((rank, sorted(out)))
+        out = PR.run_process_qsos(base, *ARGS, rank=rank, world=world, compute=compute)
+        q.put((rank, sorted(out), out.get("numeric_warning")))
     finally:
         dist.barrier()
         dist.destroy_process_group()
@@ -73,7 +82,7 @@ def test_world2_file_equals_single_process(tmp_path):
     procs = [ctx.Process(target=_worker, args=(r, 2, port, str(multi), q)) for r in range(2)]
     for pr in procs:
         pr.start()
-    got = dict(q.get(timeout=500) for _ in range(2))
+    got = {r: keys for r, keys, _ in (q.get(timeout=500) for _ in range(2))}
     for pr in procs:
         pr.join(timeout=60)
         assert pr.exitcode == 0
@@ -87,3 +96,21 @@ def test_world2_file_equals_single_process(tmp_path):
         else:
             np.testing.assert_array_equal(a[k], b[k], err_msg=k)
     assert np.isfinite(b["sample_log_likelihoods_dla"]).all()
+
+
+@pytest.mark.timeout(600)
+def test_world2_numeric_warning_reaches_rank0(tmp_path):
+    """A GPDLA_ENUMERIC report raised on rank 1 is carried into rank 0's result."""
+    from test_matv73 import write_reference_tree
+    write_reference_tree(tmp_path, Q=4, S=8, k=8)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, str(tmp_path), q, warning_compute)) for r in range(2)]
+    for pr in procs:
+        pr.start()
+    got = {r: w for r, _, w in (q.get(timeout=500) for _ in range(2))}
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    assert got[0] is not None and got[0].startswith("rank 1:")

@@ -89,6 +89,17 @@ def test_pairwise_pca_without_missing_is_pca():
     np.testing.assert_allclose(np.abs(coef), np.abs(V[:, ::-1][:, :4]), atol=1e-8)
 
 
+def test_pairwise_pca_missing_values_hand_checked():
+    """Hand-computed pca(X, 'rows', 'pairwise'): columns centred by nanmean (3, 16/3), then the
+    non-centred pairwise covariance over common rows: C = [[8/2, 8/1], [8/1, (168/9)/2]]."""
+    X = np.array([[1.0, 2.0], [3.0, np.nan], [5.0, 6.0], [np.nan, 8.0]])
+    coef, lat = T.pairwise_pca(X, 2)
+    np.testing.assert_allclose(lat, [(20 + 8 * np.sqrt(10)) / 3, (20 - 8 * np.sqrt(10)) / 3], rtol=1e-13)
+    w, V = np.linalg.eigh(np.array([[4.0, 8.0], [8.0, 28.0 / 3.0]]))
+    np.testing.assert_allclose(np.abs(coef), np.abs(V[:, ::-1]), atol=1e-13)
+    assert np.all(coef[np.argmax(np.abs(coef), axis=0), [0, 1]] > 0)
+
+
 def test_prepare_training_data_shapes():
     model = syn.make_model(k=4)
     spectra = syn.make_dr12q_like_spectra(model, 6, seed=4)
