@@ -172,12 +172,15 @@ class DeviceArray:
         check(load().gpdla_memcpy_htod(device, C.c_void_p(out.ptr), arr.ctypes.data_as(C.c_void_p), out.nbytes))
         return out
 
-    def numpy(self, rows: int | None = None):
-        """Copy to host; ``rows`` limits the copy to the leading rows (C order)."""
+    def numpy(self, rows: int | None = None, start: int = 0):
+        """Copy to host; ``rows`` limits the copy to that many rows from row ``start`` (C order)."""
         import numpy as np
-        shape = self.shape if rows is None else (min(rows, self.shape[0]),) + self.shape[1:]
+        nrow = self.shape[0] - start if rows is None else min(rows, self.shape[0] - start)
+        shape = (max(nrow, 0),) + self.shape[1:]
         out = np.empty(shape, dtype=self.dtype)
-        check(load().gpdla_memcpy_dtoh(self.device, out.ctypes.data_as(C.c_void_p), C.c_void_p(self.ptr), out.nbytes))
+        row_bytes = int(self.nbytes // self.shape[0]) if self.shape[0] else 0
+        src = C.c_void_p(int(self.ptr) + int(start) * row_bytes)
+        check(load().gpdla_memcpy_dtoh(self.device, out.ctypes.data_as(C.c_void_p), src, out.nbytes))
         return out
 
     def free(self):

@@ -11,43 +11,7 @@
 #include "internal.h"
 
 // Build-time variant switches (A/B experiments; defaults are the shipped configuration).
-#ifndef GPDLA_WAVES_PER_EU
-#define GPDLA_WAVES_PER_EU 2
-#endif
-#ifndef GPDLA_SCHED_FENCE
-#define GPDLA_SCHED_FENCE 1
-#endif
-#ifndef GPDLA_FAST_EXP
-#define GPDLA_FAST_EXP 1
-#endif
-#ifndef GPDLA_RCP_STEPS
-#define GPDLA_RCP_STEPS 1
-#endif
 // far-wing fast path: fp64 kernel off (A/B +1.4% time: spills at 256 VGPRs), int8 kernel on (-0.9%)
-#ifndef GPDLA_FAR_WING
-#define GPDLA_FAR_WING 0
-#endif
-#ifndef GPDLA_I8_FAR_WING
-#define GPDLA_I8_FAR_WING 1
-#endif
-#ifndef GPDLA_MAGIC_RINT
-#define GPDLA_MAGIC_RINT 1
-#endif
-#ifndef GPDLA_SHARED_RCP
-#define GPDLA_SHARED_RCP 1
-#endif
-#ifndef GPDLA_BATCHED_PROFILE
-#define GPDLA_BATCHED_PROFILE 1
-#endif
-#ifndef GPDLA_LDL_REGISTERS
-#define GPDLA_LDL_REGISTERS 1
-#endif
-#ifndef GPDLA_LDL_CYCLIC
-#define GPDLA_LDL_CYCLIC 1
-#endif
-#ifndef GPDLA_LDL_GATHER
-#define GPDLA_LDL_GATHER 0
-#endif
 
 namespace gpdla {
 
@@ -71,12 +35,8 @@ __device__ inline double rcp_nr(double d) {
 // 1/d in the per-pixel sweeps (d = omega^2 a^2 + sigma^2 > 0, finite): v_rcp_f64 (~2^-26) and one
 // Newton step (error ~2^-52, i.e. within a couple of ulp; the sums over n pixels are insensitive)
 __device__ inline double rcp_sweep(double d) {
-#if GPDLA_RCP_STEPS == 1
   const double r = __builtin_amdgcn_rcp(d);
   return fma(r, fma(-d, r, 1.0), r);
-#else
-  return rcp_nr(d);
-#endif
 }
 
 // ---- int8 Ozaki contraction helpers (kernels_i8.hip, gemm_i8.hip)
@@ -119,16 +79,11 @@ __device__ inline double exp_tab64(double v, const double* __restrict__ tab) {
   constexpr double kLhi = 0.010830424695086549;           // ln2/64 to 33 bits (k*kLhi exact)
   constexpr double kLlo = 1.162596423439437e-12;           // ln2/64 - kLhi
   v = fmax(v, -1100.0);                                    // keeps k in int range; exp(-1100) = 0
-#if GPDLA_MAGIC_RINT
   // k = rint(v 64/ln2) by the 1.5 2^52 shifter: the fma rounds at the units place, the low
   // mantissa word is k as a two's-complement int (no f64 <-> int conversion instructions)
   const double kd = fma(v, kInvL, 0x1.8p52);
   const int ki = __double2loint(kd);
   const double k = kd - 0x1.8p52;
-#else
-  const double k = __builtin_rint(v * kInvL);
-  const int ki = (int)k;
-#endif
   double r = fma(-k, kLhi, v);
   r = fma(-k, kLlo, r);
   double p = fma(r, 1.0 / 120.0, 1.0 / 24.0);
@@ -301,11 +256,7 @@ __device__ inline double raw_profile3(double lam, const double (&afac)[3], doubl
     if (ax < kCoreX) f = core_eval(core_lds + j * kCoreTable, ax);
     total -= f;
   }
-#if GPDLA_FAST_EXP
   return exp_tab64(N * total, exp_lds);
-#else
-  return exp(N * total);
-#endif
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -15,11 +15,6 @@
 #include "../../include/gpdla.h"
 #include "internal.h"
 
-// panel-GEMM paths: run the batched LDL^T on a second stream, overlapped with the next chunk
-#ifndef GPDLA_LDL_OVERLAP
-#define GPDLA_LDL_OVERLAP 1
-#endif
-
 using namespace gpdla;
 
 namespace {
@@ -114,10 +109,6 @@ struct gpdla_engine {
   gpdla_params params{};
   hipStream_t own_stream = nullptr;
   hipStream_t stream = nullptr;
-  // panel-GEMM paths: the batched LDL^T of sample chunk c runs on ldl_stream while the weights and
-  // GEMM of chunk c + 1 run on `stream` (Gram/u/partials double-buffered by chunk parity)
-  hipStream_t ldl_stream = nullptr;
-  hipEvent_t ev_prod[2] = {nullptr, nullptr}, ev_ldl[2] = {nullptr, nullptr};
 
   // resident model / samples / line data
   double *d_rest = nullptr, *d_mu = nullptr, *d_M = nullptr, *d_logom = nullptr;
@@ -249,11 +240,6 @@ void gpdla_engine_destroy(gpdla_engine* e) {
   if (e->h_meta) (void)hipHostFree(e->h_meta);
   if (e->blas) (void)rocblas_destroy_handle(e->blas);
   if (e->meta_done) (void)hipEventDestroy(e->meta_done);
-  for (int b = 0; b < 2; ++b) {
-    if (e->ev_prod[b]) (void)hipEventDestroy(e->ev_prod[b]);
-    if (e->ev_ldl[b]) (void)hipEventDestroy(e->ev_ldl[b]);
-  }
-  if (e->ldl_stream) (void)hipStreamDestroy(e->ldl_stream);
   if (e->own_stream) (void)hipStreamDestroy(e->own_stream);
   delete e;
 }
@@ -307,14 +293,6 @@ int gpdla_engine_create(int32_t device, const gpdla_model* model, const gpdla_sa
     return fail(set_error(GPDLA_EDEVICE, "hipEventCreate failed"));
   if (e->gemm && rocblas_create_handle(&e->blas) != rocblas_status_success)
     return fail(set_error(GPDLA_EDEVICE, "rocblas_create_handle failed"));
-  if (e->gemm && e->i8 && GPDLA_LDL_OVERLAP) {  // int8 path: +5.5%; dgemm path: -0.4% (A/B), off
-    if (hipStreamCreateWithFlags(&e->ldl_stream, hipStreamNonBlocking) != hipSuccess)
-      return fail(set_error(GPDLA_EDEVICE, "hipStreamCreate failed"));
-    for (int b = 0; b < 2; ++b)
-      if (hipEventCreateWithFlags(&e->ev_prod[b], hipEventDisableTiming) != hipSuccess ||
-          hipEventCreateWithFlags(&e->ev_ldl[b], hipEventDisableTiming) != hipSuccess)
-        return fail(set_error(GPDLA_EDEVICE, "hipEventCreate failed"));
-  }
 
   const size_t G = model->num_rest, K = model->k;
   std::vector<double> Mrow(G * K);
@@ -369,12 +347,12 @@ int gpdla_engine_set_stream(gpdla_engine* e, void* hip_stream) {
   return GPDLA_OK;
 }
 
-// Panel-GEMM path for one batch: per spectrum and chunk of samples, weights -> two dgemm ->
-// batched LDL^T (gemm_path.hip).  Weights and GEMM run on stream st in order; with an LDL stream
-// the LDL^T of chunk c runs there (after chunk c's GEMM) while st proceeds with chunk c + 1, the
-// chunk's Gram, u and partials in buffer c & 1 (chunk c + 2 waits for chunk c's LDL^T); st joins
-// the LDL stream at the end, so work queued on st afterwards sees every output.
-static int run_panel_gemm(gpdla_engine* e, int64_t nq, const int64_t* h_sb, const int64_t* h_lb,
+// Panel-GEMM path for one batch: per spectrum and chunk of samples, weights -> GEMM (int8 digits
+// on the matrix cores, or two rocBLAS dgemm) -> batched LDL^T (gemm_path.hip), in stream order.
+// (The LDL^T on a second stream beside the next chunk's weights and GEMM measured +5% with the
+// VALU LDL^T kernel of round 1; with the matrix-core LDL^T both compete for the same units and the
+// overlap measured 0%, profiles/r2f, so it was removed.)
+static int run_panel_gemm(gpdla_engine* e, bool i8, int64_t nq, const int64_t* h_sb, const int64_t* h_lb,
                           const int64_t* h_cap, const int64_t* h_cb, int64_t sc_max, double* o_sll,
                           int64_t ld, double* o_null, hipStream_t st) {
   const int K = e->K;
@@ -382,37 +360,11 @@ static int run_panel_gemm(gpdla_engine* e, int64_t nq, const int64_t* h_sb, cons
   if (rocblas_set_stream(e->blas, st) != rocblas_status_success)
     return set_error(GPDLA_EDEVICE, "rocblas_set_stream failed");
   const double one = 1.0, zero = 0.0;
-  hipStream_t ls = e->ldl_stream ? e->ldl_stream : st;
-  int64_t chunk = 0;
   double *G = e->d_G, *U = e->d_U, *q1p = e->d_q1p, *ldp = e->d_ldp;
-  // before the chunk's producers: pick its buffer, wait for the LDL^T that last read it
-  auto begin_chunk = [&]() -> hipError_t {
-    const int b = (int)(chunk & 1);
-    const int64_t sw = e->ldl_stream ? b : 0;
-    G = e->d_G + sw * E * sc_max; U = e->d_U + sw * K * sc_max;
-    q1p = e->d_q1p + sw * kWeightParts * sc_max; ldp = e->d_ldp + sw * kWeightParts * sc_max;
-    if (e->ldl_stream && chunk >= 2) return hipStreamWaitEvent(st, e->ev_ldl[b], 0);
-    return hipSuccess;
-  };
-  // after the chunk's producers: hand the chunk to the LDL stream
-  auto to_ldl = [&]() -> hipError_t {
-    if (!e->ldl_stream) return hipSuccess;
-    const int b = (int)(chunk & 1);
-    hipError_t r = hipEventRecord(e->ev_prod[b], st);
-    if (r == hipSuccess) r = hipStreamWaitEvent(ls, e->ev_prod[b], 0);
-    return r;
-  };
-  auto end_chunk = [&]() -> hipError_t {
-    hipError_t r = hipSuccess;
-    if (e->ldl_stream) r = hipEventRecord(e->ev_ldl[chunk & 1], ls);
-    ++chunk;
-    return r;
-  };
   for (int64_t q = 0; q < nq; ++q) {
     for (int64_t s0 = 0; s0 <= e->S; s0 += sc_max) {
       const int32_t sc = (int32_t)std::min<int64_t>(sc_max, e->S + 1 - s0);
-      HIP_TRY(begin_chunk());
-      if (e->i8) {  // int8 Ozaki contraction (gemm_i8.hip): weights digits -> exact GEMM -> Gram, u
+      if (i8) {  // int8 Ozaki contraction (gemm_i8.hip): weights digits -> exact GEMM -> Gram, u
         const int64_t ks = i8_gemm_kstride(h_cap[q]);
         const int64_t rows = (sc_max + 127) / 128 * 128;
         WeightsI8Args wi{};
@@ -426,47 +378,33 @@ static int run_panel_gemm(gpdla_engine* e, int64_t nq, const int64_t* h_sb, cons
         gi.adig = e->d_ai8; gi.bdig = e->d_pi8 + h_cb[q];
         gi.ent = e->d_pent + q * 2 * (int64_t)i8_gemm_entries(K); gi.G = G; gi.U = U;
         HIP_TRY(launch_gemm_i8(gi, st));
-        HIP_TRY(to_ldl());
-        LdlArgs da{};
-        da.info = e->d_info; da.q = (int32_t)q; da.k = K;
-        da.G = G; da.U = U; da.q1p = q1p; da.ldp = ldp;
-        da.S = e->S; da.s0 = s0; da.sc = sc; da.perm = e->d_perm;
-        da.sample_ll = o_sll ? o_sll + q * ld : nullptr; da.ll_null = o_null + q; da.status = e->d_status;
-        HIP_TRY(launch_ldl_batch(da, ls));
-        HIP_TRY(end_chunk());
-        continue;
+      } else {
+        WeightsArgs wa{};
+        wa.info = e->d_info; wa.q = (int32_t)q;
+        wa.srow = e->d_srow + h_sb[q] * 8; wa.lam_pad = e->d_lam + h_lb[q]; wa.cap = h_cap[q];
+        wa.offsets = e->d_off; wa.nhi = e->d_nhi; wa.S = e->S; wa.s0 = s0; wa.sc = sc;
+        wa.num_lines = e->params.num_lines; wa.lines = make_line_args(e->d_lines);
+        wa.wg = e->d_wg; wa.wu = e->d_wu; wa.q1p = q1p; wa.ldp = ldp;
+        HIP_TRY(launch_weights(wa, st));
+        // Gram (E x sc) = PG (E x cap, the slot-major Khatri-Rao rows) * Wg^T (Wg stored [cap][sc])
+        rocblas_status bs = rocblas_dgemm(e->blas, rocblas_operation_none, rocblas_operation_transpose,
+                                          (rocblas_int)E, sc, (rocblas_int)h_cap[q], &one,
+                                          e->d_panel + h_sb[q] * E, (rocblas_int)E, e->d_wg, sc, &zero,
+                                          G, (rocblas_int)E);
+        if (bs == rocblas_status_success)
+          bs = rocblas_dgemm(e->blas, rocblas_operation_none, rocblas_operation_transpose, K, sc,
+                             (rocblas_int)h_cap[q], &one, e->d_pm + h_sb[q] * K, K, e->d_wu, sc, &zero,
+                             U, K);
+        if (bs != rocblas_status_success)
+          return set_error(GPDLA_EDEVICE, "rocblas_dgemm failed: %s", rocblas_status_to_string(bs));
       }
-      WeightsArgs wa{};
-      wa.info = e->d_info; wa.q = (int32_t)q;
-      wa.srow = e->d_srow + h_sb[q] * 8; wa.lam_pad = e->d_lam + h_lb[q]; wa.cap = h_cap[q];
-      wa.offsets = e->d_off; wa.nhi = e->d_nhi; wa.S = e->S; wa.s0 = s0; wa.sc = sc;
-      wa.num_lines = e->params.num_lines; wa.lines = make_line_args(e->d_lines);
-      wa.wg = e->d_wg; wa.wu = e->d_wu; wa.q1p = q1p; wa.ldp = ldp;
-      HIP_TRY(launch_weights(wa, st));
-      // Gram (E x sc) = PG (E x cap, the slot-major Khatri-Rao rows) * Wg^T (Wg stored [cap][sc])
-      rocblas_status bs = rocblas_dgemm(e->blas, rocblas_operation_none, rocblas_operation_transpose,
-                                        (rocblas_int)E, sc, (rocblas_int)h_cap[q], &one,
-                                        e->d_panel + h_sb[q] * E, (rocblas_int)E, e->d_wg, sc, &zero,
-                                        G, (rocblas_int)E);
-      if (bs == rocblas_status_success)
-        bs = rocblas_dgemm(e->blas, rocblas_operation_none, rocblas_operation_transpose, K, sc,
-                           (rocblas_int)h_cap[q], &one, e->d_pm + h_sb[q] * K, K, e->d_wu, sc, &zero,
-                           U, K);
-      if (bs != rocblas_status_success)
-        return set_error(GPDLA_EDEVICE, "rocblas_dgemm failed: %s", rocblas_status_to_string(bs));
-      HIP_TRY(to_ldl());
       LdlArgs da{};
       da.info = e->d_info; da.q = (int32_t)q; da.k = K;
       da.G = G; da.U = U; da.q1p = q1p; da.ldp = ldp;
       da.S = e->S; da.s0 = s0; da.sc = sc; da.perm = e->d_perm;
       da.sample_ll = o_sll ? o_sll + q * ld : nullptr; da.ll_null = o_null + q; da.status = e->d_status;
-      HIP_TRY(launch_ldl_batch(da, ls));
-      HIP_TRY(end_chunk());
+      HIP_TRY(launch_ldl_batch(da, st));
     }
-  }
-  if (e->ldl_stream && chunk > 0) {  // st joins the LDL stream
-    HIP_TRY(hipEventRecord(e->ev_ldl[(chunk - 1) & 1], ls));
-    HIP_TRY(hipStreamWaitEvent(st, e->ev_ldl[(chunk - 1) & 1], 0));
   }
   return GPDLA_OK;
 }
@@ -553,17 +491,19 @@ int gpdla_engine_process(gpdla_engine* e, const gpdla_spectra* sp, const gpdla_r
       if ((rc = grow(&e->d_srow, &e->cap_srow, (size_t)slots * 8))) return rc;
       if ((rc = grow(&e->d_wg, &e->cap_wg, (size_t)(cap_max * sc_max)))) return rc;
       if ((rc = grow(&e->d_wu, &e->cap_wu, (size_t)(cap_max * sc_max)))) return rc;
-      const size_t nbuf = e->ldl_stream ? 2 : 1;  // chunk-parity buffers when the LDL^T overlaps
-      if ((rc = grow(&e->d_G, &e->cap_G, nbuf * (size_t)(E * sc_max)))) return rc;
-      if ((rc = grow(&e->d_U, &e->cap_U, nbuf * (size_t)(e->K * sc_max)))) return rc;
-      if ((rc = grow(&e->d_q1p, &e->cap_q1p, nbuf * (size_t)(kWeightParts * sc_max)))) return rc;
-      if ((rc = grow(&e->d_ldp, &e->cap_ldp, nbuf * (size_t)(kWeightParts * sc_max)))) return rc;
+      if ((rc = grow(&e->d_G, &e->cap_G, (size_t)(E * sc_max)))) return rc;
+      if ((rc = grow(&e->d_U, &e->cap_U, (size_t)(e->K * sc_max)))) return rc;
+      if ((rc = grow(&e->d_q1p, &e->cap_q1p, (size_t)(kWeightParts * sc_max)))) return rc;
+      if ((rc = grow(&e->d_ldp, &e->cap_ldp, (size_t)(kWeightParts * sc_max)))) return rc;
     } else {
       if ((rc = grow(&e->d_scratch, &e->cap_scr, (size_t)blocks_x * nq * kSamplesPerBlock * es))) return rc;
     }
-    // int8 contraction for this batch (exactness bound on the slot count, else the fp64 kernel)
-    const bool batch_i8 = e->i8 && !e->gemm && lpix_max <= kI8MaxSlots;
-    if (e->i8 && e->gemm) {
+    // int8 contraction for this batch: its int32 level sums are exact only up to kI8MaxSlots
+    // slots, so a batch holding a longer spectrum runs the fp64 kernels (fused or dgemm) instead
+    const bool i8_exact = lpix_max <= kI8MaxSlots;
+    const bool batch_i8 = e->i8 && !e->gemm && i8_exact;
+    const bool batch_gemm_i8 = e->i8 && e->gemm && i8_exact;
+    if (batch_gemm_i8) {
       if ((rc = grow(&e->d_pi8, &e->cap_pi8, (size_t)chunks))) return rc;
       if ((rc = grow(&e->d_pent, &e->cap_pent, (size_t)nq * 2 * i8_gemm_entries(e->K)))) return rc;
       if ((rc = grow(&e->d_ai8, &e->cap_ai8,
@@ -677,7 +617,7 @@ int gpdla_engine_process(gpdla_engine* e, const gpdla_spectra* sp, const gpdla_r
     if ((rc = record_start(e, &t0, 0))) return rc;
     HIP_TRY(launch_prep(e->gemm ? 0 : e->K, pa, st));
     if (batch_i8) HIP_TRY(launch_convert_i8(e->K, ca, st));
-    if (e->i8 && e->gemm) {
+    if (batch_gemm_i8) {
       ConvertGemmI8Args cg{};
       cg.k = e->K; cg.info = e->d_info; cg.panel = e->d_panel; cg.panel_m = e->d_pm; cg.srow = e->d_srow;
       cg.slot_base = pa.slot_base; cg.slot_cap = pa.slot_cap; cg.bbase = pa.slot_cap + QB;
@@ -691,7 +631,7 @@ int gpdla_engine_process(gpdla_engine* e, const gpdla_spectra* sp, const gpdla_r
       HIP_TRY(launch_likelihood_i8(e->K, li, st));
     } else if (!e->gemm) {
       HIP_TRY(launch_likelihood(e->K, la, st));
-    } else if ((rc = run_panel_gemm(e, nq, h_sb, h_lb, h_cap, h_cb, sc_max, o_sll, ld, o_null, st))) {
+    } else if ((rc = run_panel_gemm(e, batch_gemm_i8, nq, h_sb, h_lb, h_cap, h_cb, sc_max, o_sll, ld, o_null, st))) {
       return rc;
     }
     HIP_TRY(hipEventRecord(t1.stop, st));

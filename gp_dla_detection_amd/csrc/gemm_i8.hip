@@ -22,9 +22,6 @@ namespace gpdla {
 namespace {
 
 #define MFMA_I8(A, B, C) __builtin_amdgcn_mfma_i32_16x16x64_i8((A), (B), (C), 0, 0, 0)
-#ifndef GPDLA_GEMM_I8_REGPF
-#define GPDLA_GEMM_I8_REGPF 1
-#endif
 
 // --------------------------------------------------------------------------------------------
 // convert: grid (entries / 64, spectra), 256 threads = 64 entries x 4 segments
@@ -206,17 +203,21 @@ __device__ inline void dma_piece(const uint8_t* sbase, uint32_t voffset, uint32_
 #pragma clang diagnostic pop
 }
 
-// --------------------------------------------------------------------------------------------
-// GEMM: grid (rows / 128 sample tiles, entries / 64 entry tiles), 4 waves; wave w owns samples
-// 32 w .. 32 w + 31 of the tile (2 row tiles) x all 64 entries (4 column tiles).  Per 64-slot K
-// step the block stages A (4 planes x 128 samples x 64 B) and B (4 planes x 64 entries x 64 B)
-// in LDS, 16 B granules XOR-swizzled by row so the MFMA operand reads are bank-conflict free.
-// --------------------------------------------------------------------------------------------
 constexpr int kGTileS = 128, kGTileE = 64;
 
+// --------------------------------------------------------------------------------------------
+// GEMM: grid (rows / 128 sample tiles, entries / 64 entry tiles), 4 waves; wave w owns samples
+// 32 w .. 32 w + 31 of the tile (2 row tiles) x all 64 entries (4 column tiles of
+// v_mfma_i32_16x16x64_i8, 10 digit pairs, int32 per level).  The weight digits (A) go
+// global -> VGPRs in the MFMA operand layout (each wave owns its 32 samples,
+// so A has no reuse across the block's waves and LDS would only add traffic), prefetched one K
+// step ahead; only the panel digits (B, shared by the 4 waves) are staged, by LDS-DMA into a
+// double-buffered tile.  Per K step a wave reads 16 B-operand granules from LDS for 80 MFMAs
+// (200 B per MFMA; staging both operands through LDS cost 300 B per MFMA plus the A writes,
+// which kept the matrix cores waiting on LDS bandwidth).
+// --------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256, 2) void gemm_i8_kernel(GemmI8Args a) {
-  __shared__ __attribute__((aligned(16))) uint8_t As[4 * kGTileS * 64];
-  __shared__ __attribute__((aligned(16))) uint8_t Bs[4 * kGTileE * 64];
+  __shared__ __attribute__((aligned(16))) uint8_t Bs[2][4 * kGTileE * 64];
   const SpecInfo inf = a.info[a.q];
   if (inf.J == 0) return;
   const int K = a.k;
@@ -228,15 +229,36 @@ __global__ __launch_bounds__(256, 2) void gemm_i8_kernel(GemmI8Args a) {
   const int s_tile = blockIdx.x * kGTileS;
   const int e_tile = blockIdx.y * kGTileE;
   const bool u_tile = e_tile >= Ep;
-  const int nks = (16 * ((inf.L + 15) / 16)) / 16;  // 4 Ls16 / 64
+  const int nks = (16 * ((inf.L + 15) / 16)) / 16;  // 64-slot K steps: 4 Ls16 / 64
   const int64_t planeA = a.rows * a.kstride, planeB = (int64_t)NE * a.kstride;
-  const uint8_t* A0 = a.adig + (u_tile ? 4 * planeA : 0) + (int64_t)s_tile * 16;
+  const int g = lane >> 4;
+  // A: lane (row lane & 15, 16-slot group g of the K step); planes stored [group][sample][16 B]
+  const uint8_t* A0 = a.adig + (u_tile ? 4 * planeA : 0) +
+                      ((int64_t)g * a.rows + s_tile + 32 * wave_s + (lane & 15)) * 16;
   const uint8_t* B0 = a.bdig + (int64_t)e_tile * a.kstride;
-  const uint32_t as_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)As;
-  const uint32_t bs_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)Bs;
-  // this lane's piece geometry: row (l >> 2) of a 16-row piece, LDS granule l & 3 holds global
-  // granule (l & 3) ^ ((row >> 2) & 3)
+  const uint32_t bs_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)&Bs[0][0];
+  // B piece geometry (16 entry rows x 64 B per 1 KiB piece; 4 pieces per wave per K step):
+  // row (lane >> 2) of the piece, LDS granule lane & 3 holds global granule (lane & 3) ^ ((row >> 2) & 3)
   const int prow = lane >> 2;
+  uint32_t boff[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int piece = wave_s * 4 + i;
+    const int p = piece >> 2, row = (piece & 3) * 16 + prow;
+    boff[i] = (uint32_t)(p * planeB + (int64_t)row * a.kstride + 16 * ((lane & 3) ^ ((row >> 2) & 3)));
+  }
+  auto stage_b = [&](int ks, int buf) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      dma_piece(B0 + ks * 64, boff[i], bs_base + (uint32_t)(buf * (4 * kGTileE * 64) + (wave_s * 4 + i) * 1024));
+  };
+  auto load_a = [&](int ks, v4i (&r)[2][4]) {
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+      for (int p = 0; p < 4; ++p)
+        r[rt][p] = *reinterpret_cast<const v4i*>(A0 + p * planeA + (int64_t)ks * 4 * a.rows * 16 + rt * 256);
+  };
   v4i acc[4][2][4];
 #pragma unroll
   for (int l = 0; l < 4; ++l)
@@ -244,71 +266,26 @@ __global__ __launch_bounds__(256, 2) void gemm_i8_kernel(GemmI8Args a) {
     for (int rt = 0; rt < 2; ++rt)
 #pragma unroll
       for (int ct = 0; ct < 4; ++ct) acc[l][rt][ct] = (v4i){0, 0, 0, 0};
-  const int g = lane >> 4;
-#if GPDLA_GEMM_I8_REGPF
-  // register prefetch: each wave loads its 12 pieces of step ks + 1 into VGPRs while step ks's
-  // MFMAs run, then stores them to LDS after the barrier (double buffering without a second tile)
-  auto load_pieces = [&](int ks, v4i (&reg)[12]) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int piece = wave_s * 8 + i;
-      const int p = piece >> 3, row = (piece & 7) * 16 + prow;
-      const int64_t off = (int64_t)(ks * 4 + ((lane & 3) ^ ((row >> 2) & 3))) * a.rows * 16 + row * 16;
-      reg[i] = *reinterpret_cast<const v4i*>(A0 + p * planeA + off);
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int piece = wave_s * 4 + i;
-      const int p = piece >> 2, row = (piece & 3) * 16 + prow;
-      const int64_t off = (int64_t)row * a.kstride + ks * 64 + 16 * ((lane & 3) ^ ((row >> 2) & 3));
-      reg[8 + i] = *reinterpret_cast<const v4i*>(B0 + p * planeB + off);
-    }
-  };
-  v4i pf[12];
-  load_pieces(0, pf);
+  v4i Ad[2][4], An[2][4];
+  stage_b(0, 0);
+  load_a(0, Ad);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
   for (int ks = 0; ks < nks; ++ks) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i) *reinterpret_cast<v4i*>(As + (wave_s * 8 + i) * 1024 + lane * 16) = pf[i];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) *reinterpret_cast<v4i*>(Bs + (wave_s * 4 + i) * 1024 + lane * 16) = pf[8 + i];
-    __syncthreads();
-    if (ks + 1 < nks) load_pieces(ks + 1, pf);
-#else
-  for (int ks = 0; ks < nks; ++ks) {
-    // A: 32 pieces (plane p = piece / 8, rows 16 (piece % 8) ..), 8 per wave
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int piece = wave_s * 8 + i;
-      const int p = piece >> 3, row = (piece & 7) * 16 + prow;
-      const uint32_t voffset = (uint32_t)((int64_t)(ks * 4 + ((lane & 3) ^ ((row >> 2) & 3))) * a.rows * 16 + row * 16);
-      dma_piece(A0 + p * planeA, voffset, as_base + (uint32_t)(piece * 1024));
+    const int cur = ks & 1;
+    const bool more = ks + 1 < nks;
+    if (more) {
+      stage_b(ks + 1, cur ^ 1);
+      load_a(ks + 1, An);
     }
-    // B: 16 pieces (plane p = piece / 4, entries 16 (piece % 4) ..), 4 per wave
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int piece = wave_s * 4 + i;
-      const int p = piece >> 2, row = (piece & 3) * 16 + prow;
-      const uint32_t voffset = (uint32_t)((int64_t)row * a.kstride + ks * 64 + 16 * ((lane & 3) ^ ((row >> 2) & 3)));
-      dma_piece(B0 + p * planeB, voffset, bs_base + (uint32_t)(piece * 1024));
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-#endif
-    v4i Ad[2][4];
-#pragma unroll
-    for (int rt = 0; rt < 2; ++rt) {
-      const int row = 32 * wave + 16 * rt + (lane & 15);
-#pragma unroll
-      for (int p = 0; p < 4; ++p)
-        Ad[rt][p] = *reinterpret_cast<const v4i*>(As + p * (kGTileS * 64) + row * 64 + 16 * (g ^ ((row >> 2) & 3)));
-    }
+    const uint8_t* Bc = Bs[cur];
 #pragma unroll
     for (int ct = 0; ct < 4; ++ct) {
       const int row = 16 * ct + (lane & 15);
       v4i Bd[4];
 #pragma unroll
       for (int p = 0; p < 4; ++p)
-        Bd[p] = *reinterpret_cast<const v4i*>(Bs + p * (kGTileE * 64) + row * 64 + 16 * (g ^ ((row >> 2) & 3)));
+        Bd[p] = *reinterpret_cast<const v4i*>(Bc + p * (kGTileE * 64) + row * 64 + 16 * (g ^ ((row >> 2) & 3)));
 #pragma unroll
       for (int rt = 0; rt < 2; ++rt) {
         const v4i* Ar = Ad[rt];
@@ -324,7 +301,14 @@ __global__ __launch_bounds__(256, 2) void gemm_i8_kernel(GemmI8Args a) {
         acc[3][rt][ct] = MFMA_I8(Ar[3], Bd[0], acc[3][rt][ct]);
       }
     }
-    __syncthreads();  // the tiles are overwritten by the next step's DMA
+    if (more) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // next step's B DMA and A loads landed
+#pragma unroll
+      for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+        for (int p = 0; p < 4; ++p) Ad[rt][p] = An[rt][p];
+    }
+    __syncthreads();  // everyone's DMA landed; buffer cur is free for step ks + 2
   }
   // epilogue: D lane map of 16x16x64: sample 4 (lane >> 4) + r, entry lane & 15
 #pragma unroll

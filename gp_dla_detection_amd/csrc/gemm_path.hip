@@ -4,8 +4,9 @@
 //                     Wg[slot][s] = a^2/d, Wu[slot][s] = a r/d, per-segment sum r^2/d, sum log d
 //   rocBLAS dgemm x2  Gram[s] = PG^T Wg[:, s] (Khatri-Rao panel, k(k+1)/2 columns) and
 //                     u[s] = M^T Wu[:, s]  (engine.hip)  -- log_mvnpdf_low_rank.m:13-23
-//   ldl_batch_kernel  augmented LDL^T of [[I + Gram, u], [u', sum r^2/d]] per sample -> logdet and
-//                     r'K^-1 r (log_mvnpdf_low_rank.m:24-32), one wave per sample.
+//   ldl_mfma_kernel   augmented LDL^T of [[I + Gram, u], [u', sum r^2/d]] per sample -> logdet and
+//                     r'K^-1 r (log_mvnpdf_low_rank.m:24-32), 4 samples per wave on the f64
+//                     matrix cores.
 // Slot layout, neutral padding rows and sample order are those of the fused path (kernels.hip).
 #include <hip/hip_runtime.h>
 
@@ -123,38 +124,40 @@ __device__ inline double sum_parts(const double* p) {
   return acc;
 }
 
-// Augmented LDL^T per sample, one wave per sample (4 per block), matrix packed lower-triangular
-// in LDS: A(i, j), j <= i <= k, at i(i+1)/2 + j; row k is [u', sum r^2/d].  Right-looking: at
-// pivot p every lane updates a share of the trailing triangle (index table tri: element t ->
-// (row offset, column offset)); after the k pivots A(k, k) = r'D^-1 r - u'B^-1 u = r'K^-1 r.
-constexpr int kTriMax = kGemmMaxK * (kGemmMaxK + 1) / 2;
-constexpr int kPackedMax = (kGemmMaxK + 1) * (kGemmMaxK + 2) / 2;
-
 __device__ inline void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-__global__ __launch_bounds__(256) void ldl_batch_kernel(LdlArgs a) {
-  __shared__ uint32_t tri[kTriMax];
-  __shared__ double mats[4][kPackedMax];
-  const int K = a.k;
-  const int T0 = K * (K + 1) / 2;
-  for (int t = threadIdx.x; t < T0; t += 256) {
-    int ai = (int)((sqrtf(8.0f * (float)t + 1.0f) - 1.0f) * 0.5f);
-    while ((ai + 1) * (ai + 2) / 2 <= t) ++ai;
-    while (ai * (ai + 1) / 2 > t) --ai;
-    tri[t] = ((uint32_t)ai << 16) | (uint32_t)(t - ai * (ai + 1) / 2);
-  }
-  __syncthreads();
+// Batched augmented LDL^T on the f64 matrix cores: one wave per 4 samples, the 4 samples being the
+// 4 independent blocks of v_mfma_f64_4x4x4_4b.  The augmented matrix [[I + Gram, u], [u', r'D^-1 r]]
+// of rank k + 1 is padded with identity rows to N = 4 NT and held as its NT (NT + 1) / 2 upper
+// 4 x 4 tiles S(L, I), L <= I, one double per lane per tile in the MFMA D layout (lane 16 i + 4 b +
+// j holds S(4L + i, 4I + j) of sample b).  Right-looking block elimination, per block column J:
+//   * the diagonal tile goes through LDS to the 16 lanes of its sample, each of which factors it
+//     (4 x 4 LDL^T, pivots D_p -> log det / r'K^-1 r) and solves for its element of S_JJ^-1;
+//   * X_L = S_JJ^-1 S(J, L) for every L > J                         (one MFMA each);
+//   * S(L, I) -= X_L' S(J, I) for every J < L <= I                 (one MFMA each: the Schur
+//     complement S_LI - S_LJ S_JJ^-1 S_JI, using S_LJ = S_JL').
+// Operand maps of 4x4x4_4b (probed, tools/probe_layout.hip): A[i][k] at lane 16k + 4b + i,
+// B[k][j] at 16k + 4b + j, D[i][j] at 16i + 4b + j -- so a D-layout register passed as B is the
+// tile itself and passed as A is its transpose, which is what both products need.  After the NT
+// block steps log det B = sum_{p<k} log D_p and r'K^-1 r = D_k (log_mvnpdf_low_rank.m:24-32).
+template <int NT>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT <= 13 ? 2 : 1))) void ldl_mfma_kernel(LdlArgs a) {
+  constexpr int NTT = NT * (NT + 1) / 2;
+  __shared__ __attribute__((aligned(16))) double diag_all[4][2][64];  // double-buffered by J parity
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int sl = blockIdx.x * 4 + wave;
-  if (sl >= a.sc) return;  // wave-uniform; no block barrier below
+  const int b = (lane >> 2) & 3, ti = lane >> 4, tj = lane & 3;
+  const int sl = (blockIdx.x * 4 + wave) * 4 + b;  // this lane's sample within the chunk
+  const bool live = sl < a.sc;
+  const int K = a.k;
   const int64_t s = a.s0 + sl;
   const SpecInfo inf = a.info[a.q];
+  const bool write = live && ti == 0 && tj == 0;
   auto emit = [&](double ll) {
-    if (lane != 0) return;
+    if (!write) return;
     if (s == a.S) *a.ll_null = ll;
     else if (a.sample_ll) a.sample_ll[a.perm[s]] = ll;
   };
@@ -162,286 +165,121 @@ __global__ __launch_bounds__(256) void ldl_batch_kernel(LdlArgs a) {
     emit(NAN);
     return;
   }
-  double* A = mats[wave];
-  auto at = [&](int i, int j) -> double& { return A[i * (i + 1) / 2 + j]; };
-  const int64_t E = T0;
-  const double* Gs = a.G + (int64_t)sl * E;
-  int start = 0;
-  for (int r = 0; r < K; ++r) {  // Gram (r, c), r <= c, row-major upper -> A(c, r); B = I + Gram
-    for (int c = r + lane; c < K; c += 64) at(c, r) = Gs[start + (c - r)] + (c == r ? 1.0 : 0.0);
-    start += K - r;
-  }
-  for (int j = lane; j < K; j += 64) at(K, j) = a.U[(int64_t)sl * K + j];
-  const double* q = a.q1p + (int64_t)sl * kWeightParts;
-  const double* l4 = a.ldp + (int64_t)sl * kWeightParts;
-  if (lane == 0) at(K, K) = sum_parts(q);
-  const double logdet_d = sum_parts(l4);
-  wave_sync();
-  double logdet_b = 0.0;
-  bool bad = false;
-  for (int p = 0; p < K; ++p) {
-    const double d = at(p, p);
-    bad |= !(d > 0.0);
-    logdet_b += log(d);
-    const double invd = 1.0 / d;
-    const int R = K - p, T = R * (R + 1) / 2;
-    for (int t = lane; t < T; t += 64) {
-      const uint32_t ab = tri[t];
-      const int i = p + 1 + (int)(ab >> 16), j = p + 1 + (int)(ab & 0xffff);
-      at(i, j) = fma(-at(i, p) * invd, at(j, p), at(i, j));
-    }
-    wave_sync();
-  }
-  const double quad = at(K, K);
-  double ll = -0.5 * (quad + (logdet_d + logdet_b) + inf.n * kLog2Pi);  // log_mvnpdf_low_rank.m:30-32
-  if (bad || !(fabs(ll) < INFINITY)) {
-    ll = NAN;
-    if (lane == 0) atomicOr(a.status, 1);
-  }
-  emit(ll);
-}
-
-// Register form of the same augmented LDL^T (k <= 63): one wave per sample, lane j holds column
-// j of [[I + Gram, u], [u', sum r^2/d]] (rows 0..k) in VGPRs.  At pivot p every lane j > p
-// updates its column with column p.  Column p is row p by symmetry, and row p is spread over the
-// lanes (lane i holds A(p, i) = A(i, p) in col[p]): one ds_write_b64 per pivot publishes it to a
-// 64-double LDS line that every lane then reads by broadcast (2 entries per ds_read_b128), so the
-// update is ~1.5 instructions per entry with no cross-lane shuffles and no barrier (the wave's
-// LDS operations complete in order).  KB bounds k + 1 at compile time (register arrays, unrolled
-// pivots); the rank itself is a.k.
-__device__ inline double readlane_d(double v, int lane) {
-  const int lo = __builtin_amdgcn_readlane(__double2loint(v), lane);
-  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), lane);
-  return __hiloint2double(hi, lo);
-}
-
-template <int KB>
-__global__ __launch_bounds__(256) void ldl_reg_kernel(LdlArgs a) {
-  constexpr int kStage = (KB - 1) * KB / 2 + KB;  // packed Gram + u of the largest rank in the bucket
-  __shared__ __attribute__((aligned(16))) double rowp_all[4][2][64];  // double-buffered by pivot parity
-  __shared__ __attribute__((aligned(16))) double stage_all[4][kStage];
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  double* stage = stage_all[wave];
-  const int sl = blockIdx.x * 4 + wave;
-  if (sl >= a.sc) return;  // wave-uniform
-  const int K = a.k;
-  const int64_t s = a.s0 + sl;
-  const SpecInfo inf = a.info[a.q];
-  auto emit = [&](double ll) {
-    if (lane != 0) return;
-    if (s == a.S) *a.ll_null = ll;
-    else if (a.sample_ll) a.sample_ll[a.perm[s]] = ll;
-  };
-  if (inf.J == 0) {
-    emit(NAN);
-    return;
-  }
   const int64_t E = (int64_t)K * (K + 1) / 2;
-  const double* Gs = a.G + (int64_t)sl * E;
-  const double* Us = a.U + (int64_t)sl * K;
-  const double* q = a.q1p + (int64_t)sl * kWeightParts;
-  const double* l4 = a.ldp + (int64_t)sl * kWeightParts;
-  const int j = lane;
-  // the sample's packed Gram and u, copied coalesced into this wave's LDS slice, then gathered
-  // column-wise (the lower half of a column is strided in the packed layout)
-  {  // all loads in flight before the first LDS store (one global-memory latency, not ~20)
-    constexpr int kIt = (kStage + 63) / 64;
-    double tmp[kIt];
+  const int slc = live ? sl : 0;  // idle samples of the last wave compute on sample 0, discarded
+  const double* Gs = a.G + (int64_t)slc * E;
+  const double* Us = a.U + (int64_t)slc * K;
+  const double q1 = sum_parts(a.q1p + (int64_t)slc * kWeightParts);
+  const double logdet_d = sum_parts(a.ldp + (int64_t)slc * kWeightParts);
+  // Load the tiles: straight-line code (unconditional loads from valid addresses, then selects), so
+  // the NT (NT + 1) / 2 loads go out back to back.  Since 4 (NT - 1) <= k, only the last tile
+  // column (I = NT - 1) holds the u column (c = k), r'D^-1 r (r = c = k) and identity padding
+  // (c > k); every other tile is Gram only.  Gram offsets follow gram_tile_index (internal.h): a
+  // compile-time tile base plus a per-lane position inside the tile.
+  const int di = min(ti, tj), dj = max(ti, tj);            // diagonal tiles: upper-triangle slot
+  const int ldiag = di * 4 - di * (di - 1) / 2 + (dj - di), loff = 4 * ti + tj;
+  const double done = ti == tj ? 1.0 : 0.0;
+  const int w = K - 4 * (NT - 1);                           // Gram columns in the last tile column
+  constexpr int base2 = 10 * (NT - 1) + 8 * (NT - 1) * (NT - 2);
+  double T[NTT];  // tile (L, I), L <= I, at L NT - L (L - 1) / 2 + (I - L)
 #pragma unroll
-    for (int it = 0; it < kIt; ++it) {
-      const int t = it * 64 + lane;
-      tmp[it] = t < E ? Gs[t] : (t < E + K ? Us[t - E] : 0.0);
-    }
+  for (int L = 0; L < NT; ++L) {
 #pragma unroll
-    for (int it = 0; it < kIt; ++it) {
-      const int t = it * 64 + lane;
-      if (t < E + K) stage[t] = tmp[it];
-    }
-  }
-  __builtin_amdgcn_wave_barrier();
-  double col[KB];
-#pragma unroll
-  for (int i = 0; i < KB; ++i) {
-    double v = 0.0;
-    if (i <= K && j <= K) {
-      if (i < K && j < K) {
-        const int r = i < j ? i : j, c = i < j ? j : i;  // Gram (r, c), row-major upper
-        v = stage[r * K - r * (r - 1) / 2 + (c - r)] + (i == j ? 1.0 : 0.0);  // B = I + Gram
-      } else if (i == K && j == K) {
-        v = sum_parts(q);  // sum r^2 / d
+    for (int I = L; I < NT; ++I) {
+      double v;
+      if (I < NT - 1) {
+        const int tb = 10 * L + 16 * (L * (NT - 2) - L * (L - 1) / 2) + (I == L ? 0 : 10 + 16 * (I - L - 1));
+        v = I == L ? Gs[tb + ldiag] + done : Gs[tb + loff];   // B = I + Gram
+      } else if (L < NT - 1) {
+        // rows 4L + ti < k, column c = 4 (NT - 1) + tj: Gram if tj < w, u if tj == w, padding after
+        const int r = 4 * L + ti;
+        const double g = Gs[base2 + L * 4 * w + ti * w + min(tj, max(w - 1, 0))], u = Us[r];
+        v = tj < w ? g : (tj == w ? u : 0.0);
       } else {
-        v = stage[E + (i == K ? j : i)];  // u in row k / column k
+        // corner tile: Gram (di <= dj < w), then u (dj == w, di < w), r'D^-1 r (di == dj == w),
+        // identity padding
+        const int r = 4 * L + di;
+        const int cw = max(w, 1);
+        const double g = Gs[base2 + L * 4 * w + min(di, cw - 1) * w - min(di, cw - 1) * (min(di, cw - 1) - 1) / 2 +
+                            (min(dj, cw - 1) - min(di, cw - 1))];
+        const double u = Us[min(r, K - 1)];
+        v = dj < w ? g + done : (dj == w ? (di < w ? u : q1) : done);
       }
+      T[L * NT - L * (L - 1) / 2 + (I - L)] = v;
     }
-    col[i] = v;
   }
-  double pb = 1.0;  // prod D_p = pb 2^eb (frexp-renormalised, one log at the end)
+  double pb = 1.0;  // prod_{p<k} D_p = pb 2^eb
   int eb = 0;
+  double quad = 0.0;
   bool bad = false;
 #pragma unroll
-  for (int p = 0; p < KB - 1; ++p) {
-    if (p < K) {
-      // two LDS lines alternate, so pivot p + 1's store cannot overwrite the line pivot p is
-      // still reading; the one wave barrier orders this pivot's store before its loads
-      double* rowp = rowp_all[wave][p & 1];
-      rowp[j] = col[p];                 // row p = column p, lane i -> A(i, p)
-      __builtin_amdgcn_wave_barrier();
-      const double d = readlane_d(col[p], p);  // the pivot straight from lane p (no LDS round trip)
-      bad |= !(d > 0.0);
-      pb *= d;
-      if ((p & 3) == 3) {
-        int ex;
-        pb = frexp(pb, &ex);
-        eb += ex;
-      }
-      const double f = (j > p && j <= K) ? col[p] * rcp_nr(d) : 0.0;  // A(j, p) / D_p
-      // rows past k hold zeros in every lane and stay zero: no per-row guard
+  for (int J = 0; J < NT; ++J) {
+    // ---- diagonal tile -> LDS -> every lane of the sample
+    const int jj = J * NT - J * (J - 1) / 2;
+    double* diag = diag_all[wave][J & 1];
+    diag[b * 16 + ti * 4 + tj] = T[jj];
+    wave_sync();
+    const double* dg = diag + b * 16;  // row-major 4 x 4 tile of this lane's sample
+    const double2 r00 = *reinterpret_cast<const double2*>(dg + 0), r02 = *reinterpret_cast<const double2*>(dg + 2);
+    const double2 r12 = *reinterpret_cast<const double2*>(dg + 6), r22 = *reinterpret_cast<const double2*>(dg + 10);
+    const double m[16] = {r00.x, r00.y, r02.x, r02.y, 0, dg[5], r12.x, r12.y, 0, 0, r22.x, r22.y, 0, 0, 0, dg[15]};
+    // 4 x 4 LDL^T of the (symmetric) tile from its upper triangle
+    double a00 = m[0], a01 = m[1], a02 = m[2], a03 = m[3];
+    double a11 = m[5], a12 = m[6], a13 = m[7];
+    double a22 = m[10], a23 = m[11], a33 = m[15];
+    const double D0 = a00, i0 = rcp_nr(D0);
+    const double l10 = a01 * i0, l20 = a02 * i0, l30 = a03 * i0;
+    a11 = fma(-l10, a01, a11); a12 = fma(-l10, a02, a12); a13 = fma(-l10, a03, a13);
+    a22 = fma(-l20, a02, a22); a23 = fma(-l20, a03, a23); a33 = fma(-l30, a03, a33);
+    const double D1 = a11, i1 = rcp_nr(D1);
+    const double l21 = a12 * i1, l31 = a13 * i1;
+    a22 = fma(-l21, a12, a22); a23 = fma(-l21, a13, a23); a33 = fma(-l31, a13, a33);
+    const double D2 = a22, i2 = rcp_nr(D2);
+    const double l32 = a23 * i2;
+    a33 = fma(-l32, a23, a33);
+    const double D3 = a33, i3 = rcp_nr(D3);
+    const double Dp[4] = {D0, D1, D2, D3};
 #pragma unroll
-      for (int i = p + 1; i < KB; ++i) col[i] = fma(-rowp[i], f, col[i]);  // A(i,j) -= A(i,p) A(j,p) / D_p
+    for (int t = 0; t < 4; ++t) {
+      const int p = 4 * J + t;
+      if (p < K) {
+        bad |= !(Dp[t] > 0.0) || !(Dp[t] < INFINITY);
+        pb *= Dp[t];
+      } else if (p == K) {
+        quad = Dp[t];
+      }
+    }
+    {
+      int ex;
+      pb = frexp(pb, &ex);
+      eb += ex;
+    }
+    // this lane's element of S_JJ^-1: column ti (L^-T D^-1 L^-1 e_ti), row tj, so that the register
+    // read as an MFMA A operand is S_JJ^-1 itself
+    const double e0 = ti == 0 ? 1.0 : 0.0, e1 = ti == 1 ? 1.0 : 0.0, e2 = ti == 2 ? 1.0 : 0.0,
+                 e3 = ti == 3 ? 1.0 : 0.0;
+    const double y0 = e0, y1 = fma(-l10, y0, e1), y2 = fma(-l21, y1, fma(-l20, y0, e2)),
+                 y3 = fma(-l32, y2, fma(-l31, y1, fma(-l30, y0, e3)));
+    const double x3 = y3 * i3, x2 = fma(-l32, x3, y2 * i2), x1 = fma(-l31, x3, fma(-l21, x2, y1 * i1)),
+                 x0 = fma(-l30, x3, fma(-l20, x2, fma(-l10, x1, y0 * i0)));
+    const double inv = tj == 0 ? x0 : (tj == 1 ? x1 : (tj == 2 ? x2 : x3));
+    // ---- per block row L > J (the next diagonal tile's row first): X_L = S_JJ^-1 S(J, L), then
+    //      S(L, I) -= X_L' S(J, I) for I >= L; X_L lives only for its row
+#pragma unroll
+    for (int L = J + 1; L < NT; ++L) {
+      const double x = -__builtin_amdgcn_mfma_f64_4x4x4f64(inv, T[jj + (L - J)], 0.0, 0, 0, 0);
+#pragma unroll
+      for (int I = L; I < NT; ++I) {
+        double& t = T[L * NT - L * (L - 1) / 2 + (I - L)];
+        t = __builtin_amdgcn_mfma_f64_4x4x4f64(x, T[jj + (I - J)], t, 0, 0, 0);
+      }
     }
   }
-  double diag = 0.0;  // A(k, k) of lane k = r'D^-1 r - u'B^-1 u
-#pragma unroll
-  for (int i = 0; i < KB; ++i)
-    if (i == K) diag = col[i];
-  const double quad = readlane_d(diag, K);
-  const double logdet_d = sum_parts(l4);
   const double logdet_b = log(pb) + eb * kLn2;
   double ll = -0.5 * (quad + (logdet_d + logdet_b) + inf.n * kLog2Pi);  // log_mvnpdf_low_rank.m:30-32
   if (bad || !(fabs(ll) < INFINITY)) {
     ll = NAN;
-    if (lane == 0) atomicOr(a.status, 1);
-  }
-  emit(ll);
-}
-
-// 2-D block-cyclic form of the same augmented LDL^T for the larger ranks (k + 1 <= 8 NS, NS =
-// ceil((KMAX + 1) / 8)): one wave per sample, lane (ra, cb) = (lane >> 3, lane & 7) holds
-// A(ra + 8r, cb + 8c) for the register slots r >= c -- every lower-triangle entry exactly once,
-// plus upper entries in the diagonal slots that are never read.  At pivot p the 8 lanes of
-// column class p & 7 publish column p (rows > p; rows <= p as zeros) to a 64-double LDS line;
-// every lane reads its row and column multipliers from that line (8 distinct addresses per read,
-// consecutive doubles: conflict-free) and updates its live slots r >= c >= p / 8.  Slot blocks
-// left of the pivot are skipped at compile time, so a lane issues ~Σ_p (NS - p/8)(NS - p/8 + 1)/2
-// FMAs (666 at k = 50) where the lane-per-column form issues Σ_p (KB - 1 - p) (1,325), and all 64
-// lanes hold live entries until the last column block.
-template <int KMAX>
-__global__ __launch_bounds__(256) void ldl_cyc_kernel(LdlArgs a) {
-  constexpr int NS = (KMAX + 1 + 7) / 8;
-  constexpr int N8 = 8 * NS;
-  constexpr int kStage = KMAX * (KMAX + 1) / 2 + KMAX;  // packed Gram + u of the largest rank
-  __shared__ __attribute__((aligned(16))) double colp_all[4][2][N8];  // double-buffered by pivot parity
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-#if !GPDLA_LDL_GATHER
-  __shared__ __attribute__((aligned(16))) double stage_all[4][kStage];
-  double* stage = stage_all[wave];
-#else
-  (void)kStage;
-#endif
-  const int sl = blockIdx.x * 4 + wave;
-  if (sl >= a.sc) return;  // wave-uniform
-  const int K = a.k;
-  const int64_t s = a.s0 + sl;
-  const SpecInfo inf = a.info[a.q];
-  auto emit = [&](double ll) {
-    if (lane != 0) return;
-    if (s == a.S) *a.ll_null = ll;
-    else if (a.sample_ll) a.sample_ll[a.perm[s]] = ll;
-  };
-  if (inf.J == 0) {
-    emit(NAN);
-    return;
-  }
-  const int64_t E = (int64_t)K * (K + 1) / 2;
-  const double* Gs = a.G + (int64_t)sl * E;
-  const double* Us = a.U + (int64_t)sl * K;
-  const double* q = a.q1p + (int64_t)sl * kWeightParts;
-  const double* l4 = a.ldp + (int64_t)sl * kWeightParts;
-#if GPDLA_LDL_GATHER
-  auto entry = [&](int64_t t) { return t < E ? Gs[t] : Us[t - E]; };
-#else
-  {  // coalesced copy of the packed Gram and u into this wave's LDS slice (all loads in flight first)
-    constexpr int kIt = (kStage + 63) / 64;
-    double tmp[kIt];
-#pragma unroll
-    for (int it = 0; it < kIt; ++it) {
-      const int t = it * 64 + lane;
-      tmp[it] = t < E ? Gs[t] : (t < E + K ? Us[t - E] : 0.0);
-    }
-#pragma unroll
-    for (int it = 0; it < kIt; ++it) {
-      const int t = it * 64 + lane;
-      if (t < E + K) stage[t] = tmp[it];
-    }
-  }
-  __builtin_amdgcn_wave_barrier();
-  auto entry = [&](int64_t t) { return stage[t]; };
-#endif
-  const int ra = lane >> 3, cb = lane & 7;
-  double A[NS][NS];
-#pragma unroll
-  for (int r = 0; r < NS; ++r) {
-#pragma unroll
-    for (int c = 0; c <= r; ++c) {
-      const int i = ra + 8 * r, j = cb + 8 * c;
-      double v = 0.0;
-      if (i <= K && j <= K && i >= j) {
-        if (i < K) v = entry(j * K - j * (j - 1) / 2 + (i - j)) + (i == j ? 1.0 : 0.0);  // B = I + Gram
-        else if (j < K) v = entry(E + j);                                                  // row k: u'
-        else v = sum_parts(q);                                                             // sum r^2 / d
-      }
-      A[r][c] = v;
-    }
-  }
-  double pb = 1.0;  // prod D_p = pb 2^eb (frexp-renormalised, one log at the end)
-  int eb = 0;
-  bool bad = false;
-  // column blocks unrolled (register slots compile-time per block), the 8 pivots of a block not
-#pragma unroll
-  for (int c0 = 0; c0 < NS; ++c0) {
-#pragma unroll 1
-    for (int pp = 0; pp < 8; ++pp) {
-      const int p = 8 * c0 + pp;
-      if (p >= K) break;
-      double* colp = colp_all[wave][p & 1];
-      if (cb == pp) {  // column p: rows ra + 8r, r >= c0; rows <= p published as zeros
-#pragma unroll
-        for (int r = c0; r < NS; ++r) colp[ra + 8 * r] = (r > c0 || ra + 8 * r > p) ? A[r][c0] : 0.0;
-      }
-      __builtin_amdgcn_wave_barrier();
-      const double d = readlane_d(A[c0][c0], (pp << 3) | pp);  // A(p, p)
-      bad |= !(d > 0.0);
-      pb *= d;
-      if ((p & 3) == 3) {
-        int ex;
-        pb = frexp(pb, &ex);
-        eb += ex;
-      }
-      const double invd = rcp_nr(d);
-      double R[NS], F[NS];
-#pragma unroll
-      for (int r = c0; r < NS; ++r) {
-        R[r] = colp[ra + 8 * r];          // A(i, p), zero for i <= p
-        F[r] = colp[cb + 8 * r] * invd;   // A(j, p) / D_p, zero for j <= p
-      }
-#pragma unroll
-      for (int r = c0; r < NS; ++r) {
-#pragma unroll
-        for (int c = c0; c <= r; ++c) A[r][c] = fma(-R[r], F[c], A[r][c]);  // A(i,j) -= A(i,p) A(j,p) / D_p
-      }
-    }
-  }
-  double diag = 0.0;  // A(k, k) = r'D^-1 r - u'B^-1 u, at lane (k & 7, k & 7), slot (k / 8, k / 8)
-#pragma unroll
-  for (int r = 0; r < NS; ++r)
-    if (r == (K >> 3)) diag = A[r][r];
-  const double quad = readlane_d(diag, ((K & 7) << 3) | (K & 7));
-  const double logdet_d = sum_parts(l4);
-  const double logdet_b = log(pb) + eb * kLn2;
-  double ll = -0.5 * (quad + (logdet_d + logdet_b) + inf.n * kLog2Pi);  // log_mvnpdf_low_rank.m:30-32
-  if (bad || !(fabs(ll) < INFINITY)) {
-    ll = NAN;
-    if (lane == 0) atomicOr(a.status, 1);
+    if (write) atomicOr(a.status, 1);
   }
   emit(ll);
 }
@@ -459,28 +297,15 @@ hipError_t launch_weights(const WeightsArgs& a, hipStream_t s) {
 
 hipError_t launch_ldl_batch(const LdlArgs& a, hipStream_t s) {
   if (a.k < 1 || a.k > kGemmMaxK) return hipErrorInvalidValue;
-  const dim3 grid((unsigned)((a.sc + 3) / 4)), blk(256);
-#if GPDLA_LDL_CYCLIC
-  // 2-D block-cyclic register path for k >= 32 (configs[4]: k = 50)
-  if (a.k >= 32 && a.k <= 63) {
-    if (a.k <= 39) hipLaunchKernelGGL(ldl_cyc_kernel<39>, grid, blk, 0, s, a);
-    else if (a.k <= 47) hipLaunchKernelGGL(ldl_cyc_kernel<47>, grid, blk, 0, s, a);
-    else if (a.k <= 51) hipLaunchKernelGGL(ldl_cyc_kernel<51>, grid, blk, 0, s, a);
-    else if (a.k <= 55) hipLaunchKernelGGL(ldl_cyc_kernel<55>, grid, blk, 0, s, a);
-    else hipLaunchKernelGGL(ldl_cyc_kernel<63>, grid, blk, 0, s, a);
-    return hipGetLastError();
+  // matrix-core LDL^T: 16 samples per block, NT = ceil((k + 1) / 4) tiles per side
+  const dim3 grid((unsigned)((a.sc + 15) / 16)), blk(256);
+  switch ((a.k + 1 + 3) / 4) {
+#define NT_CASE(n) case n: hipLaunchKernelGGL(ldl_mfma_kernel<n>, grid, blk, 0, s, a); break;
+    NT_CASE(1) NT_CASE(2) NT_CASE(3) NT_CASE(4) NT_CASE(5) NT_CASE(6) NT_CASE(7) NT_CASE(8) NT_CASE(9)
+    NT_CASE(10) NT_CASE(11) NT_CASE(12) NT_CASE(13) NT_CASE(14) NT_CASE(15) NT_CASE(16) NT_CASE(17)
+#undef NT_CASE
+    default: return hipErrorInvalidValue;
   }
-#endif
-#if GPDLA_LDL_REGISTERS
-  // register path: column j of the augmented (k+1) x (k+1) matrix in lane j (k <= 63)
-  if (a.k <= 15) hipLaunchKernelGGL(ldl_reg_kernel<16>, grid, blk, 0, s, a);
-  else if (a.k <= 31) hipLaunchKernelGGL(ldl_reg_kernel<32>, grid, blk, 0, s, a);
-  else if (a.k <= 47) hipLaunchKernelGGL(ldl_reg_kernel<48>, grid, blk, 0, s, a);
-  else if (a.k <= 51) hipLaunchKernelGGL(ldl_reg_kernel<52>, grid, blk, 0, s, a);   // configs[4]: k = 50
-  else if (a.k <= 63) hipLaunchKernelGGL(ldl_reg_kernel<64>, grid, blk, 0, s, a);
-  else
-#endif
-    hipLaunchKernelGGL(ldl_batch_kernel, grid, blk, 0, s, a);
   return hipGetLastError();
 }
 

@@ -157,7 +157,7 @@ struct LdlArgs {
   const SpecInfo* info;
   int32_t q;
   int32_t k;
-  const double* G;               // [sc][k(k+1)/2] Gram, row-major upper triangle per sample
+  const double* G;               // [sc][k(k+1)/2] Gram per sample, entries in gram_tile_index order
   const double* U;               // [sc][k]
   const double* q1p;
   const double* ldp;
@@ -255,6 +255,24 @@ struct LikelihoodI8Args {
 __host__ __device__ inline int64_t i8_gemm_kstride(int64_t slot_cap) {
   return 64 * ((slot_cap - 16 + 63 + 63) / 64);  // >= lpix + 63 >= 4 Ls16 (slot_cap = 4 ceil(lpix/4) + 16)
 }
+// Order of the k(k+1)/2 Gram entries (r <= c < k) in the panel-GEMM path's Khatri-Rao rows and
+// Gram arrays: tile-major over the 4 x 4 tiles the LDL^T factors (gemm_path.hip ldl_mfma_kernel), so
+// the 16 lanes reading one tile of a sample read 128 contiguous bytes.  With NT = ceil((k+1)/4) tiles
+// per side, the first 4 (NT - 1) columns form whole tile columns: tiles (L, I), L <= I <= NT - 2,
+// row-block major, 10 entries (upper triangle, i <= j) on the diagonal and 16 (i-major) off it.  The
+// w = k - 4 (NT - 1) <= 3 Gram columns of the last tile column follow: 4 w entries per tile (L, NT-1),
+// L < NT - 1, then the w (w + 1) / 2 of the corner tile.
+__host__ __device__ inline int gram_tile_index(int r, int c, int k) {
+  const int NT = (k + 4) / 4, Kf = 4 * (NT - 1), w = k - Kf;
+  const int L = r >> 2, I = c >> 2, i = r & 3, j = c & 3;
+  if (c < Kf) {
+    const int row = 10 * L + 16 * (L * (NT - 2) - L * (L - 1) / 2);
+    return row + (I == L ? i * 4 - i * (i - 1) / 2 + (j - i) : 10 + 16 * (I - L - 1) + 4 * i + j);
+  }
+  const int base2 = 10 * (NT - 1) + 8 * (NT - 1) * (NT - 2);
+  return base2 + L * 4 * w + (L == NT - 1 ? i * w - i * (i - 1) / 2 + (j - i) : i * w + j);
+}
+
 __host__ __device__ inline int i8_gemm_entries(int k) {
   return 64 * ((k * (k + 1) / 2 + 63) / 64) + 64 * ((k + 63) / 64);
 }

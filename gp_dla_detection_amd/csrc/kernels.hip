@@ -100,7 +100,7 @@ __global__ __launch_bounds__(256) void prep_kernel(PrepArgs a) {
     const int64_t first = m > 0 ? (int64_t)m + 2 * kWidth : 0;
     for (int64_t i = first + tid; i < cap + 8; i += 256) lam_pad[i] = last;
   }
-  if (tid == 0) {
+  if (tid == 0 && blockIdx.y == 0) {
     SpecInfo inf;
     inf.J = J;
     inf.L = L;
@@ -116,14 +116,15 @@ __global__ __launch_bounds__(256) void prep_kernel(PrepArgs a) {
   }
   __syncthreads();
 
-  // pass 3: panel rows, one wave per slot, lanes over entries
+  // pass 3: panel rows, one wave per slot, lanes over entries.  gridDim.y blocks share a spectrum's
+  // slots (passes 1-2 above are repeated by each of them and write identical values)
   const int lane = tid & 63, wave = tid >> 6;
   const double* rest_g = a.rest;
   const int G = a.num_rest;
   // Slot j holds segment gg = j / Ls, step t = j % Ls, i.e. pixel-order position gg L + t; the
   // steps t >= L that round each segment up to whole chunks are neutral rows (like masked pixels).
   const int Ls = L > 0 ? ((L + kChunkSteps - 1) / kChunkSteps) * kChunkSteps : kChunkSteps;
-  for (int64_t j = wave; j < cap; j += 4) {
+  for (int64_t j = wave + 4 * (int64_t)blockIdx.y; j < cap; j += 4 * (int64_t)gridDim.y) {
     const int gg = (int)(j / Ls), t = (int)(j - (int64_t)gg * Ls);
     const int pos = (gg < 4 && t < L) ? gg * L + t : -1;
     const int pix = (pos >= 0 && pos < J) ? smap[pos] : -1;
@@ -192,16 +193,14 @@ __global__ __launch_bounds__(256) void prep_kernel(PrepArgs a) {
         if (t2 >= Lay::kTiles && !((jj == 0 || jj == 1 || jj == 2) && t2 < Lay::kTiles + 2)) row[w] = 0.0;
       }
     } else {
-      // panel-GEMM layout: Khatri-Rao row (row-major upper triangle, (r, c) at r KK - r(r-1)/2 +
-      // c - r), M row, and 8 slot scalars; all zero / neutral for masked and padding slots
+      // panel-GEMM layout: Khatri-Rao row (entry (r, c) at gram_tile_index(r, c), internal.h), M
+      // row, and 8 slot scalars; all zero / neutral for masked and padding slots
       const int64_t E = (int64_t)KK * (KK + 1) / 2;
       double* pg = a.panel + (sb + j) * E;
       double* pm = a.panel_m + (sb + j) * KK;
-      int start = 0;
       for (int r = 0; r < KK; ++r) {
         const double mr = pix >= 0 ? Mi(r) : 0.0;
-        for (int c = r + lane; c < KK; c += 64) pg[start + (c - r)] = pix >= 0 ? mr * Mi(c) : 0.0;
-        start += KK - r;
+        for (int c = r + lane; c < KK; c += 64) pg[gram_tile_index(r, c, KK)] = pix >= 0 ? mr * Mi(c) : 0.0;
       }
       for (int c = lane; c < KK; c += 64) pm[c] = pix >= 0 ? Mi(c) : 0.0;
       if (lane == 0) {
@@ -253,7 +252,7 @@ __device__ inline void stage_chunk(const double* __restrict__ panel, int Ls, int
 }
 
 template <int K, int NL>
-__global__ __launch_bounds__(256, (K <= 20 ? GPDLA_WAVES_PER_EU : 1)) void likelihood_kernel(LikelihoodArgs a) {
+__global__ __launch_bounds__(256, (K <= 20 ? 2 : 1)) void likelihood_kernel(LikelihoodArgs a) {
   using Lay = Layout<K>;
   constexpr int kTiles = Lay::kTiles;
   constexpr int kGT = Lay::kGT;
@@ -262,13 +261,11 @@ __global__ __launch_bounds__(256, (K <= 20 ? GPDLA_WAVES_PER_EU : 1)) void likel
   constexpr int kBuf = 4 * kChunkSteps * kRowS;
   static_assert(kWavesPerBlock == 4, "stage_chunk: one wave per segment");
   constexpr int kWingLds = 4 * ((3 * kWingStride + 3) / 4);
-  constexpr int kFarLds = 4 * ((3 * kFarStride + 3) / 4);
-  constexpr int kCoreLds = NL == 3 ? 3 * kCoreTable + kWingLds + 64 + kFarLds : 1;
+  constexpr int kCoreLds = NL == 3 ? 3 * kCoreTable + kWingLds + 64 : 1;
   __shared__ __attribute__((aligned(16))) double lds[2 * kBuf + kCoreLds];
   double* core_lds = lds + 2 * kBuf;
   double* wing_lds = core_lds + 3 * kCoreTable;
   double* exp_lds = wing_lds + kWingLds;
-  double* far_lds = exp_lds + 64;
 
   // XCD-aware block order: the dispatcher deals consecutive blocks round-robin over the 8 XCDs,
   // so block b runs on XCD b % 8.  Virtual index v gives each XCD one contiguous eighth of the
@@ -304,7 +301,6 @@ __global__ __launch_bounds__(256, (K <= 20 ? GPDLA_WAVES_PER_EU : 1)) void likel
     for (int i = threadIdx.x; i < 3 * kCoreTable; i += 256) core_lds[i] = a.lines.buf[i];
     if (threadIdx.x < 64) exp_lds[threadIdx.x] = a.lines.buf[kLineBufExp2 + threadIdx.x];
     if (threadIdx.x < 3 * kWingStride) wing_lds[threadIdx.x] = a.lines.buf[kLineBufWing + threadIdx.x];
-    if (threadIdx.x < 3 * kFarStride) far_lds[threadIdx.x] = a.lines.buf[kLineBufFar + threadIdx.x];
   }
 
   // ---- per-lane sample constants (MFMA A-operand layout: sample = lane & 15, segment = lane >> 4)
@@ -346,7 +342,6 @@ __global__ __launch_bounds__(256, (K <= 20 ? GPDLA_WAVES_PER_EU : 1)) void likel
     double* cur = lds + (c & 1) * kBuf;
     if (c + 1 < nchunks)
       stage_chunk<K>(panel, Ls, c + 1, lds_base + (uint32_t)(((c + 1) & 1) * kBuf * 8), wave_s, voff);
-#if GPDLA_BATCHED_PROFILE
     // raw profiles of the chunk's 4 steps first: branch-free damping wings (one basic block, so
     // the 4 chains interleave), a rare core fix-up for lanes with |x| < kCoreX (raw_profile3's
     // order: bit-identical), then the 4 table exps
@@ -359,7 +354,6 @@ __global__ __launch_bounds__(256, (K <= 20 ? GPDLA_WAVES_PER_EU : 1)) void likel
         lamc[tt] = cur[(tt * 4 + g) * kRowS + Lay::kLam];
         tot[tt] = 0.0;
       }
-#if GPDLA_SHARED_RCP
       double Tj[3][kChunkSteps];
 #pragma unroll
       for (int tt = 0; tt < kChunkSteps; ++tt) {
@@ -368,22 +362,6 @@ __global__ __launch_bounds__(256, (K <= 20 ? GPDLA_WAVES_PER_EU : 1)) void likel
         cm |= (((fabs(x0) < kCoreX) | (fabs(x1) < kCoreX) | (fabs(x2) < kCoreX)) ? 1u : 0u) << tt;
         wing_T3(x0, x1, x2, Tj[0][tt], Tj[1][tt], Tj[2][tt]);
       }
-#endif
-#if GPDLA_SHARED_RCP && GPDLA_FAR_WING
-      // a wave whose 4 steps are all >= kFarX from every line centre (most chunks) takes the
-      // degree-4 far-wing polynomials (NaN T of core lanes fails the test)
-      bool ok = true;
-#pragma unroll
-      for (int tt = 0; tt < kChunkSteps; ++tt)
-        ok = ok && (Tj[0][tt] <= kFarT) && (Tj[1][tt] <= kFarT) && (Tj[2][tt] <= kFarT);
-      if (__all(ok)) {
-#pragma unroll
-        for (int j = 0; j < 3; ++j) {
-#pragma unroll
-          for (int tt = 0; tt < kChunkSteps; ++tt) tot[tt] -= far_poly(far_lds + j * kFarStride, Tj[j][tt]);
-        }
-      } else
-#endif
       // line-outer order (same per-step summation order): one line's 9 coefficients live at a
       // time, re-read from LDS per line (opaque zero offset) rather than hoisted
 #pragma unroll
@@ -393,13 +371,7 @@ __global__ __launch_bounds__(256, (K <= 20 ? GPDLA_WAVES_PER_EU : 1)) void likel
         const double* wl = wing_lds + zoff + j * kWingStride;
 #pragma unroll
         for (int tt = 0; tt < kChunkSteps; ++tt) {
-#if GPDLA_SHARED_RCP
           tot[tt] -= wing_poly(wl, Tj[j][tt]);
-#else
-          const double x = fma(lamc[tt], afac[j], -kC2);
-          cm |= (fabs(x) < kCoreX ? 1u : 0u) << tt;
-          tot[tt] -= wing_eval(wl, x);
-#endif
         }
       }
       if (cm) {
@@ -421,14 +393,9 @@ __global__ __launch_bounds__(256, (K <= 20 ? GPDLA_WAVES_PER_EU : 1)) void likel
       }
 #pragma unroll
       for (int tt = 0; tt < kChunkSteps; ++tt) {
-#if GPDLA_FAST_EXP
         rwv[tt] = exp_tab64(N * tot[tt], exp_lds);
-#else
-        rwv[tt] = exp(N * tot[tt]);
-#endif
       }
     }
-#endif
 #pragma unroll
     for (int tt = 0; tt < kChunkSteps; ++tt) {
       const double* row = cur + (tt * 4 + g) * kRowS;
@@ -441,9 +408,6 @@ __global__ __launch_bounds__(256, (K <= 20 ? GPDLA_WAVES_PER_EU : 1)) void likel
         lam = row[Lay::kLam]; y = row[Lay::kY]; noise = row[Lay::kNoise];
         mu = row[Lay::kMu]; om2 = row[Lay::kOmega2];
       }
-      // Per-step opaque zero: the wing coefficients are re-read from LDS (broadcast) every step
-      // instead of being hoisted into registers for the whole chunk.
-#if GPDLA_BATCHED_PROFILE
       double w6;
       if constexpr (NL == 3) {
         w6 = rwv[tt];
@@ -451,11 +415,6 @@ __global__ __launch_bounds__(256, (K <= 20 ? GPDLA_WAVES_PER_EU : 1)) void likel
       } else {
         w6 = raw(lam, wing_lds);
       }
-#else
-      int zoff;
-      asm volatile("s_mov_b32 %0, 0" : "=s"(zoff));
-      const double w6 = raw(lam, wing_lds + zoff);
-#endif
       // instrumental broadening, voigt.c:297-299 (zero-initialised accumulator, taps in order)
       double ab = w0 * kInstrumentProfile[0];
       ab = fma(w1, kInstrumentProfile[1], ab);
@@ -477,9 +436,7 @@ __global__ __launch_bounds__(256, (K <= 20 ? GPDLA_WAVES_PER_EU : 1)) void likel
       const double wu = ab * rd;
       q1 = fma(r, rd, q1);
       pm *= d;
-#if GPDLA_SCHED_FENCE
       __builtin_amdgcn_sched_barrier(0);
-#endif
       // B operands: tile t, entry 4t + (lane & 3) of this lane's segment row
       const double* brow = row + (lane & 3) * kJS;
 #pragma unroll
@@ -680,7 +637,9 @@ __global__ __launch_bounds__(256) void mvn_single_kernel(const double* __restric
 
 template <int K>
 hipError_t launch_prep_k(const PrepArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(prep_kernel<K>, dim3(a.q_count), dim3(256), 0, s, a);
+  // the panel-GEMM layout (K == 0) writes k(k+1)/2 doubles per slot for few spectra per batch:
+  // spread each spectrum's slots over 16 blocks
+  hipLaunchKernelGGL(prep_kernel<K>, dim3(a.q_count, K == 0 ? 16 : 1), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 

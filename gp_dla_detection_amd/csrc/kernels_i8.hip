@@ -21,10 +21,7 @@ namespace gpdla {
 
 namespace {
 
-constexpr int kI8Levels = 4;
-#ifndef I8_PIPELINE
-#define I8_PIPELINE 1
-#endif  // digit levels i + j = 0..3 kept (10 of the 16 pairs)
+constexpr int kI8Levels = 4;  // digit levels i + j = 0..3 kept (10 of the 16 pairs)
 
 // ---------------------------------------------------------------------------------------------
 // convert: fp64 fused panel (prep_kernel<K>) -> int8 digit planes + slot records + entry scales.
@@ -157,11 +154,7 @@ template <int K>
 __global__ __launch_bounds__(256, 1) void likelihood_i8_kernel(LikelihoodI8Args a) {
   using F = Layout<K>;
   using I = I8Layout<K>;
-#ifdef I8_NT_OVERRIDE
-  constexpr int NT = I8_NT_OVERRIDE;
-#else
   constexpr int NT = I::kTiles;
-#endif
   constexpr int kWingLds = 4 * ((3 * kWingStride + 3) / 4);
   constexpr int kSBuf = I::kChunkSlots * I::kScal;  // doubles per slot-record buffer
   __shared__ __attribute__((aligned(16))) uint8_t ldsb[2 * I::kChunkBytes];
@@ -211,7 +204,6 @@ __global__ __launch_bounds__(256, 1) void likelihood_i8_kernel(LikelihoodI8Args 
     stage_rec(c, buf);
   };
 
-#if I8_PIPELINE
   // software pipeline: iteration c computes chunk c's weights while its MFMAs contract chunk c-1
   // (digits kept from the previous iteration, B planes in buffer (c-1)&1; B(c) is staged into
   // buffer c&1 during iteration c).  Iteration 0 contracts an all-zero "chunk -1" (buffer 1).
@@ -219,9 +211,6 @@ __global__ __launch_bounds__(256, 1) void likelihood_i8_kernel(LikelihoodI8Args 
   stage_rec(0, 0);
   for (int i = threadIdx.x; i < I::kChunkBytes / 16; i += 256)
     reinterpret_cast<uint4*>(ldsb + I::kChunkBytes)[i] = make_uint4(0u, 0u, 0u, 0u);
-#else
-  stage(0, 0);
-#endif
   for (int i = threadIdx.x; i < 3 * kCoreTable; i += 256) core_lds[i] = a.lines.buf[i];
   if (threadIdx.x < 64) exp_lds[threadIdx.x] = a.lines.buf[kLineBufExp2 + threadIdx.x];
   if (threadIdx.x < 3 * kWingStride) wing_lds[threadIdx.x] = a.lines.buf[kLineBufWing + threadIdx.x];
@@ -258,14 +247,11 @@ __global__ __launch_bounds__(256, 1) void likelihood_i8_kernel(LikelihoodI8Args 
   double q1 = 0.0, pm = 1.0;
   int pe = 0;
 
-#if I8_PIPELINE
   v4i Apg[4], Apu[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) Apg[i] = Apu[i] = (v4i){0, 0, 0, 0};
-#endif
   for (int c = 0; c < nch; ++c) {
     const int cur = c & 1;
-#if I8_PIPELINE
     if (c + 1 < nch) stage_rec(c + 1, cur ^ 1);
     stage_b(c, cur);
     const uint8_t* bp = ldsb + (cur ^ 1) * I::kChunkBytes;  // B planes of chunk c - 1
@@ -276,16 +262,12 @@ __global__ __launch_bounds__(256, 1) void likelihood_i8_kernel(LikelihoodI8Args 
       for (int j = 0; j < 4; ++j) Bt[j] = *reinterpret_cast<const v4i*>(bp + j * I::kPlaneBytes + boff);
     };
     v4i Bq[4];
-#else
-    if (c + 1 < nch) stage(c + 1, cur ^ 1);
-#endif
     // ---- weights of this lane's 16 slots (fp64), quantised to X_A + 2^31, digits XOR 0x80
     const double* rec = ldss + cur * kSBuf + (16 * g) * I::kScal;
     // (1) line sums of the 16 slots, branch-free damping wings (one basic block: the scheduler
     //     interleaves the 16 independent chains), coefficients in SGPRs (uniform global loads)
     double tot[16];
     uint32_t cm = 0;
-#if GPDLA_SHARED_RCP && GPDLA_I8_FAR_WING
     // |x| is monotone over a lane's 16 consecutive slots: test the two ends against kFarX; a wave
     // entirely in the far wings of all three lines (most chunks) takes the degree-4 polynomials
     bool far_ok = true;
@@ -311,12 +293,10 @@ __global__ __launch_bounds__(256, 1) void likelihood_i8_kernel(LikelihoodI8Args 
         tot[e] = t;
       }
     } else
-#endif
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
       const double lam = rec[e * I::kScal];
       double t = 0.0;
-#if GPDLA_SHARED_RCP
       const double x0 = fma(lam, afac[0], -kC2), x1 = fma(lam, afac[1], -kC2), x2 = fma(lam, afac[2], -kC2);
       cm |= (((fabs(x0) < kCoreX) | (fabs(x1) < kCoreX) | (fabs(x2) < kCoreX)) ? 1u : 0u) << e;
       double T0, T1, T2;
@@ -324,14 +304,6 @@ __global__ __launch_bounds__(256, 1) void likelihood_i8_kernel(LikelihoodI8Args 
       t -= wing_poly(wing_g, T0);
       t -= wing_poly(wing_g + kWingStride, T1);
       t -= wing_poly(wing_g + 2 * kWingStride, T2);
-#else
-#pragma unroll
-      for (int j = 0; j < 3; ++j) {
-        const double x = fma(lam, afac[j], -kC2);
-        cm |= (fabs(x) < kCoreX ? 1u : 0u) << e;
-        t -= wing_eval(wing_g + j * kWingStride, x);
-      }
-#endif
       tot[e] = t;
     }
     // (2) rare fix-up (z-sorted samples: a few % of wave-chunks): the core polynomial for the
@@ -358,11 +330,7 @@ __global__ __launch_bounds__(256, 1) void likelihood_i8_kernel(LikelihoodI8Args 
     double rw[16];
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
-#if GPDLA_FAST_EXP
       rw[e] = exp_tab64(N * tot[e], exp_lds);  // voigt.c:291
-#else
-      rw[e] = exp(N * tot[e]);
-#endif
     }
     // (4) 7-tap convolution, pixel terms, weights; slot records prefetched one slot ahead
     uint32_t xg[16], xu[16];
@@ -370,12 +338,9 @@ __global__ __launch_bounds__(256, 1) void likelihood_i8_kernel(LikelihoodI8Args 
     double2 n23 = *reinterpret_cast<const double2*>(rec + 2);
     double2 n45 = *reinterpret_cast<const double2*>(rec + 4);
     double nus = rec[6];
-#if I8_PIPELINE
     load_bp(0, Bq);
-#endif
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
-#if I8_PIPELINE
       {  // tile e of chunk c - 1 (its 10 MFMAs run beside this slot's VALU work)
         const v4i B0 = Bq[0], B1 = Bq[1], B2 = Bq[2], B3 = Bq[3];
         if (e + 1 < 16) load_bp(e + 1, Bq);
@@ -391,7 +356,6 @@ __global__ __launch_bounds__(256, 1) void likelihood_i8_kernel(LikelihoodI8Args 
         acc[3][e] = MFMA_I8(A[2], B1, acc[3][e]);
         acc[3][e] = MFMA_I8(A[3], B0, acc[3][e]);
       }
-#endif
       const double y = n01.y, noise = n23.x, mu = n23.y, om2 = n45.x, gs = n45.y, us = nus;
       if (e + 1 < 16) {
         n01 = *reinterpret_cast<const double2*>(rec + (e + 1) * I::kScal);
@@ -425,7 +389,6 @@ __global__ __launch_bounds__(256, 1) void likelihood_i8_kernel(LikelihoodI8Args 
       pm = frexp(pm, &ex);
       pe += ex;
     }
-#if I8_PIPELINE
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       Apg[i] = digit_plane(xg, i);
@@ -439,15 +402,6 @@ __global__ __launch_bounds__(256, 1) void likelihood_i8_kernel(LikelihoodI8Args 
     const v4i* Ag = Apg;
     const v4i* Au = Apu;
     const uint8_t* bb = ldsb + ((nch - 1) & 1) * I::kChunkBytes;
-#else
-    v4i Ag[4], Au[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      Ag[i] = digit_plane(xg, i);
-      Au[i] = digit_plane(xu, i);
-    }
-    const uint8_t* bb = ldsb + cur * I::kChunkBytes;
-#endif
     // ---- exact int8 contraction: the 10 digit pairs of level i + j <= 3 per tile
     auto load_b = [&](int t, v4i (&Bt)[4]) {
       const int ent = 16 * t + (lane & 15);
@@ -476,10 +430,6 @@ __global__ __launch_bounds__(256, 1) void likelihood_i8_kernel(LikelihoodI8Args 
       acc[3][t] = MFMA_I8(A[3], B0, acc[3][t]);
       __builtin_amdgcn_sched_barrier(0);  // keep one tile's B digits live at a time
     }
-#if !I8_PIPELINE
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA for chunk c+1 landed
-    __syncthreads();                                   // ... and everyone's; buffer c free again
-#endif
   }
 
   // ---- combine the 4 segments of each sample (lanes l, l^16, l^32, l^48)

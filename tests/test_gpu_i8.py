@@ -135,6 +135,26 @@ def test_i8_long_spectrum_batch_falls_back_to_fp64():
     assert out["num_pixels"][1] > 30000
 
 
+def test_panel_gemm_i8_long_spectrum_batch_falls_back_to_fp64():
+    """The same kI8MaxSlots guard on the int8 panel-GEMM path (gemm_i8.hip): the batch holding a
+    30,500-pixel spectrum runs the fp64 weights + dgemm + LDL^T, bit-identical to path='panel_gemm'."""
+    model = syn.make_model(k=20)
+    samples = syn.make_samples(64)
+    base = syn.make_spectrum(model, 1)
+    lo, hi = np.log10(base["wavelengths"][0]), np.log10(base["wavelengths"][-1])
+    lam = 10.0 ** np.linspace(lo, hi, 30500)
+    rng = np.random.default_rng(7)
+    long_spec = dict(wavelengths=lam, flux=np.interp(lam, base["wavelengths"], base["flux"]),
+                     noise_variance=rng.uniform(0.01, 0.09, lam.size), pixel_mask=np.zeros(lam.size, bool),
+                     z_qso=base["z_qso"])
+    packed = syn.pack_spectra([base, long_spec])
+    ref = _run(model, samples, packed, "panel_gemm")
+    out = _run(model, samples, packed, "panel_gemm_i8")
+    for key in KEYS:
+        np.testing.assert_array_equal(out[key], ref[key])
+    assert out["num_pixels"][1] > 30000
+
+
 # ------------------------------------------------------------ int8 panel-GEMM path (any rank)
 @pytest.mark.parametrize("k", [7, 20, 50])
 def test_panel_gemm_i8_equals_fp64(k):

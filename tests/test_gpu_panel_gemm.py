@@ -73,10 +73,11 @@ def test_rank50_matches_oracle():
         assert _rel_err(out["log_likelihoods_dla"][q], ref["log_likelihood_dla"]) < 1e-9
 
 
-@pytest.mark.parametrize("k", [31, 32, 39, 40, 47, 48, 51, 52, 55, 56, 63])
+@pytest.mark.parametrize("k", [1, 2, 3, 4, 7, 11, 15, 31, 32, 39, 40, 47, 48, 51, 52, 55, 56, 59, 63, 64])
 def test_high_rank_ldl_buckets_match_oracle(k):
-    """Every rank bucket of the batched LDL^T kernels around and above the block-cyclic switch at
-    k = 32 (buckets of ldl_cyc_kernel: k <= 39, 47, 51, 55, 63), fp64 and int8 panel paths."""
+    """The matrix-core LDL^T (ldl_mfma_kernel<NT>, NT = ceil((k + 1) / 4)) at the edges of its tile
+    buckets -- k + 1 a multiple of 4 (no identity padding) and one past it -- up to the largest
+    rank the ABI accepts (k = 64, NT = 17), fp64 and int8 panel paths."""
     model = syn.make_model(k=k, seed=100 + k)
     samples = syn.make_samples(40)
     spectra = syn.make_dr12q_like_spectra(model, 2, seed=200 + k, mask_fraction=0.05)
