@@ -50,58 +50,73 @@ def effective_bytes_per_eval(n: int, k: int, w: int = 8) -> float:
     return w * (n * (k + 5) + 8) + w
 
 
-def _cpu_worker(task):
-    """One host process: the oracle over its spectra's DLA samples (spectrum by spectrum, all
-    samples of each) until the time budget is spent."""
-    model, specs, offsets, nhis, budget_s = task
+def _numpy_worker(task):
+    """The numpy oracle on one host core (secondary CPU figure), until the time budget is spent."""
+    model, spec, offsets, nhis, budget_s = task
     from threadpoolctl import threadpool_limits
     from oracle import gpdla_oracle as O
     done = 0
     with threadpool_limits(limits=1):
         t0 = time.perf_counter()
-        for spec in specs:
-            prep = O.prepare_spectrum(spec["wavelengths"], spec["flux"], spec["noise_variance"],
-                                      spec["pixel_mask"], spec["z_qso"], model)
-            zs = prep["zmin"] + (prep["zmax"] - prep["zmin"]) * offsets
-            for z, N in zip(zs, nhis):
-                O.sample_log_likelihood(prep, z, N, 3)
-                done += 1
-                if time.perf_counter() - t0 >= budget_s:
-                    return done, time.perf_counter() - t0
+        prep = O.prepare_spectrum(spec["wavelengths"], spec["flux"], spec["noise_variance"],
+                                  spec["pixel_mask"], spec["z_qso"], model)
+        zs = prep["zmin"] + (prep["zmax"] - prep["zmin"]) * offsets
+        for z, N in zip(zs, nhis):
+            O.sample_log_likelihood(prep, z, N, 3)
+            done += 1
+            if time.perf_counter() - t0 >= budget_s:
+                break
         el = time.perf_counter() - t0
     return done, el
 
 
-def host_cores() -> int:
-    """Cores this process may use, capped at the GPU box's per-GPU CPU share (16)."""
-    try:
-        n = len(os.sched_getaffinity(0))
-    except AttributeError:
-        n = os.cpu_count() or 1
-    return max(1, min(16, n))
-
-
-def cpu_baseline(model, samples, spectra, budget_s: float) -> dict:
-    """The numpy oracle (MATLAB-order restatement of process_qsos.m:186-197) on the host cores,
-    parallel over spectra like the reference's per-worker parfor (one process per core, one BLAS
-    thread each), on a bounded sample of the bench workload: worker c sweeps every DLA sample of
-    spectra c, c + cores, ... in order until the time budget is spent.  Runs before the GPU is
-    initialised (spawned workers)."""
+def cpu_baseline(model, samples, spectra, budget_s: float, k: int) -> dict:
+    """The reference's CPU path, restated in C++ with OpenMP over the DLA samples like its parfor
+    (oracle/cpu_ref.cpp: process_qsos.m:184-198, voigt.c:253-304 with an own Faddeeva function in
+    place of libcerf, log_mvnpdf_low_rank.m:5-33 in MATLAB operation order), on the host threads
+    OpenMP is given (OMP_NUM_THREADS; the GPU box sets it to its 16-core per-GPU share).
+    configs[0] (one spectrum, the null model only) is timed in full; the bench workload on a
+    bounded subset: whole spectra (all S samples each), at least 16, until ``budget_s`` is spent.
+    The numpy restatement on one core is reported beside it.  Runs before the GPU is touched."""
     import multiprocessing as mp
-    cores = host_cores()
-    tasks = [(model, [spectra[i % len(spectra)] for i in range(c, c + 64 * cores, cores)],
-              samples["offset_samples"], samples["nhi_samples"], budget_s) for c in range(cores)]
+    from oracle import cpu_ref as CR
+    from oracle import gpdla_oracle as O
+    threads = CR.threads()
+    preps = []
+    # configs[0]: one spectrum, null-model log_mvnpdf_low_rank (process_qsos.m:150-152)
+    s0 = spectra[0]
+    p0 = O.prepare_spectrum(s0["wavelengths"], s0["flux"], s0["noise_variance"], s0["pixel_mask"], s0["z_qso"], model)
+    reps = 200
     t0 = time.perf_counter()
-    with mp.get_context("spawn").Pool(cores) as pool:
-        res = pool.map(_cpu_worker, tasks)
-    wall = time.perf_counter() - t0
-    done = sum(r[0] for r in res)
-    el = max(r[1] for r in res)
-    return {"value": done / el, "unit": "evals/s", "cores": cores, "kind": "port",
-            "sample": f"{done} (spectrum, DLA-sample) evaluations: {cores} host processes x 1 thread, "
-                      f"process c sweeping all samples of bench spectra c, c+{cores}, ... for {el:.1f} s (wall incl. start-up "
-                      f"{wall:.1f} s); numpy/scipy restatement of process_qsos.m:186-197 (MATLAB is not "
-                      "available); n=800, k=20, 3 lines"}
+    for _ in range(reps):
+        ll0 = CR.log_mvnpdf_low_rank(p0["y"], p0["mu"], p0["M"], p0["omega2"] + p0["noise"])
+    c1_us = (time.perf_counter() - t0) / reps * 1e6
+    # the bench workload: whole spectra until the budget is spent (>= 16)
+    off, nhi = samples["offset_samples"], samples["nhi_samples"]
+    done = nspec = 0
+    t0 = time.perf_counter()
+    for q in range(len(spectra)):
+        sp = spectra[q]
+        prep = O.prepare_spectrum(sp["wavelengths"], sp["flux"], sp["noise_variance"], sp["pixel_mask"],
+                                  sp["z_qso"], model)
+        out = CR.sample_lls(prep, off, nhi, 3, threads)
+        assert np.all(np.isfinite(out))
+        done += out.size
+        nspec += 1
+        if nspec >= 16 and time.perf_counter() - t0 >= budget_s:
+            break
+    el = time.perf_counter() - t0
+    # secondary: the numpy restatement, one process, one BLAS thread, 3 s
+    with mp.get_context("spawn").Pool(1) as pool:
+        nd, nel = pool.map(_numpy_worker, [(model, spectra[0], off, nhi, 3.0)])[0]
+    return {"value": done / el, "unit": "evals/s", "cores": threads, "kind": "port",
+            "sample": f"{done} (spectrum, DLA-sample) evaluations = {nspec} whole spectra x {off.size} samples of the "
+                      f"bench workload in {el:.1f} s; C++ OpenMP restatement of process_qsos.m:184-198 "
+                      f"(oracle/cpu_ref.cpp, MATLAB operation order, {threads} OpenMP threads = OMP_NUM_THREADS; "
+                      f"the host shows {os.cpu_count()} logical CPUs); MATLAB is not available; n=800, k={k}, 3 lines",
+            "configs0_null_eval_us": c1_us, "configs0_log_likelihood_no_dla": ll0,
+            "numpy_1core": {"value": nd / nel, "unit": "evals/s", "cores": 1,
+                            "sample": f"{nd} evaluations of spectrum 0 in {nel:.1f} s (oracle/gpdla_oracle.py)"}}
 
 
 # BASELINE.json configs (SURVEY.md 8d).  c2 is the bench line the driver records.
@@ -137,6 +152,38 @@ def profiled_traffic(Q: int, S: int, k: int, path: str = "fused"):
         if ent["kernel"].startswith("void gpdla::likelihood_kernel<20") and "hbm_bytes_per_launch" in ent:
             return ent["hbm_bytes_per_launch"], f"{PROFILE_SUMMARY.relative_to(ROOT)} (rocprofv3 PMC)"
     return None, None
+
+
+def timed_steps(step, synchronize, steps: int, dist=None) -> float:
+    """The bench contract's timed region: barrier + device sync on both sides of exactly ``steps``
+    steps, elapsed time max-reduced over the ranks (gloo, host-side)."""
+    synchronize()
+    if dist is not None:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    synchronize()  # device-side completion of every enqueued step
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        import torch
+        tt = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    return elapsed
+
+
+def dr12q_shard(pool_pixels, total: int, rank: int, world: int, split: bool):
+    """Pool indices of this rank's DR12Q-shaped spectra: spectrum i is pool entry i % len(pool).
+    configs[2] (``split`` False) keeps all on one GPU; configs[3] splits them by LPT on pixel
+    count (shard.py), so ranks get equal sweep work although n ranges over 270..1,250."""
+    from gp_dla_detection_amd.shard import lpt_shards
+    idx = np.arange(total) % len(pool_pixels)
+    if not split or world == 1:
+        return idx
+    return idx[lpt_shards(np.asarray(pool_pixels, dtype=np.float64)[idx], world)[rank]]
 
 
 class _stdout_to_stderr:
@@ -179,7 +226,6 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
     if world > 1:
-        import torch
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         with _stdout_to_stderr():  # gloo prints its connection banner on stdout (fd 1)
@@ -200,11 +246,11 @@ def main():
     if wl["dr12q"]:
         # full DR12Q count (162,861) of DR12Q-shaped spectra (n ~ 270-1250): a pool of 4096
         # distinct synthetic spectra tiled to the count; c3 = all on one GPU, c4 = split over ranks
-        total = wl["spectra"]
-        lo, hi = (0, total) if args.workload == "c3" else (total * rank // world, total * (rank + 1) // world)
-        Q = hi - lo
         pool = syn.make_dr12q_like_spectra(model, 4096, seed=12, mask_fraction=0.0)
-        spectra = [pool[i % len(pool)] for i in range(lo, hi)]
+        mine = dr12q_shard([p["wavelengths"].size for p in pool], wl["spectra"], rank, world,
+                           split=args.workload == "c4")
+        Q = mine.size
+        spectra = [pool[i] for i in mine]
     else:
         Q = wl["spectra"]
         spectra = [syn.make_spectrum(model, rank * Q + q) for q in range(Q)]
@@ -212,7 +258,7 @@ def main():
     # CPU baseline first, while no process has touched the GPU (its workers are spawned)
     cpu = None
     if rank == 0 and world == 1 and args.cpu_budget > 0:
-        cpu = cpu_baseline(model, samples, spectra, args.cpu_budget)
+        cpu = cpu_baseline(model, samples, spectra, args.cpu_budget, args.k)
     # one GPU per local rank; on a box with fewer GPUs than ranks (rehearsal) ranks share devices
     dev = local_rank % max(1, L.load().gpdla_device_count())
     D = lambda a: L.DeviceArray.from_numpy(a, device=dev)
@@ -244,20 +290,8 @@ def main():
         step()
     eng.synchronize()
     eng.reset_stats()
-    if world > 1:
-        dist.barrier()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    eng.synchronize()  # device-side completion of every enqueued step
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
+    elapsed = timed_steps(step, eng.synchronize, args.steps, dist if world > 1 else None)
     st = eng.stats()
-    if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
 
     # alternative path on the same resident inputs (1 GPU, configs[1]): the int8 Ozaki contraction
     # next to the fp64 line, with its measured deviation from the fp64 outputs.  Not `value`: the
@@ -302,7 +336,13 @@ def main():
     inv = np.exp(sll - (lld[:, None] + np.log(S))).sum(axis=1)
     ok = ok and bool(np.max(np.abs(inv - 1)) < 1e-10)
 
-    evals_total = world * Q * S * args.steps
+    q_total = Q
+    if world > 1:  # spectra over all ranks (LPT shards of configs[3] differ in size)
+        import torch
+        qt = torch.tensor([Q], dtype=torch.int64)
+        dist.all_reduce(qt, op=dist.ReduceOp.SUM)
+        q_total = int(qt.item())
+    evals_total = q_total * S * args.steps
     value = evals_total / elapsed
     n_mean = float(np.mean(npix))
     launches = max(st["likelihood_launches"], 1)

@@ -206,7 +206,7 @@ __device__ inline void dma_piece(const uint8_t* sbase, uint32_t voffset, uint32_
 constexpr int kGTileS = 128, kGTileE = 64;
 
 // --------------------------------------------------------------------------------------------
-// GEMM: grid (rows / 128 sample tiles, entries / 64 entry tiles), 4 waves; wave w owns samples
+// GEMM: 128-sample x 64-entry block tiles (1-D grid, XCD-aware order below), 4 waves; wave w owns samples
 // 32 w .. 32 w + 31 of the tile (2 row tiles) x all 64 entries (4 column tiles of
 // v_mfma_i32_16x16x64_i8, 10 digit pairs, int32 per level).  The weight digits (A) go
 // global -> VGPRs in the MFMA operand layout (each wave owns its 32 samples,
@@ -226,8 +226,16 @@ __global__ __launch_bounds__(256, 2) void gemm_i8_kernel(GemmI8Args a) {
   const int NE = i8_gemm_entries(K);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wave_s = __builtin_amdgcn_readfirstlane(wave);
-  const int s_tile = blockIdx.x * kGTileS;
-  const int e_tile = blockIdx.y * kGTileE;
+  // XCD-contiguous, entry-tile-fastest order: the dispatcher deals linear block b to XCD b % 8, so
+  // virtual index v gives each XCD a contiguous run of (sample tile, entry tile) pairs with the
+  // entry tile fastest -- a sample tile's A digits are read into that XCD's L2 once and reused by
+  // its 21 entry tiles (the sample-tile-fastest order streams all of A once per entry tile)
+  const int ny = NE / kGTileE, nb = ((a.sc + kGTileS - 1) / kGTileS) * ny;
+  const int per = gridDim.x / 8;  // 1-D grid padded to a multiple of 8
+  const int v = (blockIdx.x % 8) * per + blockIdx.x / 8;
+  if (v >= nb) return;
+  const int s_tile = (v / ny) * kGTileS;
+  const int e_tile = (v % ny) * kGTileE;
   const bool u_tile = e_tile >= Ep;
   const int nks = (16 * ((inf.L + 15) / 16)) / 16;  // 64-slot K steps: 4 Ls16 / 64
   const int64_t planeA = a.rows * a.kstride, planeB = (int64_t)NE * a.kstride;
@@ -237,15 +245,18 @@ __global__ __launch_bounds__(256, 2) void gemm_i8_kernel(GemmI8Args a) {
                       ((int64_t)g * a.rows + s_tile + 32 * wave_s + (lane & 15)) * 16;
   const uint8_t* B0 = a.bdig + (int64_t)e_tile * a.kstride;
   const uint32_t bs_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)&Bs[0][0];
-  // B piece geometry (16 entry rows x 64 B per 1 KiB piece; 4 pieces per wave per K step):
-  // row (lane >> 2) of the piece, LDS granule lane & 3 holds global granule (lane & 3) ^ ((row >> 2) & 3)
+  // B piece geometry (16 entry rows x 64 B per 1 KiB piece; 4 pieces per wave per K step): row
+  // (lane >> 2) of the piece; K granule g of a row sits in LDS slot (g + 2 ((row >> 2) & 3)) & 3 of
+  // its 64 B.  ds_read_b128 serves a wave in the 16-lane groups {0-3,12-15,20-27}, {4-11,16-19,28-31}
+  // (+32); with row = lane & 15 and g = lane >> 4 every group then hits 16 distinct 16-B slots of the
+  // 256-B bank row (the XOR form g ^ ((row >> 2) & 3) paired lanes 0-3 with 20-23: 2-way conflicts)
   const int prow = lane >> 2;
   uint32_t boff[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int piece = wave_s * 4 + i;
     const int p = piece >> 2, row = (piece & 3) * 16 + prow;
-    boff[i] = (uint32_t)(p * planeB + (int64_t)row * a.kstride + 16 * ((lane & 3) ^ ((row >> 2) & 3)));
+    boff[i] = (uint32_t)(p * planeB + (int64_t)row * a.kstride + 16 * (((lane & 3) + 2 * ((row >> 2) & 3)) & 3));
   }
   auto stage_b = [&](int ks, int buf) {
 #pragma unroll
@@ -269,7 +280,15 @@ __global__ __launch_bounds__(256, 2) void gemm_i8_kernel(GemmI8Args a) {
   v4i Ad[2][4], An[2][4];
   stage_b(0, 0);
   load_a(0, Ad);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // Let the compiler wait for the first A step itself (an empty asm consuming the registers): its
+  // waitcnt pass then knows they are complete at the loop entry.  After an opaque asm wait it
+  // assumed them pending and put vmcnt waits in front of every step's first MFMAs, which also
+  // drained the NEXT step's prefetch loads issued just before (40% of wave cycles waiting).
+#pragma unroll
+  for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+    for (int p = 0; p < 4; ++p) asm volatile("" ::"v"(Ad[rt][p]));
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the B DMA (invisible to the compiler)
   __syncthreads();
   for (int ks = 0; ks < nks; ++ks) {
     const int cur = ks & 1;
@@ -285,7 +304,7 @@ __global__ __launch_bounds__(256, 2) void gemm_i8_kernel(GemmI8Args a) {
       v4i Bd[4];
 #pragma unroll
       for (int p = 0; p < 4; ++p)
-        Bd[p] = *reinterpret_cast<const v4i*>(Bc + p * (kGTileE * 64) + row * 64 + 16 * (g ^ ((row >> 2) & 3)));
+        Bd[p] = *reinterpret_cast<const v4i*>(Bc + p * (kGTileE * 64) + row * 64 + 16 * ((g + 2 * ((row >> 2) & 3)) & 3));
 #pragma unroll
       for (int rt = 0; rt < 2; ++rt) {
         const v4i* Ar = Ad[rt];
@@ -354,7 +373,8 @@ hipError_t launch_weights_i8(const WeightsI8Args& a, hipStream_t s) {
 hipError_t launch_gemm_i8(const GemmI8Args& a, hipStream_t s) {
   if (a.k < 1 || a.k > kGemmMaxK || a.rows % kGTileS != 0 || a.rows < a.sc || a.kstride % 64 != 0)
     return hipErrorInvalidValue;
-  const dim3 grid((unsigned)((a.sc + kGTileS - 1) / kGTileS), (unsigned)(i8_gemm_entries(a.k) / kGTileE));
+  const int nb = ((a.sc + kGTileS - 1) / kGTileS) * (i8_gemm_entries(a.k) / kGTileE);
+  const dim3 grid((unsigned)((nb + 7) / 8 * 8));  // 1-D, padded for the XCD remap
   hipLaunchKernelGGL(gemm_i8_kernel, grid, dim3(256), 0, s, a);
   return hipGetLastError();
 }

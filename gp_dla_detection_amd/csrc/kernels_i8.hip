@@ -95,7 +95,7 @@ __global__ __launch_bounds__(256) void convert_i8_kernel(ConvertI8Args a) {
             pl[3][w] |= (uint32_t)(d3 & 255) << (8 * b);
           }
         }
-        uint8_t* base = a.panel_i8 + (cb + c) * (int64_t)I::kChunkBytes + e * 64 + 16 * (g ^ ((e >> 2) & 3));
+        uint8_t* base = a.panel_i8 + (cb + c) * (int64_t)I::kChunkBytes + e * 64 + 16 * ((g + 2 * ((e >> 2) & 3)) & 3);
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           *reinterpret_cast<uint4*>(base + j * I::kPlaneBytes) = make_uint4(pl[j][0], pl[j][1], pl[j][2], pl[j][3]);
@@ -257,7 +257,7 @@ __global__ __launch_bounds__(256, 1) void likelihood_i8_kernel(LikelihoodI8Args 
     const uint8_t* bp = ldsb + (cur ^ 1) * I::kChunkBytes;  // B planes of chunk c - 1
     auto load_bp = [&](int t, v4i (&Bt)[4]) {
       const int ent = 16 * t + (lane & 15);
-      const int boff = ent * 64 + 16 * (g ^ ((ent >> 2) & 3));
+      const int boff = ent * 64 + 16 * ((g + 2 * ((ent >> 2) & 3)) & 3);
 #pragma unroll
       for (int j = 0; j < 4; ++j) Bt[j] = *reinterpret_cast<const v4i*>(bp + j * I::kPlaneBytes + boff);
     };
@@ -405,7 +405,7 @@ __global__ __launch_bounds__(256, 1) void likelihood_i8_kernel(LikelihoodI8Args 
     // ---- exact int8 contraction: the 10 digit pairs of level i + j <= 3 per tile
     auto load_b = [&](int t, v4i (&Bt)[4]) {
       const int ent = 16 * t + (lane & 15);
-      const int boff = ent * 64 + 16 * (g ^ ((ent >> 2) & 3));
+      const int boff = ent * 64 + 16 * ((g + 2 * ((ent >> 2) & 3)) & 3);
 #pragma unroll
       for (int j = 0; j < 4; ++j) Bt[j] = *reinterpret_cast<const v4i*>(bb + j * I::kPlaneBytes + boff);
     };
