@@ -261,38 +261,16 @@ __device__ inline double raw_profile3(double lam, const double (&afac)[3], doubl
 
 // ---------------------------------------------------------------------------------------------
 // Per-sample augmented LDL^T in registers, one quad of lanes per sample.
-//   srow (Layout<K>::kES doubles): Gram entries (r, c), r <= c, at gram_index(r, c); u_i at
-//   4*kGT + i; sum r^2/d, prod-d mantissa and exponent at 4*kTiles + {0,1,2}.
-//   Lane jq owns Gram columns c = 4jj + jq (rows 0..4jj+3) and u rows i = 4m + jq; pivot rows are
-//   broadcast inside the quad with DPP.  [B u; u' q1] with B = I + M'D^-1 M
-//   (log_mvnpdf_low_rank.m:22-24) is factored as L D L': log det B = sum log D_p and
-//   r'K^-1 r = q1 - u'B^-1 u is the last pivot (log_mvnpdf_low_rank.m:26-32).
+//   Lane jq of the quad owns Gram columns c = 4jj + jq (rows 0..4jj+3, A[jj][i]) and u rows
+//   i = 4m + jq (U[m]); pivot rows are broadcast inside the quad with DPP.  [B u; u' q1] with
+//   B = I + M'D^-1 M (log_mvnpdf_low_rank.m:22-24) is factored as L D L': log det B = sum log D_p
+//   and r'K^-1 r = q1 - u'B^-1 u is the last pivot (log_mvnpdf_low_rank.m:26-32).  quad = sum r^2/d,
+//   prod d = dm 2^de.
 // ---------------------------------------------------------------------------------------------
 template <int K>
-__device__ inline double ldl_log_likelihood(const double* srow, int jq, int n, bool& bad_out) {
-  using Lay = Layout<K>;
-  constexpr int kTiles = Lay::kTiles;
-  constexpr int kGT = Lay::kGT;
+__device__ inline double ldl_factor(double (&A)[(K + 3) / 4][4 * ((K + 3) / 4)], double (&U)[(K + 3) / 4],
+                                    double quad, double dm, double de, int jq, int n, bool& bad_out) {
   constexpr int NJJ = (K + 3) / 4;
-  double A[NJJ][4 * NJJ];
-  double U[NJJ];
-#pragma unroll
-  for (int jj = 0; jj < NJJ; ++jj) {
-    const int c = 4 * jj + jq;
-#pragma unroll
-    for (int i = 0; i < 4 * jj + 4; ++i) {
-      double v = 0.0;
-      if (i <= c && c < K) {
-        v = srow[gram_index<K>(i, c)];
-        if (i == c) v += 1.0;  // B = I + M' D^-1 M (log_mvnpdf_low_rank.m:23)
-      }
-      A[jj][i] = v;
-    }
-    U[jj] = (c < K) ? srow[4 * kGT + c] : 0.0;
-  }
-  double quad = srow[4 * kTiles];
-  const double dm = srow[4 * kTiles + 1];
-  const double de = srow[4 * kTiles + 2];
   double pb = 1.0;
   int eb = 0;
   bool bad = false;
@@ -332,6 +310,87 @@ __device__ inline double ldl_log_likelihood(const double* srow, int jq, int n, b
   const double ll = -0.5 * (quad + (logdet_d + logdet_b) + n * kLog2Pi);  // log_mvnpdf_low_rank.m:30-32
   bad_out = bad || !(fabs(ll) < INFINITY);
   return bad_out ? NAN : ll;
+}
+
+// The quad's matrix from a sample row in memory (Layout<K>::kES doubles): Gram entries (r, c),
+// r <= c, at gram_index(r, c); u_i at 4 kGT + i; sum r^2/d, prod-d mantissa and exponent at
+// 4 kTiles + {0,1,2}.
+template <int K>
+__device__ inline double ldl_log_likelihood(const double* srow, int jq, int n, bool& bad_out) {
+  using Lay = Layout<K>;
+  constexpr int kTiles = Lay::kTiles;
+  constexpr int kGT = Lay::kGT;
+  constexpr int NJJ = (K + 3) / 4;
+  double A[NJJ][4 * NJJ];
+  double U[NJJ];
+#pragma unroll
+  for (int jj = 0; jj < NJJ; ++jj) {
+    const int c = 4 * jj + jq;
+#pragma unroll
+    for (int i = 0; i < 4 * jj + 4; ++i) {
+      double v = 0.0;
+      if (i <= c && c < K) {
+        v = srow[gram_index<K>(i, c)];
+        if (i == c) v += 1.0;  // B = I + M' D^-1 M (log_mvnpdf_low_rank.m:23)
+      }
+      A[jj][i] = v;
+    }
+    U[jj] = (c < K) ? srow[4 * kGT + c] : 0.0;
+  }
+  return ldl_factor<K>(A, U, srow[4 * kTiles], srow[4 * kTiles + 1], srow[4 * kTiles + 2], jq, n, bad_out);
+}
+
+// lane jq of each quad gets x from lane (jq + ROT) & 3 of its quad (DPP quad_perm)
+template <int ROT>
+__device__ inline double quad_rot(double v) {
+  if constexpr ((ROT & 3) == 0) {
+    return v;
+  } else {
+    constexpr int sel = ((0 + ROT) & 3) | (((1 + ROT) & 3) << 2) | (((2 + ROT) & 3) << 4) | (((3 + ROT) & 3) << 6);
+    const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), sel, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), sel, 0xF, 0xF, false);
+    return __hiloint2double(hi, lo);
+  }
+}
+
+// The quad's matrix straight from the v_mfma_f64_4x4x4_4b accumulators (no memory): lane jq of a
+// quad holds entry 4t + jq of its sample in acc[t], so entry (i, c = 4jj + jq) = e = b + jq with
+// b = gram_index(i, 4jj) sits in lane (jq + b) & 3 of register (b >> 2) + ((jq + (b & 3)) >> 2):
+// a quad rotation by b & 3 of registers b >> 2 and b >> 2 + 1, then a select.  All indices are
+// compile-time; u_c = entry 4 kGT + c is already in lane jq.
+template <int K, int I, int JJ>
+__device__ inline double gram_entry_from_acc(const double (&acc)[Layout<K>::kTiles], int jq) {
+  constexpr int kTiles = Layout<K>::kTiles;
+  constexpr int b = I * K - I * (I - 1) / 2 - I + 4 * JJ;  // gram_index(I, 4 JJ), extended linearly
+  constexpr int G = b >> 2, gam = b & 3;
+  const double v0 = quad_rot<gam>(acc[G < kTiles ? G : kTiles - 1]);
+  if constexpr (gam == 0) {
+    return v0;
+  } else {
+    const double v1 = quad_rot<gam>(acc[G + 1 < kTiles ? G + 1 : kTiles - 1]);
+    return (jq + gam >= 4) ? v1 : v0;
+  }
+}
+
+template <int K, int JJ, int I>
+__device__ inline void fill_column_block(double (&A)[(K + 3) / 4][4 * ((K + 3) / 4)],
+                                         const double (&acc)[Layout<K>::kTiles], int jq) {
+  if constexpr (I < 4 * JJ + 4) {
+    const int c = 4 * JJ + jq;
+    const double v = gram_entry_from_acc<K, I, JJ>(acc, jq);
+    A[JJ][I] = (I <= c && c < K) ? v + (I == c ? 1.0 : 0.0) : 0.0;  // B = I + M' D^-1 M (.m:23)
+    fill_column_block<K, JJ, I + 1>(A, acc, jq);
+  }
+}
+
+template <int K, int JJ>
+__device__ inline void fill_from_acc(double (&A)[(K + 3) / 4][4 * ((K + 3) / 4)], double (&U)[(K + 3) / 4],
+                                     const double (&acc)[Layout<K>::kTiles], int jq) {
+  if constexpr (JJ < (K + 3) / 4) {
+    fill_column_block<K, JJ, 0>(A, acc, jq);
+    U[JJ] = (4 * JJ + jq < K) ? acc[Layout<K>::kGT + JJ] : 0.0;
+    fill_from_acc<K, JJ + 1>(A, U, acc, jq);
+  }
 }
 
 }  // namespace

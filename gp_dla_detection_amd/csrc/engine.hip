@@ -433,7 +433,15 @@ int gpdla_engine_process(gpdla_engine* e, const gpdla_spectra* sp, const gpdla_r
   const int64_t E = (int64_t)e->K * (e->K + 1) / 2;
   const int64_t row = e->gemm ? E : panel_row_doubles(e->K);
   const int es = e->gemm ? 0 : scratch_doubles(e->K);
-  const int64_t sc_max = std::min<int64_t>(e->S + 1, 16384);  // panel-GEMM sample chunk
+  // panel-GEMM sample chunks: the S + 1 samples (null model included) in equal chunks of at most
+  // kMaxChunk.  configs[4] (S + 1 = 100,001) measured 46.2 Mevals/s with 16,384-sample chunks (6
+  // full + a 1,697-sample tail that fills a sixth of the GPU), 47.4 with 7 equal chunks, 48.5 with
+  // 2 and 49.1 with one (profiles/r2l): larger launches keep the weights kernel's and the GEMM's
+  // grids full, and the workspaces (A digits 8 B, Gram 8 k(k+1)/2 B per sample and slot / entry)
+  // stay a few GB in 288 GB of HBM.
+  constexpr int64_t kMaxChunk = 131072;
+  const int64_t nchunk = (e->S + 1 + kMaxChunk - 1) / kMaxChunk;
+  const int64_t sc_max = (e->S + 1 + nchunk - 1) / nchunk;
   const int64_t blocks_x = (e->S + 1 + kSamplesPerBlock - 1) / kSamplesPerBlock;
 
   // pinned metadata for every batch of this call: per batch (QB+1) + 4*QB int64
@@ -495,8 +503,6 @@ int gpdla_engine_process(gpdla_engine* e, const gpdla_spectra* sp, const gpdla_r
       if ((rc = grow(&e->d_U, &e->cap_U, (size_t)(e->K * sc_max)))) return rc;
       if ((rc = grow(&e->d_q1p, &e->cap_q1p, (size_t)(kWeightParts * sc_max)))) return rc;
       if ((rc = grow(&e->d_ldp, &e->cap_ldp, (size_t)(kWeightParts * sc_max)))) return rc;
-    } else {
-      if ((rc = grow(&e->d_scratch, &e->cap_scr, (size_t)blocks_x * nq * kSamplesPerBlock * es))) return rc;
     }
     // int8 contraction for this batch: its int32 level sums are exact only up to kI8MaxSlots
     // slots, so a batch holding a longer spectrum runs the fp64 kernels (fused or dgemm) instead
@@ -509,7 +515,8 @@ int gpdla_engine_process(gpdla_engine* e, const gpdla_spectra* sp, const gpdla_r
       if ((rc = grow(&e->d_ai8, &e->cap_ai8,
                      (size_t)8 * ((sc_max + 127) / 128 * 128) * i8_gemm_kstride(cap_max + 0)))) return rc;
     }
-    if (batch_i8) {
+    if (batch_i8) {  // (the fp64 fused kernel transposes its accumulators in registers: no scratch)
+      if ((rc = grow(&e->d_scratch, &e->cap_scr, (size_t)blocks_x * nq * kSamplesPerBlock * es))) return rc;
       if ((rc = grow(&e->d_pi8, &e->cap_pi8, (size_t)chunks * i8_chunk_bytes(e->K)))) return rc;
       if ((rc = grow(&e->d_psc, &e->cap_psc, (size_t)chunks * 64 * 8))) return rc;
       if ((rc = grow(&e->d_pent, &e->cap_pent, (size_t)nq * 2 * i8_entries(e->K)))) return rc;
@@ -594,7 +601,6 @@ int gpdla_engine_process(gpdla_engine* e, const gpdla_spectra* sp, const gpdla_r
     la.offsets = e->d_off; la.nhi = e->d_nhi; la.perm = e->d_perm; la.S = e->S;
     la.num_lines = e->params.num_lines;
     la.lines = make_line_args(e->d_lines);
-    la.scratch = e->d_scratch;
     la.sample_ll = o_sll; la.ld = ld; la.ll_null = o_null; la.status = e->d_status;
 
     ConvertI8Args ca{};

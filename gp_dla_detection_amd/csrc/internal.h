@@ -183,7 +183,6 @@ struct LikelihoodArgs {
   int64_t S;
   int32_t num_lines;
   LineArgs lines;
-  double* scratch;               // [grid blocks][64][kES]: epilogue transpose tiles
   double* sample_ll;             // [q_count][ld] or nullptr
   int64_t ld;
   double* ll_null;               // [q_count]

@@ -220,8 +220,8 @@ __global__ __launch_bounds__(256) void prep_kernel(PrepArgs a) {
 //   padded wavelength, 7-tap convolution from a register window, DLA-modulated pixel terms
 //   a^2/d and a r/d (process_qsos.m:189-197), then v_mfma_f64_4x4x4_4b over the Khatri-Rao
 //   tiles (Gram + u).  Panel rows are staged chunk by chunk into a double-buffered LDS ring by
-//   global_load_lds (the next chunk's DMA overlaps this chunk's compute).  The epilogue transposes
-//   the accumulators through a block-private scratch tile and runs the per-sample augmented LDL^T.
+//   global_load_lds (the next chunk's DMA overlaps this chunk's compute).  The epilogue moves each
+//   sample's entries to its quad of lanes by DPP rotations and runs the augmented LDL^T there.
 // ---------------------------------------------------------------------------------------------
 // Stage chunk c (4 steps x 4 segments = 16 rows) into an LDS ring buffer.  Wave w copies the 4
 // rows of segment w, which are contiguous in the panel (rows w Ls + 4c .. +3), to LDS rows
@@ -471,29 +471,21 @@ __global__ __launch_bounds__(256, (K <= 20 ? 2 : 1)) void likelihood_kernel(Like
     pe += pe2 + ex;
   }
 
-  // ---- epilogue: accumulators -> this block's private scratch tile (sample-major; read straight
-  //      back from L2 after the barrier, which frees the accumulator registers), then the
-  //      augmented LDL^T per sample in registers (a quad of lanes each).
-  //      D lane map of 4x4x4_4b: sample 4*((lane>>2)&3) + (lane>>4), entry 4t + (lane&3).
-  double* scr = a.scratch + (v * kSamplesPerBlock +
-                             wave * kSamplesPerWave) * Lay::kES;
-  {
-    const int sd = 4 * ((lane >> 2) & 3) + (lane >> 4);
-    double* dst = scr + sd * Lay::kES + (lane & 3);
-#pragma unroll
-    for (int t = 0; t < kTiles; ++t) dst[4 * t] = acc[t];
-    if (lane < 16) {
-      double* sc = scr + lane * Lay::kES + 4 * kTiles;
-      sc[0] = q1;
-      sc[1] = pm;
-      sc[2] = (double)pe;
-    }
-  }
-  __syncthreads();
-  const int jq = lane & 3, sq = lane >> 2;
-  const int64_t s2 = s_base + sq;
+  // ---- epilogue: the augmented LDL^T per sample in registers, a quad of lanes each, its matrix
+  //      moved out of the accumulators by quad rotations (fill_from_acc, device_common.h).
+  //      D lane map of 4x4x4_4b: sample 4*((lane>>2)&3) + (lane>>4), entry 4t + (lane&3), so quad
+  //      Q = lane >> 2 already holds all entries of sample 4 (Q & 3) + (Q >> 2); its scalars come
+  //      from lane (that sample) of the segment-combined sums above.
+  const int jq = lane & 3, Q = lane >> 2;
+  const int sig = 4 * (Q & 3) + (Q >> 2);
+  const double qs = __shfl(q1, sig), dm = __shfl(pm, sig);
+  const int de = __shfl(pe, sig);
+  constexpr int NJJ = (K + 3) / 4;
+  double A[NJJ][4 * NJJ], U[NJJ];
+  fill_from_acc<K, 0>(A, U, acc, jq);
   bool bad;
-  const double ll = ldl_log_likelihood<K>(scr + sq * Lay::kES, jq, inf.n, bad);
+  const double ll = ldl_factor<K>(A, U, qs, dm, (double)de, jq, inf.n, bad);
+  const int64_t s2 = s_base + sig;
   if (jq == 0 && s2 <= a.S) {
     if (bad) atomicOr(a.status, 1);
     if (s2 == a.S) a.ll_null[q] = ll;

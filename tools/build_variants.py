@@ -12,7 +12,6 @@ from gp_dla_detection_amd.build import build
 
 VARIANTS: dict = {
     "base": {},
-    "order1": {"GPDLA_GEMM_ORDER": 1},
 }
 if __name__ == "__main__":
     names = sys.argv[1:] or list(VARIANTS)
