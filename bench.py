@@ -133,18 +133,91 @@ WORKLOADS = {
 }
 
 
-# rocprofv3 summary of this workload (tools/profile.sh + tools/summarize_profile.py), committed
-PROFILE_SUMMARY = ROOT / "profiles" / "r1m_summary.json"
+def run_e2e(args, world: int, rank: int, local_rank: int, dist) -> None:
+    """configs[2] end to end: the whole process_qsos script on files --
+    catalog.mat, learned_qso_model_*.mat, dla_samples.mat and preloaded_qsos.mat in (written
+    beforehand, untimed, as the reference's processed/ tree of 162,861 DR12Q-shaped spectra),
+    processed_qsos_<set>.mat (v7.3, with the 13 GB Q x S sample array) out.  The timed region is
+    process.run_process_qsos from its first file read to the last byte of the output file (no
+    warm-up: a cold engine is part of the run); the load / compute / write split is reported per
+    phase (max over ranks).  With N ranks each decodes, evaluates and writes its own spectra."""
+    import shutil
+    from gp_dla_detection_amd import _lib as L
+    from gp_dla_detection_amd import process as PR
+    from gp_dla_detection_amd import synthetic as syn
+    Q = args.spectra or 162861
+    S = args.samples or 10000
+    base = args.e2e_dir or f"/tmp/gpdla_e2e_{Q}_{S}"
+    model = syn.make_model(k=args.k or 20)
+    samples = syn.make_samples(S)
+    t0 = time.perf_counter()
+    if rank == 0:
+        pool = syn.make_dr12q_like_spectra(model, 4096, seed=12, mask_fraction=0.0)
+        names = syn.write_processed_tree(base, model, samples, [pool[i % len(pool)] for i in range(Q)])
+        del pool
+    setup_s = time.perf_counter() - t0
+    print(f"[e2e rank {rank}] processed/ tree ready in {setup_s:.1f} s", file=sys.stderr, flush=True)
+    if dist is not None:
+        box = [names if rank == 0 else None]
+        dist.broadcast_object_list(box, src=0)
+        names = box[0]
+        dist.barrier()
+    dev = local_rank % max(1, L.load().gpdla_device_count())
+    tm = {}
+    t0 = time.perf_counter()
+    PR.run_process_qsos(base, names["training_release"], names["training_set_name"], names["dla_catalog_name"],
+                        names["prior_ind"], names["release"], names["test_set_name"], names["test_ind"],
+                        device=dev, rank=rank, world=world, timings=tm)
+    if dist is not None:
+        dist.barrier()
+    total = time.perf_counter() - t0
+    print(f"[e2e rank {rank}] run_process_qsos {total:.1f} s {tm}", file=sys.stderr, flush=True)
+    phases = [tm.get("load_s", 0.0), tm.get("compute_s", 0.0), tm.get("write_s", 0.0), total]
+    if dist is not None:
+        import torch
+        tt = torch.tensor(phases, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        phases = [float(v) for v in tt]
+    load_s, compute_s, write_s, total = phases
+    out_path = f"{base}/{names['release']}/processed/processed_qsos_{names['test_set_name']}.mat"
+    if rank == 0:
+        out_bytes = os.path.getsize(out_path)
+        evals = Q * S
+        proj8 = (load_s + compute_s) * world / 8
+        print(json.dumps({
+            "metric": "(spectrum x DLA-sample) log-evidence evals/sec", "value": evals / total, "unit": "evals/s",
+            "n_gpus": world, "steps": 1, "warmup": 0, "ms_per_step": total * 1e3, "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic (seeded; DR12Q-shaped pool of 4096 spectra tiled to the count), written as the "
+                    "reference's processed/ tree before the timed region",
+            "config": {"workload": f"configs[2] end to end: process_qsos on files, {Q} spectra x {S} samples, k=20, "
+                                   f"fp64 -> processed_qsos v7.3 ({out_bytes / 1e9:.1f} GB)",
+                       "spectra": Q, "num_samples": S, "parallelism": f"spectrum-shard x{world}"},
+            "e2e": {"total_s": total, "load_s": load_s, "compute_s": compute_s, "write_s": write_s,
+                    "setup_untimed_s": setup_s, "output_bytes": out_bytes, "output_dir": base,
+                    "projection_8_ranks_s": {"load+compute scaled, write scaled": proj8 + write_s * world / 8,
+                                             "load+compute scaled, write as measured": proj8 + write_s},
+                    "note": "load = catalogues, model, samples and this rank's preloaded_qsos cells "
+                            "(process_qsos.m:1-63); compute = the engine incl. its creation (:88-212); "
+                            "write = priors/posteriors and the v7.3 file (:222-249), page cache, no fsync"}}),
+              flush=True)
+        if not args.e2e_keep:
+            shutil.rmtree(base, ignore_errors=True)
+
+
+# rocprofv3 summaries of the bench workloads (tools/profile.sh + tools/summarize_profile.py), committed
+PROFILE_SUMMARY = ROOT / "profiles" / "r2a_summary.json"        # configs[1], fused fp64
+PROFILE_SUMMARY_C5 = ROOT / "profiles" / "r2a_c5_summary.json"  # configs[4], int8 panel-GEMM
 
 
 def profiled_traffic(Q: int, S: int, k: int, path: str = "fused"):
-    """HBM bytes per likelihood launch from the committed PMC profile of the default workload
-    (2 x FETCH_SIZE + WRITE_SIZE, gfx950 correction per MI355X_MICROARCH.md; includes
-    Infinity-Cache hits).  None for other workloads or if no summary is present."""
-    c5 = ROOT / "profiles" / "r1l_c5_traffic.json"
-    if (Q, S, k) == (128, 100000, 50) and path == "panel-GEMM-int8" and c5.exists():
-        # configs[4]: per batch (the engine launch bench times), summed over its kernels
-        return json.loads(c5.read_text())["hbm_bytes_per_batch"], f"{c5.relative_to(ROOT)} (rocprofv3 PMC)"
+    """HBM bytes per likelihood launch from the committed PMC profile of the workload (2 x
+    FETCH_SIZE + WRITE_SIZE, gfx950 correction per MI355X_MICROARCH.md; includes Infinity-Cache
+    hits): the fused kernel's launch for configs[1], the whole batch (prep, weights, GEMM, LDL^T,
+    reduce) for configs[4].  None for other workloads or if no summary is present."""
+    if (Q, S, k) == (128, 100000, 50) and path == "panel-GEMM-int8" and PROFILE_SUMMARY_C5.exists():
+        d = json.loads(PROFILE_SUMMARY_C5.read_text())
+        return d["per_batch"]["hbm_bytes_per_batch"], f"{PROFILE_SUMMARY_C5.relative_to(ROOT)} (rocprofv3 PMC, per batch)"
     if (Q, S, k) != (1024, 10000, 20) or path != "fused" or not PROFILE_SUMMARY.exists():
         return None, None
     d = json.loads(PROFILE_SUMMARY.read_text())
@@ -206,10 +279,12 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c2",
+    ap.add_argument("--e2e-dir", default=None, help="e2e: directory for the processed/ tree (default /tmp/...)")
+    ap.add_argument("--e2e-keep", action="store_true", help="e2e: keep the files afterwards")
+    ap.add_argument("--workload", choices=sorted(WORKLOADS) + ["e2e"], default="c2",
                     help="BASELINE.json configs: c2 = configs[1] (default bench line), c3 = configs[2] "
                          "(full DR12Q, 1 GPU), c4 = configs[3] (full DR12Q split over the ranks), "
-                         "c5 = configs[4] (k=50, 10^5 samples)")
+                         "c5 = configs[4] (k=50, 10^5 samples); e2e = configs[2] end to end on files")
     ap.add_argument("--spectra", type=int, default=None, help="override: spectra per GPU (c2/c5)")
     ap.add_argument("--samples", type=int, default=None, help="override: DLA samples")
     ap.add_argument("--k", type=int, default=None, help="override: rank")
@@ -230,6 +305,13 @@ def main():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         with _stdout_to_stderr():  # gloo prints its connection banner on stdout (fd 1)
             dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    if args.workload == "e2e":
+        run_e2e(args, world, rank, local_rank, dist if world > 1 else None)
+        if world > 1:
+            with _stdout_to_stderr():
+                dist.destroy_process_group()
+        return
 
     from gp_dla_detection_amd import _lib as L
     from gp_dla_detection_amd import synthetic as syn

@@ -766,6 +766,34 @@ static int lines_on_device(double** d_lines) {
   return GPDLA_OK;
 }
 
+// Device buffers of the standalone entry points, cached per device and grown on demand: the MEX
+// drop-ins are called once per sample from a MATLAB loop, so allocating and
+// freeing device memory per call would dominate them.  Calls are serialised per device.
+struct StandaloneBufs {
+  std::mutex mu;
+  char* buf = nullptr;
+  size_t cap = 0;
+};
+
+static StandaloneBufs& standalone_bufs(int dev) {
+  static std::mutex mu;
+  static std::vector<StandaloneBufs*> per_dev;
+  std::lock_guard<std::mutex> lock(mu);
+  if ((int)per_dev.size() <= dev) per_dev.resize(dev + 1, nullptr);
+  if (!per_dev[dev]) per_dev[dev] = new StandaloneBufs();
+  return *per_dev[dev];
+}
+
+static hipError_t standalone_reserve(StandaloneBufs& b, size_t bytes) {
+  if (bytes <= b.cap && b.buf) return hipSuccess;
+  if (b.buf) (void)hipFree(b.buf);
+  b.buf = nullptr;
+  b.cap = 0;
+  hipError_t e = hipMalloc((void**)&b.buf, bytes);
+  if (e == hipSuccess) b.cap = bytes;
+  return e;
+}
+
 int gpdla_voigt_batch_f64(const double* lambdas, int64_t n_padded, const double* z, const double* N,
                           int64_t count, int32_t num_lines, double* out) {
   if (!lambdas || !z || !N || !out) return set_error(GPDLA_EINVAL, "null argument");
@@ -776,19 +804,22 @@ int gpdla_voigt_batch_f64(const double* lambdas, int64_t n_padded, const double*
   if (rc) return rc;
   double* d_lines = nullptr;
   if ((rc = lines_on_device(&d_lines))) return rc;
+  int dev = 0;
+  HIP_TRY(hipGetDevice(&dev));
+  StandaloneBufs& sb = standalone_bufs(dev);
+  std::lock_guard<std::mutex> lock(sb.mu);
   const int64_t n_out = n_padded - 2 * kWidth;
-  double *d_lam = nullptr, *d_z = nullptr, *d_N = nullptr, *d_out = nullptr;
-  auto cleanup = [&] { for (double* p : {d_lam, d_z, d_N, d_out}) if (p) (void)hipFree(p); };
-  hipError_t err = hipMalloc((void**)&d_lam, n_padded * 8);
-  if (err == hipSuccess) err = hipMalloc((void**)&d_z, count * 8);
-  if (err == hipSuccess) err = hipMalloc((void**)&d_N, count * 8);
-  if (err == hipSuccess) err = hipMalloc((void**)&d_out, count * n_out * 8);
+  const size_t bytes = (size_t)(n_padded + 2 * count + count * n_out) * 8;
+  hipError_t err = standalone_reserve(sb, bytes);
+  double* d_lam = (double*)sb.buf;
+  double* d_z = d_lam + n_padded;
+  double* d_N = d_z + count;
+  double* d_out = d_N + count;
   if (err == hipSuccess) err = hipMemcpy(d_lam, lambdas, n_padded * 8, hipMemcpyHostToDevice);
   if (err == hipSuccess) err = hipMemcpy(d_z, z, count * 8, hipMemcpyHostToDevice);
   if (err == hipSuccess) err = hipMemcpy(d_N, N, count * 8, hipMemcpyHostToDevice);
   if (err == hipSuccess) err = launch_voigt_batch(d_lam, n_padded, d_z, d_N, count, num_lines, make_line_args(d_lines), d_out, nullptr);
   if (err == hipSuccess) err = hipMemcpy(out, d_out, count * n_out * 8, hipMemcpyDeviceToHost);
-  cleanup();
   if (err != hipSuccess) return set_error(GPDLA_EDEVICE, "voigt: %s", hipGetErrorString(err));
   return GPDLA_OK;
 }
@@ -805,26 +836,33 @@ int gpdla_log_mvnpdf_low_rank_f64(const double* y, const double* mu, const doubl
   if (k > 64) return set_error(GPDLA_EUNSUPPORTED, "k=%d > 64 in the standalone entry point", k);
   int rc = check_device(0);
   if (rc) return rc;
-  double *dy = nullptr, *dmu = nullptr, *dM = nullptr, *dd = nullptr, *dout = nullptr;
-  int32_t* dst = nullptr;
-  hipError_t err = hipMalloc((void**)&dy, n * 8);
-  if (err == hipSuccess) err = hipMalloc((void**)&dmu, n * 8);
-  if (err == hipSuccess) err = hipMalloc((void**)&dM, n * k * 8);
-  if (err == hipSuccess) err = hipMalloc((void**)&dd, n * 8);
-  if (err == hipSuccess) err = hipMalloc((void**)&dout, 8);
-  if (err == hipSuccess) err = hipMalloc((void**)&dst, 4);
+  int dev = 0;
+  HIP_TRY(hipGetDevice(&dev));
+  StandaloneBufs& sb = standalone_bufs(dev);
+  std::lock_guard<std::mutex> lock(sb.mu);
+  // one staging copy: [y | mu | d | M | out | status]
+  const size_t nd = (size_t)n * (3 + k) + 2;
+  hipError_t err = standalone_reserve(sb, nd * 8);
+  double* dy = (double*)sb.buf;
+  double* dmu = dy + n;
+  double* dd = dmu + n;
+  double* dM = dd + n;
+  double* dout = dM + (size_t)n * k;
+  int32_t* dst = (int32_t*)(dout + 1);
+  std::vector<double> host(nd - 2);
+  std::memcpy(host.data(), y, n * 8);
+  std::memcpy(host.data() + n, mu, n * 8);
+  std::memcpy(host.data() + 2 * n, d, n * 8);
+  std::memcpy(host.data() + 3 * n, M, (size_t)n * k * 8);
+  if (err == hipSuccess) err = hipMemcpy(dy, host.data(), (nd - 2) * 8, hipMemcpyHostToDevice);
   if (err == hipSuccess) err = hipMemset(dst, 0, 4);
-  if (err == hipSuccess) err = hipMemcpy(dy, y, n * 8, hipMemcpyHostToDevice);
-  if (err == hipSuccess) err = hipMemcpy(dmu, mu, n * 8, hipMemcpyHostToDevice);
-  if (err == hipSuccess) err = hipMemcpy(dM, M, n * k * 8, hipMemcpyHostToDevice);
-  if (err == hipSuccess) err = hipMemcpy(dd, d, n * 8, hipMemcpyHostToDevice);
   if (err == hipSuccess) err = launch_mvn_single(dy, dmu, dM, dd, n, k, dout, dst, nullptr);
-  int32_t status = 0;
-  if (err == hipSuccess) err = hipMemcpy(out, dout, 8, hipMemcpyDeviceToHost);
-  if (err == hipSuccess) err = hipMemcpy(&status, dst, 4, hipMemcpyDeviceToHost);
-  for (void* p : {(void*)dy, (void*)dmu, (void*)dM, (void*)dd, (void*)dout, (void*)dst})
-    if (p) (void)hipFree(p);
+  double res[2] = {0, 0};
+  if (err == hipSuccess) err = hipMemcpy(res, dout, 16, hipMemcpyDeviceToHost);
   if (err != hipSuccess) return set_error(GPDLA_EDEVICE, "log_mvnpdf_low_rank: %s", hipGetErrorString(err));
+  *out = res[0];
+  int32_t status = 0;
+  std::memcpy(&status, &res[1], 4);
   if (status) return set_error(GPDLA_ENUMERIC, "B = I + M'D^-1M is not positive definite");
   return GPDLA_OK;
 }

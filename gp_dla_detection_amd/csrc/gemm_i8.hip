@@ -234,8 +234,23 @@ __global__ __launch_bounds__(256, 2) void gemm_i8_kernel(GemmI8Args a) {
   const int per = gridDim.x / 8;  // 1-D grid padded to a multiple of 8
   const int v = (blockIdx.x % 8) * per + blockIdx.x / 8;
   if (v >= nb) return;
+#ifndef GPDLA_GEMM_EGROUP
+#define GPDLA_GEMM_EGROUP 0
+#endif
+#if GPDLA_GEMM_EGROUP
+  // entry-group-major: the entry tiles in groups of GPDLA_GEMM_EGROUP (a group's B digits fit an
+  // XCD's 4 MB L2), inside a group sample tile outer / entry tile inner
+  const int nx = nb / ny;
+  constexpr int EG = GPDLA_GEMM_EGROUP;
+  const int grp = v / (nx * EG);                 // full groups first
+  const int g0 = grp * EG, gs = min(EG, ny - g0);
+  const int w = v - grp * nx * EG;
+  const int s_tile = (w / gs) * kGTileS;
+  const int e_tile = (g0 + w % gs) * kGTileE;
+#else
   const int s_tile = (v / ny) * kGTileS;
   const int e_tile = (v % ny) * kGTileE;
+#endif
   const bool u_tile = e_tile >= Ep;
   const int nks = (16 * ((inf.L + 15) / 16)) / 16;  // 64-slot K steps: 4 Ls16 / 64
   const int64_t planeA = a.rows * a.kstride, planeB = (int64_t)NE * a.kstride;

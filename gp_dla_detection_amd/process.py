@@ -267,7 +267,7 @@ def _indices(sel, n: int) -> np.ndarray:
 def run_process_qsos(base_directory: str, training_release: str, training_set_name: str,
                      dla_catalog_name: str, prior_ind, release: str, test_set_name: str, test_ind,
                      params: Parameters | None = None, device: int = 0, save: bool = True,
-                     rank: int = 0, world: int = 1, compute=None) -> dict:
+                     rank: int = 0, world: int = 1, compute=None, timings: dict | None = None) -> dict:
     """The whole ``process_qsos`` script (process_qsos.m:1-249) on files laid out as the reference
     lays them out (set_parameters.m:79-86):
 
@@ -289,10 +289,16 @@ def run_process_qsos(base_directory: str, training_release: str, training_set_na
     deferred region; every rank then writes its own rows of that region in place (disjoint
     parts of one memory-mapped file), so the 13 GB full-DR12Q array is never gathered.
     ``compute(model, samples, packed, params, device) -> dict`` replaces the engine (tests).
+    ``timings`` (a dict) receives this rank's wall seconds per phase: load (the four input files,
+    process_qsos.m:1-63), compute (the engine, :88-212) and write (priors / posteriors and the
+    v7.3 file, :222-249).
     Rank 0 returns the saved scalars; other ranks their local results."""
+    import time
     from .matv73 import LazyArray, loadmat, open_region
     from .shard import contiguous_shards, merge_shards
     compute = compute or _engine_compute
+    tm = timings if timings is not None else {}
+    t_start = time.perf_counter()
     tdir, rdir = processed_directory(base_directory, training_release), processed_directory(base_directory, release)
     prior_catalog = loadmat(f"{tdir}/catalog.mat")
     pind = evaluate_index(prior_ind, prior_catalog=prior_catalog, dla_catalog_name=dla_catalog_name).astype(bool).ravel()
@@ -315,7 +321,11 @@ def run_process_qsos(base_directory: str, training_release: str, training_set_na
     packed = pack_spectra(spectra) if spectra else dict(
         offsets=np.zeros(1, np.int64), wavelengths=np.zeros(0), flux=np.zeros(0), noise_variance=np.zeros(0),
         pixel_mask=np.zeros(0, np.uint8), z_qsos=np.zeros(0))
+    t_load = time.perf_counter()
+    tm["load_s"] = t_load - t_start
     res = compute(model, samples, packed, params, device)
+    t_comp = time.perf_counter()
+    tm["compute_s"] = t_comp - t_load
     meta = dict(training_release=training_release, training_set_name=training_set_name,
                 dla_catalog_name=dla_catalog_name, prior_ind=pind, release=release,
                 test_set_name=test_set_name)
@@ -326,6 +336,7 @@ def run_process_qsos(base_directory: str, training_release: str, training_set_na
         out["test_ind"] = tind
         if save:
             save_processed_qsos(path, out)
+        tm["write_s"] = time.perf_counter() - t_comp
         return out
     import torch.distributed as dist
     small = {k: v for k, v in res.items() if k != "sample_log_likelihoods_dla"}
@@ -350,9 +361,9 @@ def run_process_qsos(base_directory: str, training_release: str, training_set_na
         view = open_region(path, region[0])
         if mine.size:
             view[mine[0]:mine[-1] + 1] = res["sample_log_likelihoods_dla"]      # this rank's rows
-        view.base.flush()
-        del view
+        del view                                                     # (page cache; no msync, as matv73)
         dist.barrier()
+    tm["write_s"] = time.perf_counter() - t_comp
     return out if rank == 0 else res
 
 

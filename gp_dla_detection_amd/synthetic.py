@@ -122,3 +122,42 @@ def pack_spectra(spectra: list[dict]) -> dict:
     return dict(offsets=offsets, wavelengths=cat("wavelengths", np.float64), flux=cat("flux", np.float64),
                 noise_variance=cat("noise_variance", np.float64), pixel_mask=cat("pixel_mask", np.uint8),
                 z_qsos=np.array([s["z_qso"] for s in spectra], dtype=np.float64))
+
+
+def write_processed_tree(base: str, model: dict, samples: dict, spectra: list, release: str = "dr12q",
+                         training_set_name: str = "dr9q_minus_concordance",
+                         dla_catalog_name: str = "dr9q_concordance", seed: int = 3) -> dict:
+    """The reference's ``<base>/<release>/processed/`` directory (set_parameters.m:79-86) with every
+    file process_qsos.m reads, for synthetic inputs: catalog.mat (z_qsos, filter_flags, in_dr9 and
+    the containers.Map variables los_inds / dla_inds / z_dlas as structs keyed by catalogue name,
+    build_catalogs.m:50-53), learned_qso_model_<set>.mat (learn_qso_model.m:113-123),
+    dla_samples.mat (generate_dla_samples.m:59-63) and preloaded_qsos.mat (the four cell arrays of
+    preload_qsos.m:77-80).  The catalogue doubles as the prior catalogue (release ==
+    training_release).  Returns the index strings for ``process.run_process_qsos``."""
+    from pathlib import Path
+
+    from .matv73 import savemat73
+    from .process import save_dla_samples
+    rng = np.random.default_rng(seed)
+    d = Path(base) / release / "processed"
+    d.mkdir(parents=True, exist_ok=True)
+    Q = len(spectra)
+    z = np.array([s["z_qso"] for s in spectra], dtype=np.float64)
+    dla = rng.uniform(size=Q) < 0.1
+    z_dlas = [np.array([zq - rng.uniform(0.05, 0.5)]) if f else np.zeros(0) for zq, f in zip(z, dla)]
+    savemat73(str(d / "catalog.mat"), dict(
+        z_qsos=z, filter_flags=np.zeros(Q, np.uint8), in_dr9=rng.uniform(size=Q) < 0.8,
+        los_inds={dla_catalog_name: np.ones(Q, bool)}, dla_inds={dla_catalog_name: dla},
+        z_dlas={dla_catalog_name: z_dlas}))
+    savemat73(str(d / f"learned_qso_model_{training_set_name}.mat"),
+              {k: model[k] for k in ("rest_wavelengths", "mu", "M", "log_omega", "log_c_0", "log_tau_0", "log_beta")})
+    save_dla_samples(str(d / "dla_samples.mat"), samples)
+    savemat73(str(d / "preloaded_qsos.mat"), dict(
+        all_wavelengths=[s["wavelengths"] for s in spectra], all_flux=[s["flux"] for s in spectra],
+        all_noise_variance=[s["noise_variance"] for s in spectra],
+        all_pixel_mask=[np.asarray(s["pixel_mask"], dtype=bool) for s in spectra]))
+    return dict(training_release=release, training_set_name=training_set_name,
+                dla_catalog_name=dla_catalog_name,
+                prior_ind=" prior_catalog.in_dr9 & prior_catalog.los_inds(dla_catalog_name) & "
+                          "(prior_catalog.filter_flags == 0)",
+                release=release, test_set_name=release, test_ind="(catalog.filter_flags == 0)")

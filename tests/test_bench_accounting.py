@@ -33,10 +33,10 @@ def test_i8_ops_per_eval(bench):
 
 def test_profiled_traffic_lookup(bench):
     t, src = bench.profiled_traffic(1024, 10000, 20, "fused")
-    assert t is not None and t > 0 and "r1m_summary" in src
+    assert t is not None and t > 0 and "r2a_summary" in src
     t5, src5 = bench.profiled_traffic(128, 100000, 50, "panel-GEMM-int8")
-    want = json.loads((ROOT / "profiles" / "r1l_c5_traffic.json").read_text())["hbm_bytes_per_batch"]
-    assert t5 == want and "r1l_c5_traffic" in src5
+    want = json.loads((ROOT / "profiles" / "r2a_c5_summary.json").read_text())["per_batch"]["hbm_bytes_per_batch"]
+    assert t5 == want and "r2a_c5_summary" in src5
     # other workloads / paths: no profiled number is claimed
     assert bench.profiled_traffic(128, 100000, 50, "panel-GEMM") == (None, None)
     assert bench.profiled_traffic(64, 10000, 20, "fused") == (None, None)

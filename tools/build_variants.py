@@ -12,6 +12,9 @@ from gp_dla_detection_amd.build import build
 
 VARIANTS: dict = {
     "base": {},
+    "eg11": {"GPDLA_GEMM_EGROUP": 11},
+    "eg7": {"GPDLA_GEMM_EGROUP": 7},
+    "eg4": {"GPDLA_GEMM_EGROUP": 4},
 }
 if __name__ == "__main__":
     names = sys.argv[1:] or list(VARIANTS)

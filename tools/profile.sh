@@ -4,10 +4,11 @@
 # Output: gpurun_out/prof_<tag>/...
 set -euo pipefail
 TAG=${1:-r1}
+shift || true
 OUT=$PWD/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-ARGS="--steps 3 --warmup 1 --cpu-budget 0"
+ARGS="--steps 3 --warmup 1 --cpu-budget 0 --no-alt $*"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o trace --output-format csv -- python3 bench.py $ARGS > "$OUT/bench_trace.json"
 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/fetch" -o fetch --output-format csv -- python3 bench.py $ARGS > "$OUT/bench_fetch.json"
 timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/write" -o write --output-format csv -- python3 bench.py $ARGS > "$OUT/bench_write.json"

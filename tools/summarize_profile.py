@@ -51,6 +51,14 @@ def main(src: str, tag: str, dst: str = "profiles"):
             if k in sq:
                 ent[cn] = sum(sq[k]) / len(sq[k])
         out["kernels"].append(ent)
+    # per batch (one gpdla_engine_process batch = one prep launch): the HBM bytes of every kernel
+    # with counters, for the panel paths whose "launch" is a batch of many kernels
+    preps = [e for e in out["kernels"] if e["kernel"].startswith("void gpdla::prep_kernel")]
+    if preps:
+        nb = sum(e["calls"] for e in preps)
+        tot = sum(e["hbm_bytes_per_launch"] * e["calls"] for e in out["kernels"] if "hbm_bytes_per_launch" in e)
+        out["per_batch"] = {"batches": nb, "hbm_bytes_per_batch": tot / nb,
+                            "kernel_ms_per_batch": sum(e["avg_ms"] * e["calls"] for e in out["kernels"]) / nb}
     (dst / f"{tag}_summary.json").write_text(json.dumps(out, indent=1))
     lines = [f"# rocprofv3 summary `{tag}`", "",
              f"bench under trace: {bench['value']:.4g} {bench['unit']}, {bench['ms_per_step']:.2f} ms/step", "",
@@ -63,6 +71,10 @@ def main(src: str, tag: str, dst: str = "profiles"):
         gbs = f"{e['hbm_gbs']:.0f}" if "hbm_gbs" in e else "-"
         lines.append(f"| {e['kernel']} | {e['calls']} | {e['avg_ms']:.3f} | {e['pct']:.2f} | {gb} | {gbs} | "
                      f"{per('SQ_INSTS_VALU')} | {per('SQ_INSTS_MFMA')} | {per('SQ_INSTS_LDS')} |")
+    if "per_batch" in out:
+        pb = out["per_batch"]
+        lines += ["", f"per batch ({pb['batches']} batches): {pb['hbm_bytes_per_batch'] / 1e9:.2f} GB of HBM traffic, "
+                      f"{pb['kernel_ms_per_batch']:.2f} ms of kernel time"]
     (dst / f"{tag}_summary.md").write_text("\n".join(lines) + "\n")
     print("\n".join(lines))
 
