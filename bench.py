@@ -39,10 +39,36 @@ def algorithmic_flops_per_eval(n: int, k: int) -> float:
     return n * k * (k + 1) + 2 * n * k + 10 * n + k ** 3 / 3 + 2 * k ** 2
 
 
-def i8_ops_per_eval(n: float, k: int) -> float:
-    """int8 MFMA ops of the exact Gram/u contraction: 10 digit pairs
-    (levels <= 3) x n slots x (k(k+1)/2 Gram + k u entries), 2 ops per multiply-add."""
-    return 2 * 10 * n * (k * (k + 1) / 2 + k)
+def i8_ops_per_eval(n: float, k: int, gram_pairs: int = 10) -> float:
+    """int8 MFMA ops of the exact Gram/u contraction, 2 ops per multiply-add:
+    n slots x (k(k+1)/2 Gram entries x gram_pairs + k u entries x 10) digit pairs.  gram_pairs = 10
+    for the 32-bit scheme (4 digits, levels <= 3), 6 for panel_gemm_i8_24 (3 digits, levels <= 2;
+    its u entries keep 4 digits)."""
+    return 2 * n * (gram_pairs * k * (k + 1) / 2 + 10 * k)
+
+
+def i8_roofline(st: dict, n: float, k: int, Q: int, S: int, steps: int, path: str) -> dict:
+    """Roofline of the int8 panel paths' dominant kernel, the int8 GEMM (gemm_i8.hip): its algorithmic
+    int8 ops per launch / its average launch time (HIP events around each launch on the engine's
+    stream, gpdla_stats.contraction_ms), against the dense int8 MFMA peak (2x BF16 per clock,
+    MI355X_MICROARCH.md).  The whole batch (weights + GEMM + LDL^T) is reported beside it."""
+    pairs = 6 if path.endswith("-24") else 10
+    ops = i8_ops_per_eval(n, k, pairs)
+    nl = max(st["contraction_launches"], 1)
+    gemm_ms = st["contraction_ms"] / nl
+    evals_per_gemm = Q * (S + 1) * steps / nl
+    achieved = ops * evals_per_gemm / (gemm_ms * 1e-3) / 1e12
+    batch_ms = st["likelihood_ms"] / max(st["likelihood_launches"], 1)
+    evals_per_batch = Q * (S + 1) * steps / max(st["likelihood_launches"], 1)
+    return {"bound": "mfma", "mfma_dtype": "i8", "unit": "TOPS", "peak": I8_PEAK_TOPS, "achieved": achieved,
+            "frac": achieved / I8_PEAK_TOPS, "avg_launch_ms": gemm_ms, "evals_per_launch": evals_per_gemm,
+            "i8_ops_per_eval": ops,
+            "whole_batch": {"avg_ms": batch_ms, "evals": evals_per_batch,
+                            "achieved_tops": ops * evals_per_batch / (batch_ms * 1e-3) / 1e12,
+                            "fp64_equivalent_tflops": algorithmic_flops_per_eval(n, k) * evals_per_batch
+                                                      / (batch_ms * 1e-3) / 1e12},
+            "note": "gemm_i8 launches only (one per spectrum and sample chunk; the Gram and u launches of "
+                    "the 24-bit path counted as one); the batch adds the weights and LDL^T kernels"}
 
 
 def effective_bytes_per_eval(n: int, k: int, w: int = 8) -> float:
@@ -127,9 +153,10 @@ WORKLOADS = {
                label="configs[2]: full DR12Q count (162,861 DR12Q-shaped spectra) x 10^4 samples, k=20, fp64, 1 GPU"),
     "c4": dict(spectra=162861, samples=10000, k=20, dr12q=True, scaling="strong",
                label="configs[3]: full DR12Q count split over the ranks (spectrum shards), k=20, fp64"),
-    "c5": dict(spectra=128, samples=100000, k=50, dr12q=False, scaling="weak", default_path="panel_gemm_i8",
-               label="configs[4]: 128 spectra/GPU x 10^5 DLA samples, k=50 (quoted in fp32; run on the "
-                     "int8 panel-GEMM path, 2e-9 from fp64, or --path panel_gemm for the fp64 GEMMs)"),
+    "c5": dict(spectra=128, samples=100000, k=50, dr12q=False, scaling="weak", default_path="panel_gemm_i8_24",
+               label="configs[4]: 128 spectra/GPU x 10^5 DLA samples, k=50 (quoted in fp32; run on the int8 "
+                     "panel-GEMM path with the 24-bit Gram contraction, ~2e-7 from fp64; --path panel_gemm_i8 "
+                     "for the 32-bit one, ~4e-9; --path panel_gemm for the fp64 GEMMs)"),
 }
 
 
@@ -207,17 +234,23 @@ def run_e2e(args, world: int, rank: int, local_rank: int, dist) -> None:
 
 # rocprofv3 summaries of the bench workloads (tools/profile.sh + tools/summarize_profile.py), committed
 PROFILE_SUMMARY = ROOT / "profiles" / "r2a_summary.json"        # configs[1], fused fp64
-PROFILE_SUMMARY_C5 = ROOT / "profiles" / "r2a_c5_summary.json"  # configs[4], int8 panel-GEMM
+PROFILE_SUMMARY_C5 = {"panel-GEMM-int8": ROOT / "profiles" / "r2a_c5_summary.json",      # configs[4], 32-bit
+                      "panel-GEMM-int8-24": ROOT / "profiles" / "r2b_c5_summary.json"}   # configs[4], 24-bit
 
 
 def profiled_traffic(Q: int, S: int, k: int, path: str = "fused"):
-    """HBM bytes per likelihood launch from the committed PMC profile of the workload (2 x
-    FETCH_SIZE + WRITE_SIZE, gfx950 correction per MI355X_MICROARCH.md; includes Infinity-Cache
-    hits): the fused kernel's launch for configs[1], the whole batch (prep, weights, GEMM, LDL^T,
-    reduce) for configs[4].  None for other workloads or if no summary is present."""
-    if (Q, S, k) == (128, 100000, 50) and path == "panel-GEMM-int8" and PROFILE_SUMMARY_C5.exists():
-        d = json.loads(PROFILE_SUMMARY_C5.read_text())
-        return d["per_batch"]["hbm_bytes_per_batch"], f"{PROFILE_SUMMARY_C5.relative_to(ROOT)} (rocprofv3 PMC, per batch)"
+    """HBM bytes per launch of the roofline kernel from the committed PMC profile of the workload
+    (2 x FETCH_SIZE + WRITE_SIZE, gfx950 correction per MI355X_MICROARCH.md; includes Infinity-Cache
+    hits): the fused kernel for configs[1]; for configs[4] the int8 GEMM launches of one spectrum and
+    sample chunk (the Gram and u launches of the 24-bit path together).  None for other workloads or
+    if no summary is present."""
+    if (Q, S, k) == (128, 100000, 50) and path in PROFILE_SUMMARY_C5 and PROFILE_SUMMARY_C5[path].exists():
+        f = PROFILE_SUMMARY_C5[path]
+        d = json.loads(f.read_text())
+        rows = [e for e in d["kernels"] if "gemm_i8_kernel" in e["kernel"] and "hbm_bytes_per_launch" in e]
+        if rows:
+            return sum(e["hbm_bytes_per_launch"] for e in rows), f"{f.relative_to(ROOT)} (rocprofv3 PMC, gemm_i8 launches)"
+        return None, None
     if (Q, S, k) != (1024, 10000, 20) or path != "fused" or not PROFILE_SUMMARY.exists():
         return None, None
     d = json.loads(PROFILE_SUMMARY.read_text())
@@ -288,7 +321,7 @@ def main():
     ap.add_argument("--spectra", type=int, default=None, help="override: spectra per GPU (c2/c5)")
     ap.add_argument("--samples", type=int, default=None, help="override: DLA samples")
     ap.add_argument("--k", type=int, default=None, help="override: rank")
-    ap.add_argument("--path", choices=["auto", "fused", "fused_i8", "panel_gemm", "panel_gemm_i8"], default="auto",
+    ap.add_argument("--path", choices=["auto", "fused", "fused_i8", "panel_gemm", "panel_gemm_i8", "panel_gemm_i8_24"], default="auto",
                     help="likelihood path (Engine path=): auto = fused fp64 kernel for the compiled ranks, "
                          "fused_i8 = the int8 Ozaki contraction (k=20), panel_gemm = weights + dgemm + LDL^T")
     ap.add_argument("--no-alt", action="store_true",
@@ -358,6 +391,8 @@ def main():
         path = "fused-int8"
     elif args.path == "panel_gemm_i8":
         path = "panel-GEMM-int8"
+    elif args.path == "panel_gemm_i8_24":
+        path = "panel-GEMM-int8-24"
     elif args.path == "panel_gemm" or args.k not in (4, 8, 10, 12, 16, 20, 24):
         path = "panel-GEMM"
     else:
@@ -436,7 +471,7 @@ def main():
 
     traffic, traffic_src = profiled_traffic(Q, S, args.k, path)
     # batched LDL^T kernel of the panel paths (gemm_path.hip launch_ldl_batch)
-    ldl_name = "ldl_cyc_kernel" if args.k >= 32 else "ldl_reg_kernel"
+    ldl_name = f"ldl_mfma_kernel<{(args.k + 4) // 4}>"
     result = {
         "metric": "(spectrum x DLA-sample) log-evidence evals/sec",
         "value": value,
@@ -448,8 +483,10 @@ def main():
         "higher_is_better": True,
         "scaling": wl["scaling"],
         "vs_baseline": None,
-        "dtype": "f64" if path in ("fused", "panel-GEMM") else
-                 "f64+i8 (Gram/u contraction exact in int8/int32 over 32-bit-quantised operands, fp64 elsewhere)",
+        "dtype": {"fused": "f64", "panel-GEMM": "f64",
+                  "panel-GEMM-int8-24": "f64+i8 (Gram contraction exact in int8/int32 over 24-bit-quantised "
+                                        "operands, u over 32-bit, fp64 elsewhere; fp32-class, ~2e-7 from fp64)"}.get(
+                     path, "f64+i8 (Gram/u contraction exact in int8/int32 over 32-bit-quantised operands, fp64 elsewhere)"),
         "data": "synthetic (seeded; SURVEY.md 8d model/spectra, unscrambled Halton samples)"
                 + ("; DR12Q-shaped pool of 4096 spectra tiled to the count" if wl["dr12q"] else ""),
         "config": {"workload": f"{wl['label']}; this rank: {Q} spectra, mean n={n_mean:.0f}, 3 Lyman lines",
@@ -457,26 +494,18 @@ def main():
                    "likelihood_path": path, "parallelism": f"spectrum-shard x{world}"},
         "roofline": {"bound": "mfma", "achieved": achieved_tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved_tf / FP64_PEAK_TFLOPS, "traffic": traffic,
-                     **({} if path != "panel-GEMM-int8" else {
-                         # the contraction runs on the int8 matrix cores: price it against their
-                         # dense peak (2x BF16 per clock, MI355X_MICROARCH.md); the fp64-equivalent
-                         # TFLOP/s above is the algorithmic fp64 work / time and may exceed the FP64 peak
-                         "bound": "mfma", "mfma_dtype": "i8", "unit": "TOPS", "peak": I8_PEAK_TOPS,
-                         "achieved": i8_ops_per_eval(n_mean, args.k) * evals_per_launch / (avg_ms * 1e-3) / 1e12,
-                         "frac": i8_ops_per_eval(n_mean, args.k) * evals_per_launch / (avg_ms * 1e-3) / 1e12
-                                 / I8_PEAK_TOPS,
-                         "i8_ops_per_eval": i8_ops_per_eval(n_mean, args.k),
-                         "fp64_equivalent_tflops": achieved_tf,
-                         "note": "int8 ops over the whole batch time (weights + int8 GEMM + LDL^T overlapped); "
-                                 "gemm_i8_kernel alone runs ~2.2x this rate, ~1,700 TOPS (profiles/r1l_summary.md)"}),
                      "traffic_source": traffic_src,
                      "kernel": {"fused": f"likelihood_kernel<{args.k}>",
                                 "fused-int8": f"likelihood_i8_kernel<{args.k}>",
-                                "panel-GEMM-int8": f"weights_i8_kernel + gemm_i8_kernel + {ldl_name} (per batch)"}.get(
+                                "panel-GEMM-int8": "gemm_i8_kernel<4>",
+                                "panel-GEMM-int8-24": "gemm_i8_kernel<3> (Gram) + gemm_i8_kernel<4> (u)"}.get(
                                     path, f"weights_kernel + rocBLAS dgemm + {ldl_name} (per batch)"),
                      "avg_launch_ms": avg_ms,
                      "flops_per_eval": algorithmic_flops_per_eval(n_mean, args.k),
-                     "evals_per_launch": evals_per_launch},
+                     "evals_per_launch": evals_per_launch,
+                     # int8 panel paths: the int8 GEMM kernel's own roofline (overrides the fields above)
+                     **({} if not path.startswith("panel-GEMM-int8") else i8_roofline(st, n_mean, args.k, Q, S,
+                                                                                      args.steps, path))},
         "hbm_effective": {"achieved": eff_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                           "frac": eff_gbs / HBM_PEAK_GBS,
                           "bytes_per_eval": effective_bytes_per_eval(n_mean, args.k),

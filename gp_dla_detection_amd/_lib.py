@@ -27,6 +27,7 @@ PATH_FUSED = 1
 PATH_PANEL_GEMM = 2
 PATH_FUSED_I8 = 3
 PATH_PANEL_GEMM_I8 = 4
+PATH_PANEL_GEMM_I8_24 = 5
 
 dp = C.POINTER(C.c_double)
 i64p = C.POINTER(C.c_int64)
@@ -69,7 +70,8 @@ class Results(C.Structure):
 class Stats(C.Structure):
     _fields_ = [("prep_ms", C.c_double), ("likelihood_ms", C.c_double), ("reduce_ms", C.c_double),
                 ("prep_launches", C.c_int64), ("likelihood_launches", C.c_int64),
-                ("reduce_launches", C.c_int64), ("spectra", C.c_int64), ("sample_evals", C.c_int64)]
+                ("reduce_launches", C.c_int64), ("spectra", C.c_int64), ("sample_evals", C.c_int64),
+                ("contraction_ms", C.c_double), ("contraction_launches", C.c_int64)]
 
 
 # every symbol include/gpdla.h declares, with its ctypes signature

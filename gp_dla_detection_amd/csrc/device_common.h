@@ -10,9 +10,6 @@
 
 #include "internal.h"
 
-// Build-time variant switches (A/B experiments; defaults are the shipped configuration).
-// far-wing fast path: fp64 kernel off (A/B +1.4% time: spills at 256 VGPRs), int8 kernel on (-0.9%)
-
 namespace gpdla {
 
 namespace {

@@ -94,7 +94,7 @@ int grow(T** p, size_t* cap, size_t count) {
 
 struct TimedLaunch {
   hipEvent_t start, stop;
-  int kind;  // 0 prep, 1 likelihood, 2 reduce
+  int kind;  // 0 prep, 1 likelihood, 2 reduce, 3 contraction (panel-GEMM paths, inside 1)
 };
 
 }  // namespace
@@ -105,6 +105,7 @@ struct gpdla_engine {
   int64_t S = 0;
   bool gemm = false;                 // panel-GEMM path (gemm_path.hip + rocBLAS) instead of fused
   bool i8 = false;                   // fused path with the int8 Ozaki contraction (kernels_i8.hip)
+  int i8_nd = 4;                     // int8 panel-GEMM digit planes: 4 (levels <= 3) or 3 (_I8_24)
   rocblas_handle blas = nullptr;
   gpdla_params params{};
   hipStream_t own_stream = nullptr;
@@ -151,6 +152,7 @@ struct gpdla_engine {
   size_t cap_hmeta = 0;
   hipEvent_t meta_done = nullptr;
 
+
   std::vector<TimedLaunch> pending;
   gpdla_stats stats{};
 };
@@ -173,6 +175,7 @@ int resolve_events(gpdla_engine* e) {
     if (t.kind == 0) { e->stats.prep_ms += ms; e->stats.prep_launches++; }
     if (t.kind == 1) { e->stats.likelihood_ms += ms; e->stats.likelihood_launches++; }
     if (t.kind == 2) { e->stats.reduce_ms += ms; e->stats.reduce_launches++; }
+    if (t.kind == 3) { e->stats.contraction_ms += ms; e->stats.contraction_launches++; }
     (void)hipEventDestroy(t.start);
     (void)hipEventDestroy(t.stop);
   }
@@ -192,7 +195,7 @@ int validate_params(const gpdla_params* p) {
     return set_error(GPDLA_EINVAL, "invalid wavelength parameters");
   if (p->max_batch_spectra < 0) return set_error(GPDLA_EINVAL, "max_batch_spectra < 0");
   if (p->path != GPDLA_PATH_AUTO && p->path != GPDLA_PATH_FUSED && p->path != GPDLA_PATH_PANEL_GEMM &&
-      p->path != GPDLA_PATH_FUSED_I8 && p->path != GPDLA_PATH_PANEL_GEMM_I8)
+      p->path != GPDLA_PATH_FUSED_I8 && p->path != GPDLA_PATH_PANEL_GEMM_I8 && p->path != GPDLA_PATH_PANEL_GEMM_I8_24)
     return set_error(GPDLA_EINVAL, "path=%d", p->path);
   return GPDLA_OK;
 }
@@ -240,6 +243,7 @@ void gpdla_engine_destroy(gpdla_engine* e) {
   if (e->h_meta) (void)hipHostFree(e->h_meta);
   if (e->blas) (void)rocblas_destroy_handle(e->blas);
   if (e->meta_done) (void)hipEventDestroy(e->meta_done);
+
   if (e->own_stream) (void)hipStreamDestroy(e->own_stream);
   delete e;
 }
@@ -252,10 +256,11 @@ int gpdla_engine_create(int32_t device, const gpdla_model* model, const gpdla_sa
   if (rc) return rc;
   if ((rc = validate_params(params))) return rc;
   const bool fused_ok = rank_supported(model->k);
-  const bool use_gemm = params->path == GPDLA_PATH_PANEL_GEMM || params->path == GPDLA_PATH_PANEL_GEMM_I8 ||
+  const bool gemm_i8 = params->path == GPDLA_PATH_PANEL_GEMM_I8 || params->path == GPDLA_PATH_PANEL_GEMM_I8_24;
+  const bool use_gemm = params->path == GPDLA_PATH_PANEL_GEMM || gemm_i8 ||
                         (params->path == GPDLA_PATH_AUTO && !fused_ok);
-  const bool use_i8 = params->path == GPDLA_PATH_FUSED_I8 || params->path == GPDLA_PATH_PANEL_GEMM_I8;
-  if (params->path == GPDLA_PATH_PANEL_GEMM_I8 && params->num_lines != 3)
+  const bool use_i8 = params->path == GPDLA_PATH_FUSED_I8 || gemm_i8;
+  if (gemm_i8 && params->num_lines != 3)
     return set_error(GPDLA_EUNSUPPORTED, "int8 panel-GEMM path needs num_lines=3 (num_lines=%d)", params->num_lines);
   if (params->path == GPDLA_PATH_FUSED_I8 && (!i8_supported(model->k) || params->num_lines != 3))
     return set_error(GPDLA_EUNSUPPORTED, "int8 fused path needs k=20 and num_lines=3 (k=%d, num_lines=%d)",
@@ -279,6 +284,7 @@ int gpdla_engine_create(int32_t device, const gpdla_model* model, const gpdla_sa
   e->S = samples->num_samples;
   e->gemm = use_gemm;
   e->i8 = use_i8;
+  e->i8_nd = params->path == GPDLA_PATH_PANEL_GEMM_I8_24 ? 3 : 4;
   e->params = *params;
   e->num_rest = model->num_rest;
   e->c0 = std::exp(model->log_c_0);     // process_qsos.m:84-86
@@ -293,6 +299,7 @@ int gpdla_engine_create(int32_t device, const gpdla_model* model, const gpdla_sa
     return fail(set_error(GPDLA_EDEVICE, "hipEventCreate failed"));
   if (e->gemm && rocblas_create_handle(&e->blas) != rocblas_status_success)
     return fail(set_error(GPDLA_EDEVICE, "rocblas_create_handle failed"));
+
 
   const size_t G = model->num_rest, K = model->k;
   std::vector<double> Mrow(G * K);
@@ -349,9 +356,9 @@ int gpdla_engine_set_stream(gpdla_engine* e, void* hip_stream) {
 
 // Panel-GEMM path for one batch: per spectrum and chunk of samples, weights -> GEMM (int8 digits
 // on the matrix cores, or two rocBLAS dgemm) -> batched LDL^T (gemm_path.hip), in stream order.
-// (The LDL^T on a second stream beside the next chunk's weights and GEMM measured +5% with the
-// VALU LDL^T kernel of round 1; with the matrix-core LDL^T both compete for the same units and the
-// overlap measured 0%, profiles/r2f, so it was removed.)
+// (Second streams measured no gain and were removed: the LDL^T beside the next chunk's weights and
+// GEMM +5% with round 1's VALU LDL^T, 0% with the matrix-core one (profiles/r2f); the weights kernel
+// beside the previous chunk's GEMM and LDL^T, double-buffered, +0.5% (round 2, profiles/r2c).)
 static int run_panel_gemm(gpdla_engine* e, bool i8, int64_t nq, const int64_t* h_sb, const int64_t* h_lb,
                           const int64_t* h_cap, const int64_t* h_cb, int64_t sc_max, double* o_sll,
                           int64_t ld, double* o_null, hipStream_t st) {
@@ -361,23 +368,29 @@ static int run_panel_gemm(gpdla_engine* e, bool i8, int64_t nq, const int64_t* h
     return set_error(GPDLA_EDEVICE, "rocblas_set_stream failed");
   const double one = 1.0, zero = 0.0;
   double *G = e->d_G, *U = e->d_U, *q1p = e->d_q1p, *ldp = e->d_ldp;
+  const int64_t rows = (sc_max + 127) / 128 * 128;
   for (int64_t q = 0; q < nq; ++q) {
     for (int64_t s0 = 0; s0 <= e->S; s0 += sc_max) {
       const int32_t sc = (int32_t)std::min<int64_t>(sc_max, e->S + 1 - s0);
       if (i8) {  // int8 Ozaki contraction (gemm_i8.hip): weights digits -> exact GEMM -> Gram, u
         const int64_t ks = i8_gemm_kstride(h_cap[q]);
-        const int64_t rows = (sc_max + 127) / 128 * 128;
+        uint8_t* adig = e->d_ai8;
         WeightsI8Args wi{};
         wi.info = e->d_info; wi.q = (int32_t)q;
         wi.srow = e->d_srow + h_sb[q] * 8; wi.lam_pad = e->d_lam + h_lb[q]; wi.kstride = ks;
         wi.offsets = e->d_off; wi.nhi = e->d_nhi; wi.S = e->S; wi.s0 = s0; wi.sc = sc; wi.rows = rows;
-        wi.lines = make_line_args(e->d_lines); wi.adig = e->d_ai8; wi.q1p = q1p; wi.ldp = ldp;
+        wi.lines = make_line_args(e->d_lines); wi.nd = e->i8_nd; wi.adig = adig; wi.q1p = q1p; wi.ldp = ldp;
         HIP_TRY(launch_weights_i8(wi, st));
         GemmI8Args gi{};
-        gi.info = e->d_info; gi.q = (int32_t)q; gi.k = K; gi.kstride = ks; gi.rows = rows; gi.sc = sc;
-        gi.adig = e->d_ai8; gi.bdig = e->d_pi8 + h_cb[q];
+        gi.info = e->d_info; gi.q = (int32_t)q; gi.k = K; gi.kstride = ks; gi.rows = rows; gi.sc = sc; gi.nd = e->i8_nd;
+        gi.adig = adig; gi.bdig = e->d_pi8 + h_cb[q];
         gi.ent = e->d_pent + q * 2 * (int64_t)i8_gemm_entries(K); gi.G = G; gi.U = U;
+        TimedLaunch tg{};
+        int rc;
+        if ((rc = record_start(e, &tg, 3))) return rc;
         HIP_TRY(launch_gemm_i8(gi, st));
+        HIP_TRY(hipEventRecord(tg.stop, st));
+        e->pending.push_back(tg);
       } else {
         WeightsArgs wa{};
         wa.info = e->d_info; wa.q = (int32_t)q;
@@ -627,7 +640,7 @@ int gpdla_engine_process(gpdla_engine* e, const gpdla_spectra* sp, const gpdla_r
       ConvertGemmI8Args cg{};
       cg.k = e->K; cg.info = e->d_info; cg.panel = e->d_panel; cg.panel_m = e->d_pm; cg.srow = e->d_srow;
       cg.slot_base = pa.slot_base; cg.slot_cap = pa.slot_cap; cg.bbase = pa.slot_cap + QB;
-      cg.bdig = e->d_pi8; cg.ent = e->d_pent;
+      cg.bdig = e->d_pi8; cg.ent = e->d_pent; cg.nd = e->i8_nd;
       HIP_TRY(launch_convert_gemm_i8(cg, (int32_t)nq, st));
     }
     HIP_TRY(hipEventRecord(t0.stop, st));

@@ -83,7 +83,8 @@ __global__ __launch_bounds__(256) void convert_gemm_i8_kernel(ConvertGemmI8Args 
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j)
-      *reinterpret_cast<uint4*>(base + j * plane + t0) = make_uint4(pl[j][0], pl[j][1], pl[j][2], pl[j][3]);
+      if (j < (is_u ? 4 : a.nd))  // u entries keep 4 digits (launch_gemm_i8)
+        *reinterpret_cast<uint4*>(base + j * plane + t0) = make_uint4(pl[j][0], pl[j][1], pl[j][2], pl[j][3]);
   }
   s_cs[g][le] = colsum;
   __syncthreads();
@@ -182,9 +183,8 @@ __global__ __launch_bounds__(256) void weights_i8_kernel(WeightsI8Args a) {
     if (active) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const v4i dg = digit_plane(xg, i), du = digit_plane(xu, i);
-        *reinterpret_cast<v4i*>(ag + i * plane + (int64_t)(tg / 16) * a.rows * 16) = dg;
-        *reinterpret_cast<v4i*>(au + i * plane + (int64_t)(tg / 16) * a.rows * 16) = du;
+        if (i < a.nd) *reinterpret_cast<v4i*>(ag + i * plane + (int64_t)(tg / 16) * a.rows * 16) = digit_plane(xg, i);
+        *reinterpret_cast<v4i*>(au + i * plane + (int64_t)(tg / 16) * a.rows * 16) = digit_plane(xu, i);  // 4 u digits
       }
     }
   }
@@ -208,16 +208,19 @@ constexpr int kGTileS = 128, kGTileE = 64;
 // --------------------------------------------------------------------------------------------
 // GEMM: 128-sample x 64-entry block tiles (1-D grid, XCD-aware order below), 4 waves; wave w owns samples
 // 32 w .. 32 w + 31 of the tile (2 row tiles) x all 64 entries (4 column tiles of
-// v_mfma_i32_16x16x64_i8, 10 digit pairs, int32 per level).  The weight digits (A) go
+// v_mfma_i32_16x16x64_i8, the ND (ND + 1) / 2 digit pairs of level <= ND - 1, int32 per level: 10
+// pairs for ND = 4, 6 for ND = 3).  The weight digits (A) go
 // global -> VGPRs in the MFMA operand layout (each wave owns its 32 samples,
 // so A has no reuse across the block's waves and LDS would only add traffic), prefetched one K
 // step ahead; only the panel digits (B, shared by the 4 waves) are staged, by LDS-DMA into a
-// double-buffered tile.  Per K step a wave reads 16 B-operand granules from LDS for 80 MFMAs
-// (200 B per MFMA; staging both operands through LDS cost 300 B per MFMA plus the A writes,
+// double-buffered tile.  Per K step a wave reads 4 ND B-operand granules from LDS for 8 ND (ND + 1) / 2
+// MFMAs (staging both operands through LDS cost 50% more LDS traffic per MFMA plus the A writes,
 // which kept the matrix cores waiting on LDS bandwidth).
 // --------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256, 2) void gemm_i8_kernel(GemmI8Args a) {
-  __shared__ __attribute__((aligned(16))) uint8_t Bs[2][4 * kGTileE * 64];
+template <int ND>
+// 3 blocks per CU for ND = 3 (168 VGPRs; +5% over 2), 2 for ND = 4 (222 VGPRs)
+__global__ __launch_bounds__(256, ND == 3 ? 3 : 2) void gemm_i8_kernel(GemmI8Args a) {
+  __shared__ __attribute__((aligned(16))) uint8_t Bs[2][ND * kGTileE * 64];
   const SpecInfo inf = a.info[a.q];
   if (inf.J == 0) return;
   const int K = a.k;
@@ -230,27 +233,12 @@ __global__ __launch_bounds__(256, 2) void gemm_i8_kernel(GemmI8Args a) {
   // virtual index v gives each XCD a contiguous run of (sample tile, entry tile) pairs with the
   // entry tile fastest -- a sample tile's A digits are read into that XCD's L2 once and reused by
   // its 21 entry tiles (the sample-tile-fastest order streams all of A once per entry tile)
-  const int ny = NE / kGTileE, nb = ((a.sc + kGTileS - 1) / kGTileS) * ny;
+  const int ny = a.ny, nb = ((a.sc + kGTileS - 1) / kGTileS) * ny;  // this launch's entry tiles
   const int per = gridDim.x / 8;  // 1-D grid padded to a multiple of 8
   const int v = (blockIdx.x % 8) * per + blockIdx.x / 8;
   if (v >= nb) return;
-#ifndef GPDLA_GEMM_EGROUP
-#define GPDLA_GEMM_EGROUP 0
-#endif
-#if GPDLA_GEMM_EGROUP
-  // entry-group-major: the entry tiles in groups of GPDLA_GEMM_EGROUP (a group's B digits fit an
-  // XCD's 4 MB L2), inside a group sample tile outer / entry tile inner
-  const int nx = nb / ny;
-  constexpr int EG = GPDLA_GEMM_EGROUP;
-  const int grp = v / (nx * EG);                 // full groups first
-  const int g0 = grp * EG, gs = min(EG, ny - g0);
-  const int w = v - grp * nx * EG;
-  const int s_tile = (w / gs) * kGTileS;
-  const int e_tile = (g0 + w % gs) * kGTileE;
-#else
   const int s_tile = (v / ny) * kGTileS;
-  const int e_tile = (v % ny) * kGTileE;
-#endif
+  const int e_tile = (a.e_tile0 + v % ny) * kGTileE;
   const bool u_tile = e_tile >= Ep;
   const int nks = (16 * ((inf.L + 15) / 16)) / 16;  // 64-slot K steps: 4 Ls16 / 64
   const int64_t planeA = a.rows * a.kstride, planeB = (int64_t)NE * a.kstride;
@@ -260,89 +248,94 @@ __global__ __launch_bounds__(256, 2) void gemm_i8_kernel(GemmI8Args a) {
                       ((int64_t)g * a.rows + s_tile + 32 * wave_s + (lane & 15)) * 16;
   const uint8_t* B0 = a.bdig + (int64_t)e_tile * a.kstride;
   const uint32_t bs_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)&Bs[0][0];
-  // B piece geometry (16 entry rows x 64 B per 1 KiB piece; 4 pieces per wave per K step): row
-  // (lane >> 2) of the piece; K granule g of a row sits in LDS slot (g + 2 ((row >> 2) & 3)) & 3 of
-  // its 64 B.  ds_read_b128 serves a wave in the 16-lane groups {0-3,12-15,20-27}, {4-11,16-19,28-31}
-  // (+32); with row = lane & 15 and g = lane >> 4 every group then hits 16 distinct 16-B slots of the
-  // 256-B bank row (the XOR form g ^ ((row >> 2) & 3) paired lanes 0-3 with 20-23: 2-way conflicts)
+  // B piece geometry (16 entry rows x 64 B per 1 KiB piece, 4 per plane; ND pieces per wave per K
+  // step): row (lane >> 2) of the piece; K granule g of a row sits in LDS slot (g + 2 ((row >> 2) & 3))
+  // & 3 of its 64 B.  ds_read_b128 serves a wave in the 16-lane groups {0-3,12-15,20-27},
+  // {4-11,16-19,28-31} (+32); with row = lane & 15 and g = lane >> 4 every group then hits 16 distinct
+  // 16-B slots of the 256-B bank row (the XOR form g ^ ((row >> 2) & 3) paired lanes 0-3 with 20-23:
+  // 2-way conflicts)
   const int prow = lane >> 2;
-  uint32_t boff[4];
+  uint32_t boff[ND];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int piece = wave_s * 4 + i;
+  for (int i = 0; i < ND; ++i) {
+    const int piece = wave_s * ND + i;
     const int p = piece >> 2, row = (piece & 3) * 16 + prow;
     boff[i] = (uint32_t)(p * planeB + (int64_t)row * a.kstride + 16 * (((lane & 3) + 2 * ((row >> 2) & 3)) & 3));
   }
   auto stage_b = [&](int ks, int buf) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-      dma_piece(B0 + ks * 64, boff[i], bs_base + (uint32_t)(buf * (4 * kGTileE * 64) + (wave_s * 4 + i) * 1024));
+    for (int i = 0; i < ND; ++i)
+      dma_piece(B0 + ks * 64, boff[i], bs_base + (uint32_t)(buf * (ND * kGTileE * 64) + (wave_s * ND + i) * 1024));
   };
-  auto load_a = [&](int ks, v4i (&r)[2][4]) {
+  auto load_a = [&](int ks, v4i (&r)[2][ND]) {
 #pragma unroll
     for (int rt = 0; rt < 2; ++rt)
 #pragma unroll
-      for (int p = 0; p < 4; ++p)
+      for (int p = 0; p < ND; ++p)
         r[rt][p] = *reinterpret_cast<const v4i*>(A0 + p * planeA + (int64_t)ks * 4 * a.rows * 16 + rt * 256);
+    __builtin_amdgcn_sched_barrier(0);  // the prefetch goes out before the step's MFMAs
   };
-  v4i acc[4][2][4];
+  v4i acc[ND][2][4];
 #pragma unroll
-  for (int l = 0; l < 4; ++l)
+  for (int l = 0; l < ND; ++l)
 #pragma unroll
     for (int rt = 0; rt < 2; ++rt)
 #pragma unroll
       for (int ct = 0; ct < 4; ++ct) acc[l][rt][ct] = (v4i){0, 0, 0, 0};
-  v4i Ad[2][4], An[2][4];
-  stage_b(0, 0);
-  load_a(0, Ad);
-  // Let the compiler wait for the first A step itself (an empty asm consuming the registers): its
-  // waitcnt pass then knows they are complete at the loop entry.  After an opaque asm wait it
-  // assumed them pending and put vmcnt waits in front of every step's first MFMAs, which also
-  // drained the NEXT step's prefetch loads issued just before (40% of wave cycles waiting).
-#pragma unroll
-  for (int rt = 0; rt < 2; ++rt)
-#pragma unroll
-    for (int p = 0; p < 4; ++p) asm volatile("" ::"v"(Ad[rt][p]));
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the B DMA (invisible to the compiler)
-  __syncthreads();
-  for (int ks = 0; ks < nks; ++ks) {
-    const int cur = ks & 1;
-    const bool more = ks + 1 < nks;
-    if (more) {
-      stage_b(ks + 1, cur ^ 1);
-      load_a(ks + 1, An);
-    }
-    const uint8_t* Bc = Bs[cur];
+  // one K step's MFMAs on A registers Ar and LDS buffer buf
+  auto compute = [&](const v4i (&Ar)[2][ND], int buf) {
+    const uint8_t* Bc = Bs[buf];
 #pragma unroll
     for (int ct = 0; ct < 4; ++ct) {
       const int row = 16 * ct + (lane & 15);
-      v4i Bd[4];
+      v4i Bd[ND];
 #pragma unroll
-      for (int p = 0; p < 4; ++p)
+      for (int p = 0; p < ND; ++p)
         Bd[p] = *reinterpret_cast<const v4i*>(Bc + p * (kGTileE * 64) + row * 64 + 16 * ((g + 2 * ((row >> 2) & 3)) & 3));
 #pragma unroll
       for (int rt = 0; rt < 2; ++rt) {
-        const v4i* Ar = Ad[rt];
-        acc[0][rt][ct] = MFMA_I8(Ar[0], Bd[0], acc[0][rt][ct]);
-        acc[1][rt][ct] = MFMA_I8(Ar[0], Bd[1], acc[1][rt][ct]);
-        acc[1][rt][ct] = MFMA_I8(Ar[1], Bd[0], acc[1][rt][ct]);
-        acc[2][rt][ct] = MFMA_I8(Ar[0], Bd[2], acc[2][rt][ct]);
-        acc[2][rt][ct] = MFMA_I8(Ar[1], Bd[1], acc[2][rt][ct]);
-        acc[2][rt][ct] = MFMA_I8(Ar[2], Bd[0], acc[2][rt][ct]);
-        acc[3][rt][ct] = MFMA_I8(Ar[0], Bd[3], acc[3][rt][ct]);
-        acc[3][rt][ct] = MFMA_I8(Ar[1], Bd[2], acc[3][rt][ct]);
-        acc[3][rt][ct] = MFMA_I8(Ar[2], Bd[1], acc[3][rt][ct]);
-        acc[3][rt][ct] = MFMA_I8(Ar[3], Bd[0], acc[3][rt][ct]);
+        // level l = i + j: A digit i (most significant first) x B digit j
+#pragma unroll
+        for (int l = 0; l < ND; ++l)
+#pragma unroll
+          for (int i = 0; i <= l; ++i) acc[l][rt][ct] = MFMA_I8(Ar[rt][i], Bd[l - i], acc[l][rt][ct]);
       }
+      __builtin_amdgcn_sched_barrier(0);  // one column tile's B reads + MFMAs at a time (registers)
     }
-    if (more) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // next step's B DMA and A loads landed
+  };
+  // Wait for this wave's outstanding loads (the next step's B DMA, which the compiler cannot see, and
+  // A loads into Ar), then hand Ar through an empty asm that "redefines" it: the compiler's waitcnt
+  // pass would otherwise still count those loads as pending and, at the first MFMA reading Ar, insert
+  // a vmcnt(N) that does not count the DMA issued after them -- draining the NEXT step's prefetch.
+  auto land = [&](v4i (&Ar)[2][ND]) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
-      for (int rt = 0; rt < 2; ++rt)
+    for (int rt = 0; rt < 2; ++rt)
 #pragma unroll
-        for (int p = 0; p < 4; ++p) Ad[rt][p] = An[rt][p];
+      for (int p = 0; p < ND; ++p) asm volatile("" : "+v"(Ar[rt][p]));
+    __syncthreads();  // everyone's DMA landed; the other LDS buffer is free again
+  };
+  // Two A register sets used in turn (steps of even / odd ks) and the loop unrolled by two: no
+  // register copies; the conditional prefetches are safe for the waitcnt pass because every path
+  // goes through land() before the registers are read.
+  v4i A0r[2][ND], A1r[2][ND];
+  stage_b(0, 0);
+  load_a(0, A0r);
+  land(A0r);
+  for (int ks = 0; ks < nks; ks += 2) {
+    const bool m1 = ks + 1 < nks, m2 = ks + 2 < nks;
+    if (m1) {
+      stage_b(ks + 1, 1);
+      load_a(ks + 1, A1r);
     }
-    __syncthreads();  // everyone's DMA landed; buffer cur is free for step ks + 2
+    compute(A0r, 0);
+    land(A1r);
+    if (m2) {
+      stage_b(ks + 2, 0);
+      load_a(ks + 2, A0r);
+    }
+    if (m1) compute(A1r, 1);
+    land(A0r);
   }
   // epilogue: D lane map of 16x16x64: sample 4 (lane >> 4) + r, entry lane & 15
 #pragma unroll
@@ -357,10 +350,10 @@ __global__ __launch_bounds__(256, 2) void gemm_i8_kernel(GemmI8Args a) {
       for (int r = 0; r < 4; ++r) {
         const int sl = s_tile + 32 * wave + 16 * rt + 4 * (lane >> 4) + r;
         if (sl >= a.sc) continue;
-        double val = (double)acc[3][rt][ct][r] * 0x1p24;
-        val = fma((double)acc[2][rt][ct][r], 0x1p32, val);
-        val = fma((double)acc[1][rt][ct][r], 0x1p40, val);
-        val = fma((double)acc[0][rt][ct][r], 0x1p48, val);
+        // sum_l 2^(48 - 8 l) C_l, least significant level first
+        double val = (double)acc[ND - 1][rt][ct][r] * __builtin_ldexp(1.0, 48 - 8 * (ND - 1));
+#pragma unroll
+        for (int l = ND - 2; l >= 0; --l) val = fma((double)acc[l][rt][ct][r], __builtin_ldexp(1.0, 48 - 8 * l), val);
         val = (val + off0) * sc;
         if (u_tile) a.U[(int64_t)sl * K + col] = val;
         else a.G[(int64_t)sl * E + col] = val;
@@ -385,12 +378,27 @@ hipError_t launch_weights_i8(const WeightsI8Args& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t launch_gemm_i8(const GemmI8Args& a, hipStream_t s) {
-  if (a.k < 1 || a.k > kGemmMaxK || a.rows % kGTileS != 0 || a.rows < a.sc || a.kstride % 64 != 0)
+// nd = 4: one launch over all entry tiles.  nd = 3: the Gram tiles on the 3-digit kernel, then the u
+// tiles on the 4-digit one (the u contraction carries most of the 24-bit scheme's error: emulated
+// 2.1e-7 with 3 u digits, 7e-8 with 4, tests/support/emulate_i8.py; the u tiles are 1 of 21 at k = 50)
+hipError_t launch_gemm_i8(const GemmI8Args& a0, hipStream_t s) {
+  if (a0.k < 1 || a0.k > kGemmMaxK || a0.rows % kGTileS != 0 || a0.rows < a0.sc || a0.kstride % 64 != 0 ||
+      (a0.nd != 3 && a0.nd != 4))
     return hipErrorInvalidValue;
-  const int nb = ((a.sc + kGTileS - 1) / kGTileS) * (i8_gemm_entries(a.k) / kGTileE);
-  const dim3 grid((unsigned)((nb + 7) / 8 * 8));  // 1-D, padded for the XCD remap
-  hipLaunchKernelGGL(gemm_i8_kernel, grid, dim3(256), 0, s, a);
+  const int K = a0.k, Ep = 64 * ((K * (K + 1) / 2 + 63) / 64);
+  const int ng = Ep / kGTileE, nu = i8_gemm_entries(K) / kGTileE - ng;
+  const int nst = (a0.sc + kGTileS - 1) / kGTileS;
+  auto grid = [&](int ny) { return dim3((unsigned)((nst * ny + 7) / 8 * 8)); };  // 1-D, padded for the XCD remap
+  GemmI8Args a = a0;
+  if (a0.nd == 4) {
+    a.e_tile0 = 0; a.ny = ng + nu;
+    hipLaunchKernelGGL(gemm_i8_kernel<4>, grid(a.ny), dim3(256), 0, s, a);
+  } else {
+    a.e_tile0 = 0; a.ny = ng;
+    hipLaunchKernelGGL(gemm_i8_kernel<3>, grid(a.ny), dim3(256), 0, s, a);
+    a.e_tile0 = ng; a.ny = nu;
+    hipLaunchKernelGGL(gemm_i8_kernel<4>, grid(a.ny), dim3(256), 0, s, a);
+  }
   return hipGetLastError();
 }
 

@@ -285,6 +285,7 @@ struct ConvertGemmI8Args {
   const int64_t* slot_base;      // device [q]
   const int64_t* slot_cap;       // device [q]
   const int64_t* bbase;          // device [q]: byte offset of the spectrum's B digit planes
+  int32_t nd;                    // Gram digit planes written: 4 (levels <= 3) or 3 (levels <= 2); u: 4
   uint8_t* bdig;                 // [planes 4][entries][kstride] per spectrum
   double* ent;                   // [q][2][entries]: s_e / scaleA, c * colsum_e
 };
@@ -301,6 +302,7 @@ struct WeightsI8Args {
   int32_t sc;
   int64_t rows;                  // sample rows allocated per digit plane (>= sc, multiple of 128)
   LineArgs lines;
+  int32_t nd;                    // Gram digit planes written (4 or 3); u: 4
   uint8_t* adig;                 // [type 2 (Gram, u)][plane 4][rows][kstride]
   double* q1p;
   double* ldp;
@@ -313,6 +315,8 @@ struct GemmI8Args {
   int64_t kstride;
   int64_t rows;
   int32_t sc;
+  int32_t nd;                    // Gram digit planes per operand: 4 (10 pairs, levels <= 3) or 3 (6 pairs); u: 4
+  int32_t e_tile0, ny;           // set by launch_gemm_i8: first 64-entry tile and tile count of a launch
   const uint8_t* adig;
   const uint8_t* bdig;           // this spectrum's B planes
   const double* ent;             // this spectrum's [2][entries]

@@ -25,7 +25,8 @@ def _model_struct(model: dict, keep: list) -> L.Model:
 
 
 _PATHS = {"auto": L.PATH_AUTO, "fused": L.PATH_FUSED, "panel_gemm": L.PATH_PANEL_GEMM,
-          "fused_i8": L.PATH_FUSED_I8, "panel_gemm_i8": L.PATH_PANEL_GEMM_I8}
+          "fused_i8": L.PATH_FUSED_I8, "panel_gemm_i8": L.PATH_PANEL_GEMM_I8,
+          "panel_gemm_i8_24": L.PATH_PANEL_GEMM_I8_24}
 
 
 def _params_struct(p: Parameters, max_batch_spectra: int = 0, path: str = "auto") -> L.Params:

@@ -61,6 +61,12 @@ extern "C" {
  * GPDLA_PATH_FUSED_I8), any rank 1..64 with num_lines = 3; for BASELINE configs[4] (k = 50, quoted in
  * fp32) it agrees with fp64 to ~1e-9 relative, far inside fp32's ~5e-6. */
 #define GPDLA_PATH_PANEL_GEMM_I8 4
+/* GPDLA_PATH_PANEL_GEMM_I8 with a 24-bit Gram contraction: 3 digit planes per operand and the 6 digit
+ * pairs of level <= 2 for the k(k+1)/2 Gram entries (instead of 4 planes and 10 pairs: 40% fewer
+ * matrix-core operations); the k u entries keep the 32-bit scheme.  Fp32-class, as BASELINE configs[4]
+ * is quoted (an fp32 Gram/Cholesky gives 4.5-6e-6): a few 1e-7 relative from fp64 on
+ * the log-likelihoods at k = 50, inside the 1e-6 contract. */
+#define GPDLA_PATH_PANEL_GEMM_I8_24 5
 
 /* Learned null model (learned_qso_model_<set>.mat, read at process_qsos.m:30-35).  Host memory. */
 typedef struct gpdla_model {
@@ -124,6 +130,8 @@ typedef struct gpdla_stats {
   double prep_ms, likelihood_ms, reduce_ms;
   int64_t prep_launches, likelihood_launches, reduce_launches;
   int64_t spectra, sample_evals;       /* sample_evals = sum over spectra of S (null evals excluded) */
+  double contraction_ms;               /* int8 panel-GEMM path: the gemm_i8 launches (part of likelihood_ms) */
+  int64_t contraction_launches;
 } gpdla_stats;
 
 typedef struct gpdla_engine gpdla_engine;
@@ -138,8 +146,7 @@ int gpdla_engine_process(gpdla_engine* engine, const gpdla_spectra* spectra,
 /* Wait for enqueued work; returns GPDLA_ENUMERIC if any pivot was non-positive since the last call. */
 int gpdla_engine_synchronize(gpdla_engine* engine);
 /* Use an external hipStream_t (NULL restores the engine's own stream).  All work of a process call
- * is ordered on that stream: the int8 panel-GEMM path also runs its batched LDL^T on an internal
- * second stream, joined back (hipStreamWaitEvent) before the call's later kernels and its copies. */
+ * is ordered on that stream. */
 int gpdla_engine_set_stream(gpdla_engine* engine, void* hip_stream);
 int gpdla_engine_get_stats(gpdla_engine* engine, gpdla_stats* stats);
 int gpdla_engine_reset_stats(gpdla_engine* engine);

@@ -29,13 +29,27 @@ def test_flops_and_bytes_per_eval(bench):
 def test_i8_ops_per_eval(bench):
     # 10 digit pairs x n slots x (1275 Gram + 50 u entries) x 2 ops at k = 50
     assert bench.i8_ops_per_eval(800, 50) == 2 * 10 * 800 * 1325
+    # 24-bit Gram contraction: 6 pairs per Gram entry, the u entries keep 10
+    assert bench.i8_ops_per_eval(800, 50, 6) == 2 * 800 * (6 * 1275 + 10 * 50)
+
+
+def test_i8_roofline_uses_the_gemm_launches(bench):
+    st = {"contraction_ms": 20.0, "contraction_launches": 20, "likelihood_ms": 30.0, "likelihood_launches": 2}
+    r = bench.i8_roofline(st, 800, 50, Q=10, S=99, steps=2, path="panel-GEMM-int8-24")
+    ops = bench.i8_ops_per_eval(800, 50, 6)
+    # 20 GEMM launches of 1 ms over 10 spectra x 100 evals x 2 steps
+    assert r["avg_launch_ms"] == 1.0 and r["evals_per_launch"] == 100
+    assert r["achieved"] == pytest.approx(ops * 100 / 1e-3 / 1e12)
+    assert r["frac"] == pytest.approx(r["achieved"] / bench.I8_PEAK_TOPS)
+    assert r["whole_batch"]["avg_ms"] == 15.0
 
 
 def test_profiled_traffic_lookup(bench):
     t, src = bench.profiled_traffic(1024, 10000, 20, "fused")
     assert t is not None and t > 0 and "r2a_summary" in src
     t5, src5 = bench.profiled_traffic(128, 100000, 50, "panel-GEMM-int8")
-    want = json.loads((ROOT / "profiles" / "r2a_c5_summary.json").read_text())["per_batch"]["hbm_bytes_per_batch"]
+    rows = json.loads((ROOT / "profiles" / "r2a_c5_summary.json").read_text())["kernels"]
+    want = sum(e["hbm_bytes_per_launch"] for e in rows if "gemm_i8_kernel" in e["kernel"])
     assert t5 == want and "r2a_c5_summary" in src5
     # other workloads / paths: no profiled number is claimed
     assert bench.profiled_traffic(128, 100000, 50, "panel-GEMM") == (None, None)

@@ -11,10 +11,9 @@ sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 from gp_dla_detection_amd.build import build
 
 VARIANTS: dict = {
-    "base": {},
-    "eg11": {"GPDLA_GEMM_EGROUP": 11},
-    "eg7": {"GPDLA_GEMM_EGROUP": 7},
-    "eg4": {"GPDLA_GEMM_EGROUP": 4},
+    "occ3pipe": {"GPDLA_GEMM_OCC": 3},
+    "occ3nopipe": {"GPDLA_GEMM_OCC": 3, "GPDLA_PIPE": 0},
+    "occ2pipe": {"GPDLA_GEMM_OCC": 2},
 }
 if __name__ == "__main__":
     names = sys.argv[1:] or list(VARIANTS)
