@@ -11,6 +11,7 @@
 // followed by the fp64 augmented LDL^T of gemm_path.hip (log_mvnpdf_low_rank.m:22-32).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdint>
 
@@ -148,10 +149,12 @@ __global__ __launch_bounds__(256) void weights_i8_kernel(WeightsI8Args a) {
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
       const int t = tg + e;
-      double lam, y = 0.0, noise = 1.0, mu = 0.0, om2 = 0.0;  // neutral past the segment
+      // neutral past the segment (quantisation scales as prep_kernel computes them for y = mu = om2 = 0,
+      // noise = 1: u_bound = 1)
+      double lam, y = 0.0, noise = 1.0, mu = 0.0, om2 = 0.0, su = kI8ScaleU, sg = kI8ScaleG;
       if (t < L) {
         const double* sr = a.srow + ((int64_t)g * Ls + t) * 8;
-        lam = sr[0]; y = sr[1]; noise = sr[2]; mu = sr[3]; om2 = sr[4];
+        lam = sr[0]; y = sr[1]; noise = sr[2]; mu = sr[3]; om2 = sr[4]; su = sr[6]; sg = sr[7];
       } else {
         lam = a.lam_pad[(int64_t)g * L + t + 2 * kWidth];
       }
@@ -171,8 +174,8 @@ __global__ __launch_bounds__(256) void weights_i8_kernel(WeightsI8Args a) {
       const double rd = r * dinv;
       q1 = fma(r, rd, q1);
       pm *= d;
-      xg[e] = (uint32_t)__builtin_rint(a2 * dinv * ((om2 + noise) * kI8ScaleG)) ^ 0x80808080u;
-      xu[e] = (uint32_t)__builtin_rint(fma(ab * rd, kI8ScaleU / u_bound(y, mu, noise), 0x1p31)) ^ 0x80808080u;
+      xg[e] = (uint32_t)__builtin_rint(a2 * dinv * sg) ^ 0x80808080u;
+      xu[e] = (uint32_t)__builtin_rint(fma(ab * rd, su, 0x1p31)) ^ 0x80808080u;
       asm volatile("" : "+v"(xg[e]), "+v"(xu[e]), "+v"(q1), "+v"(pm));  // no sinking across slots
     }
     {
@@ -206,16 +209,23 @@ __device__ inline void dma_piece(const uint8_t* sbase, uint32_t voffset, uint32_
 constexpr int kGTileS = 128, kGTileE = 64;
 
 // --------------------------------------------------------------------------------------------
-// GEMM: 128-sample x 64-entry block tiles (1-D grid, XCD-aware order below), 4 waves; wave w owns samples
-// 32 w .. 32 w + 31 of the tile (2 row tiles) x all 64 entries (4 column tiles of
-// v_mfma_i32_16x16x64_i8, the ND (ND + 1) / 2 digit pairs of level <= ND - 1, int32 per level: 10
-// pairs for ND = 4, 6 for ND = 3).  The weight digits (A) go
-// global -> VGPRs in the MFMA operand layout (each wave owns its 32 samples,
-// so A has no reuse across the block's waves and LDS would only add traffic), prefetched one K
-// step ahead; only the panel digits (B, shared by the 4 waves) are staged, by LDS-DMA into a
-// double-buffered tile.  Per K step a wave reads 4 ND B-operand granules from LDS for 8 ND (ND + 1) / 2
-// MFMAs (staging both operands through LDS cost 50% more LDS traffic per MFMA plus the A writes,
-// which kept the matrix cores waiting on LDS bandwidth).
+// GEMM: 128-sample x 64-entry tiles, 4 waves per block; wave w owns samples 32 w .. 32 w + 31 of the
+// tile (2 row tiles) x all 64 entries (4 column tiles of v_mfma_i32_16x16x64_i8, the ND (ND + 1) / 2
+// digit pairs of level <= ND - 1, int32 per level: 10 pairs for ND = 4, 6 for ND = 3).  The weight
+// digits (A) go global -> VGPRs in the MFMA operand layout (each wave owns its 32 samples, so A has no
+// reuse across the block's waves and LDS would only add traffic), prefetched one K step ahead; only
+// the panel digits (B, shared by the 4 waves) are staged, by LDS-DMA into a double-buffered tile.
+// Per K step a wave reads 4 ND B-operand granules from LDS for 8 ND (ND + 1) / 2 MFMAs (staging both
+// operands through LDS cost 50% more LDS traffic per MFMA plus the A writes, which kept the matrix
+// cores waiting on LDS bandwidth).
+//
+// Persistent blocks: a block walks its tiles as ONE stream of K steps, so the next tile's first step
+// is prefetched behind the current tile's last MFMAs and epilogue stores (measured equal to one block
+// per tile: the kernel is bound by L2 -> CU traffic -- a loads-only variant ran 0.77 ms of its 0.80,
+// an MFMA-only one 0.51; profiles/r2/c5_ab).  Tile order is
+// XCD-contiguous and entry-tile-fastest: the dispatcher deals linear block b to XCD b % 8, XCD x owns
+// a contiguous run of (sample tile, entry tile) pairs, and its blocks advance through the run side by
+// side -- a sample tile's A digits are read into that XCD's L2 once and reused by its entry tiles.
 // --------------------------------------------------------------------------------------------
 template <int ND>
 // 3 blocks per CU for ND = 3 (168 VGPRs; +5% over 2), 2 for ND = 4 (222 VGPRs)
@@ -229,24 +239,29 @@ __global__ __launch_bounds__(256, ND == 3 ? 3 : 2) void gemm_i8_kernel(GemmI8Arg
   const int NE = i8_gemm_entries(K);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wave_s = __builtin_amdgcn_readfirstlane(wave);
-  // XCD-contiguous, entry-tile-fastest order: the dispatcher deals linear block b to XCD b % 8, so
-  // virtual index v gives each XCD a contiguous run of (sample tile, entry tile) pairs with the
-  // entry tile fastest -- a sample tile's A digits are read into that XCD's L2 once and reused by
-  // its 21 entry tiles (the sample-tile-fastest order streams all of A once per entry tile)
-  const int ny = a.ny, nb = ((a.sc + kGTileS - 1) / kGTileS) * ny;  // this launch's entry tiles
-  const int per = gridDim.x / 8;  // 1-D grid padded to a multiple of 8
-  const int v = (blockIdx.x % 8) * per + blockIdx.x / 8;
-  if (v >= nb) return;
-  const int s_tile = (v / ny) * kGTileS;
-  const int e_tile = (a.e_tile0 + v % ny) * kGTileE;
-  const bool u_tile = e_tile >= Ep;
+  // this block's tiles.  The 8 XCDs form an SX x EX grid over (sample tiles, entry tiles): XCD x owns
+  // sample-tile range x / EX and entry-tile range x % EX; its per blocks take local tiles j, j + per,
+  // ... in entry-fastest order.  EX = 2 keeps an XCD's B digits (half the entries) closer to resident
+  // in its L2 beside the A digits of the sample tiles in flight (-3% GEMM time against EX = 1, which
+  // re-reads all of B per sample tile; EX = 4 -2%)
+  const int ny = a.ny, nst = (a.sc + kGTileS - 1) / kGTileS;
+  const int EX = ny >= 2 ? 2 : 1, SX = 8 / EX;  // (the u launch has one entry tile)
+  const int per = gridDim.x / 8;  // blocks per XCD (1-D grid, a multiple of 8)
+  const int x = blockIdx.x % 8;
+  const int ex = x % EX, sx = x / EX;
+  const int e0 = ny * ex / EX, e1 = ny * (ex + 1) / EX;       // entry tiles of this XCD
+  const int s0 = nst * sx / SX, s1 = nst * (sx + 1) / SX;     // sample tiles of this XCD
+  const int nye = e1 - e0;
+  const int nloc = (s1 - s0) * nye;
+  const int j0 = blockIdx.x / 8;
+  if (j0 >= nloc) return;
+  const int ntile = (nloc - j0 + per - 1) / per;
   const int nks = (16 * ((inf.L + 15) / 16)) / 16;  // 64-slot K steps: 4 Ls16 / 64
+  const int nsteps = ntile * nks;
   const int64_t planeA = a.rows * a.kstride, planeB = (int64_t)NE * a.kstride;
   const int g = lane >> 4;
   // A: lane (row lane & 15, 16-slot group g of the K step); planes stored [group][sample][16 B]
-  const uint8_t* A0 = a.adig + (u_tile ? 4 * planeA : 0) +
-                      ((int64_t)g * a.rows + s_tile + 32 * wave_s + (lane & 15)) * 16;
-  const uint8_t* B0 = a.bdig + (int64_t)e_tile * a.kstride;
+  const int64_t a_lane = ((int64_t)g * a.rows + 32 * wave_s + (lane & 15)) * 16;
   const uint32_t bs_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)&Bs[0][0];
   // B piece geometry (16 entry rows x 64 B per 1 KiB piece, 4 per plane; ND pieces per wave per K
   // step): row (lane >> 2) of the piece; K granule g of a row sits in LDS slot (g + 2 ((row >> 2) & 3))
@@ -262,26 +277,33 @@ __global__ __launch_bounds__(256, ND == 3 ? 3 : 2) void gemm_i8_kernel(GemmI8Arg
     const int p = piece >> 2, row = (piece & 3) * 16 + prow;
     boff[i] = (uint32_t)(p * planeB + (int64_t)row * a.kstride + 16 * (((lane & 3) + 2 * ((row >> 2) & 3)) & 3));
   }
-  auto stage_b = [&](int ks, int buf) {
+  auto tile_s = [&](int i) { return (s0 + (j0 + i * per) / nye) * kGTileS; };
+  auto tile_e = [&](int i) { return (a.e_tile0 + e0 + (j0 + i * per) % nye) * kGTileE; };
+  // global K step gs = tile i, step ks: B DMA into buffer buf and A loads into registers r
+  auto prefetch = [&](int gs, v4i (&r)[2][ND], int buf) {
+    const int i = gs / nks, ks = gs - i * nks;
+    const int e_tile = tile_e(i);
+    const uint8_t* B0 = a.bdig + (int64_t)e_tile * a.kstride + ks * 64;
 #pragma unroll
-    for (int i = 0; i < ND; ++i)
-      dma_piece(B0 + ks * 64, boff[i], bs_base + (uint32_t)(buf * (ND * kGTileE * 64) + (wave_s * ND + i) * 1024));
-  };
-  auto load_a = [&](int ks, v4i (&r)[2][ND]) {
+    for (int pi = 0; pi < ND; ++pi)
+      dma_piece(B0, boff[pi], bs_base + (uint32_t)(buf * (ND * kGTileE * 64) + (wave_s * ND + pi) * 1024));
+    const uint8_t* A0 = a.adig + (e_tile >= Ep ? 4 * planeA : 0) + (int64_t)tile_s(i) * 16 + a_lane +
+                        (int64_t)ks * 4 * a.rows * 16;
 #pragma unroll
     for (int rt = 0; rt < 2; ++rt)
 #pragma unroll
-      for (int p = 0; p < ND; ++p)
-        r[rt][p] = *reinterpret_cast<const v4i*>(A0 + p * planeA + (int64_t)ks * 4 * a.rows * 16 + rt * 256);
+      for (int p = 0; p < ND; ++p) r[rt][p] = *reinterpret_cast<const v4i*>(A0 + p * planeA + rt * 256);
     __builtin_amdgcn_sched_barrier(0);  // the prefetch goes out before the step's MFMAs
   };
   v4i acc[ND][2][4];
+  auto zero_acc = [&]() {
 #pragma unroll
-  for (int l = 0; l < ND; ++l)
+    for (int l = 0; l < ND; ++l)
 #pragma unroll
-    for (int rt = 0; rt < 2; ++rt)
+      for (int rt = 0; rt < 2; ++rt)
 #pragma unroll
-      for (int ct = 0; ct < 4; ++ct) acc[l][rt][ct] = (v4i){0, 0, 0, 0};
+        for (int ct = 0; ct < 4; ++ct) acc[l][rt][ct] = (v4i){0, 0, 0, 0};
+  };
   // one K step's MFMAs on A registers Ar and LDS buffer buf
   auto compute = [&](const v4i (&Ar)[2][ND], int buf) {
     const uint8_t* Bc = Bs[buf];
@@ -303,10 +325,39 @@ __global__ __launch_bounds__(256, ND == 3 ? 3 : 2) void gemm_i8_kernel(GemmI8Arg
       __builtin_amdgcn_sched_barrier(0);  // one column tile's B reads + MFMAs at a time (registers)
     }
   };
+  // epilogue of tile i: D lane map of 16x16x64: sample 4 (lane >> 4) + r, entry lane & 15
+  auto epilogue = [&](int i) {
+    const int s_tile = tile_s(i), e_tile = tile_e(i);
+    const bool u_tile = e_tile >= Ep;
+#pragma unroll
+    for (int ct = 0; ct < 4; ++ct) {
+      const int e = e_tile + 16 * ct + (lane & 15);
+      const int col = u_tile ? e - Ep : e;
+      if (u_tile ? col >= K : col >= E) continue;
+      const double sc = a.ent[e], off0 = a.ent[NE + e];
+#pragma unroll
+      for (int rt = 0; rt < 2; ++rt) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int sl = s_tile + 32 * wave + 16 * rt + 4 * (lane >> 4) + r;
+          if (sl >= a.sc) continue;
+          // sum_l 2^(48 - 8 l) C_l, least significant level first
+          double val = (double)acc[ND - 1][rt][ct][r] * __builtin_ldexp(1.0, 48 - 8 * (ND - 1));
+#pragma unroll
+          for (int l = ND - 2; l >= 0; --l) val = fma((double)acc[l][rt][ct][r], __builtin_ldexp(1.0, 48 - 8 * l), val);
+          val = (val + off0) * sc;
+          if (u_tile) a.U[(int64_t)sl * K + col] = val;
+          else a.G[(int64_t)sl * E + col] = val;
+        }
+      }
+    }
+    zero_acc();
+  };
   // Wait for this wave's outstanding loads (the next step's B DMA, which the compiler cannot see, and
   // A loads into Ar), then hand Ar through an empty asm that "redefines" it: the compiler's waitcnt
   // pass would otherwise still count those loads as pending and, at the first MFMA reading Ar, insert
   // a vmcnt(N) that does not count the DMA issued after them -- draining the NEXT step's prefetch.
+  // (The epilogue's stores are outstanding here too; the vmcnt(0) waits for them as well.)
   auto land = [&](v4i (&Ar)[2][ND]) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
@@ -315,50 +366,25 @@ __global__ __launch_bounds__(256, ND == 3 ? 3 : 2) void gemm_i8_kernel(GemmI8Arg
       for (int p = 0; p < ND; ++p) asm volatile("" : "+v"(Ar[rt][p]));
     __syncthreads();  // everyone's DMA landed; the other LDS buffer is free again
   };
-  // Two A register sets used in turn (steps of even / odd ks) and the loop unrolled by two: no
+  // Two A register sets used in turn (even / odd global steps) and the loop unrolled by two: no
   // register copies; the conditional prefetches are safe for the waitcnt pass because every path
   // goes through land() before the registers are read.
+  zero_acc();
   v4i A0r[2][ND], A1r[2][ND];
-  stage_b(0, 0);
-  load_a(0, A0r);
+  prefetch(0, A0r, 0);
   land(A0r);
-  for (int ks = 0; ks < nks; ks += 2) {
-    const bool m1 = ks + 1 < nks, m2 = ks + 2 < nks;
-    if (m1) {
-      stage_b(ks + 1, 1);
-      load_a(ks + 1, A1r);
-    }
+  for (int gs = 0; gs < nsteps; gs += 2) {
+    const bool m1 = gs + 1 < nsteps, m2 = gs + 2 < nsteps;
+    if (m1) prefetch(gs + 1, A1r, 1);
     compute(A0r, 0);
+    if ((gs + 1) % nks == 0) epilogue(gs / nks);
     land(A1r);
-    if (m2) {
-      stage_b(ks + 2, 0);
-      load_a(ks + 2, A0r);
+    if (m2) prefetch(gs + 2, A0r, 0);
+    if (m1) {
+      compute(A1r, 1);
+      if ((gs + 2) % nks == 0) epilogue((gs + 1) / nks);
     }
-    if (m1) compute(A1r, 1);
     land(A0r);
-  }
-  // epilogue: D lane map of 16x16x64: sample 4 (lane >> 4) + r, entry lane & 15
-#pragma unroll
-  for (int ct = 0; ct < 4; ++ct) {
-    const int e = e_tile + 16 * ct + (lane & 15);
-    const int col = u_tile ? e - Ep : e;
-    if (u_tile ? col >= K : col >= E) continue;
-    const double sc = a.ent[e], off0 = a.ent[NE + e];
-#pragma unroll
-    for (int rt = 0; rt < 2; ++rt) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int sl = s_tile + 32 * wave + 16 * rt + 4 * (lane >> 4) + r;
-        if (sl >= a.sc) continue;
-        // sum_l 2^(48 - 8 l) C_l, least significant level first
-        double val = (double)acc[ND - 1][rt][ct][r] * __builtin_ldexp(1.0, 48 - 8 * (ND - 1));
-#pragma unroll
-        for (int l = ND - 2; l >= 0; --l) val = fma((double)acc[l][rt][ct][r], __builtin_ldexp(1.0, 48 - 8 * l), val);
-        val = (val + off0) * sc;
-        if (u_tile) a.U[(int64_t)sl * K + col] = val;
-        else a.G[(int64_t)sl * E + col] = val;
-      }
-    }
   }
 }
 
@@ -388,16 +414,22 @@ hipError_t launch_gemm_i8(const GemmI8Args& a0, hipStream_t s) {
   const int K = a0.k, Ep = 64 * ((K * (K + 1) / 2 + 63) / 64);
   const int ng = Ep / kGTileE, nu = i8_gemm_entries(K) / kGTileE - ng;
   const int nst = (a0.sc + kGTileS - 1) / kGTileS;
-  auto grid = [&](int ny) { return dim3((unsigned)((nst * ny + 7) / 8 * 8)); };  // 1-D, padded for the XCD remap
+  // persistent grid: at most the resident blocks (3 or 2 per CU), a multiple of 8 (one run per XCD)
+  int dev = 0, ncu = 256;
+  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+  auto grid = [&](int ny, int per_cu) {
+    const int nb = std::min(nst * ny, per_cu * ncu);
+    return dim3((unsigned)((nb + 7) / 8 * 8));
+  };
   GemmI8Args a = a0;
   if (a0.nd == 4) {
     a.e_tile0 = 0; a.ny = ng + nu;
-    hipLaunchKernelGGL(gemm_i8_kernel<4>, grid(a.ny), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(gemm_i8_kernel<4>, grid(a.ny, 2), dim3(256), 0, s, a);
   } else {
     a.e_tile0 = 0; a.ny = ng;
-    hipLaunchKernelGGL(gemm_i8_kernel<3>, grid(a.ny), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(gemm_i8_kernel<3>, grid(a.ny, 3), dim3(256), 0, s, a);
     a.e_tile0 = ng; a.ny = nu;
-    hipLaunchKernelGGL(gemm_i8_kernel<4>, grid(a.ny), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(gemm_i8_kernel<4>, grid(a.ny, 2), dim3(256), 0, s, a);
   }
   return hipGetLastError();
 }

@@ -207,8 +207,10 @@ __global__ __launch_bounds__(256) void prep_kernel(PrepArgs a) {
         double* sr = a.srow + (sb + j) * 8;
 #pragma unroll
         for (int w = 0; w < 6; ++w) sr[w] = sc[w];
-        sr[6] = 0.0;
-        sr[7] = 0.0;
+        // the int8 path's per-slot quantisation scales (gemm_i8.hip weights_i8_kernel), hoisted out
+        // of the per-sample loop: u~ scale 2^31 / beta and Gram scale (omega^2 + sigma^2) 2^32
+        sr[6] = kI8ScaleU / u_bound(sc[1], sc[3], sc[2]);
+        sr[7] = (sc[4] + sc[2]) * kI8ScaleG;
       }
     }
   }

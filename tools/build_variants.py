@@ -11,9 +11,9 @@ sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 from gp_dla_detection_amd.build import build
 
 VARIANTS: dict = {
-    "occ3pipe": {"GPDLA_GEMM_OCC": 3},
-    "occ3nopipe": {"GPDLA_GEMM_OCC": 3, "GPDLA_PIPE": 0},
-    "occ2pipe": {"GPDLA_GEMM_OCC": 2},
+    "wide3": {},
+    "wide2": {"GPDLA_WIDE_STAGES": 2},
+    "narrow": {"GPDLA_GEMM_WIDE": 0},
 }
 if __name__ == "__main__":
     names = sys.argv[1:] or list(VARIANTS)
