@@ -61,8 +61,13 @@ __global__ __launch_bounds__(256) void convert_gemm_i8_kernel(ConvertGemmI8Args 
   mx = fmax(fmax(s_mx[0][le], s_mx[1][le]), fmax(s_mx[2][le], s_mx[3][le]));
   const double s_e = mx > 0.0 ? mx * (1.0 / (127.0 * 0x1p24)) : 1.0;  // |X_B| <= 127 2^24
   long long colsum = 0;
-  uint8_t* base = a.bdig + a.bbase[q] + (int64_t)e * kstride + (int64_t)g * Ls16;
-  const int64_t plane = (int64_t)NE * kstride;
+  // B layout (the GEMM's LDS image, pre-swizzled): [entry tile 64][K step][plane 4][row 64][64 B], K
+  // granule gr of row r at 16-B slot (gr + 2 ((r >> 2) & 3)) & 3 -- one K step of an entry tile is a
+  // contiguous 4 KiB per plane, so each 1-KiB DMA piece reads 8 whole cache lines
+  const int64_t nksmax = kstride / 64;
+  const int r = e & 63;
+  uint8_t* tbase = a.bdig + a.bbase[q] + (int64_t)(e >> 6) * nksmax * 4 * 4096 + (int64_t)r * 64;
+  const int rsw = 2 * ((r >> 2) & 3);
   for (int t0 = 0; t0 < Ls16; t0 += 16) {
     uint32_t pl[4][4];
 #pragma unroll
@@ -82,10 +87,12 @@ __global__ __launch_bounds__(256) void convert_gemm_i8_kernel(ConvertGemmI8Args 
         pl[3][w] |= (uint32_t)(d3 & 255) << (8 * b);
       }
     }
+    const int kk = g * Ls16 + t0, ks = kk >> 6, gr = (kk >> 4) & 3;
+    uint8_t* dst = tbase + (int64_t)ks * 4 * 4096 + 16 * ((gr + rsw) & 3);
 #pragma unroll
     for (int j = 0; j < 4; ++j)
       if (j < (is_u ? 4 : a.nd))  // u entries keep 4 digits (launch_gemm_i8)
-        *reinterpret_cast<uint4*>(base + j * plane + t0) = make_uint4(pl[j][0], pl[j][1], pl[j][2], pl[j][3]);
+        *reinterpret_cast<uint4*>(dst + j * 4096) = make_uint4(pl[j][0], pl[j][1], pl[j][2], pl[j][3]);
   }
   s_cs[g][le] = colsum;
   __syncthreads();
@@ -258,32 +265,27 @@ __global__ __launch_bounds__(256, ND == 3 ? 3 : 2) void gemm_i8_kernel(GemmI8Arg
   const int ntile = (nloc - j0 + per - 1) / per;
   const int nks = (16 * ((inf.L + 15) / 16)) / 16;  // 64-slot K steps: 4 Ls16 / 64
   const int nsteps = ntile * nks;
-  const int64_t planeA = a.rows * a.kstride, planeB = (int64_t)NE * a.kstride;
+  const int64_t planeA = a.rows * a.kstride, nksmax = a.kstride / 64;
   const int g = lane >> 4;
   // A: lane (row lane & 15, 16-slot group g of the K step); planes stored [group][sample][16 B]
   const int64_t a_lane = ((int64_t)g * a.rows + 32 * wave_s + (lane & 15)) * 16;
   const uint32_t bs_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)&Bs[0][0];
-  // B piece geometry (16 entry rows x 64 B per 1 KiB piece, 4 per plane; ND pieces per wave per K
-  // step): row (lane >> 2) of the piece; K granule g of a row sits in LDS slot (g + 2 ((row >> 2) & 3))
-  // & 3 of its 64 B.  ds_read_b128 serves a wave in the 16-lane groups {0-3,12-15,20-27},
-  // {4-11,16-19,28-31} (+32); with row = lane & 15 and g = lane >> 4 every group then hits 16 distinct
-  // 16-B slots of the 256-B bank row (the XOR form g ^ ((row >> 2) & 3) paired lanes 0-3 with 20-23:
-  // 2-way conflicts)
-  const int prow = lane >> 2;
+  // B pieces (16 entry rows x 64 B per 1 KiB piece, 4 per plane; ND pieces per wave per K step) are
+  // contiguous 1 KiB runs of the pre-swizzled global image (convert_gemm_i8_kernel): K granule g of
+  // row `row` sits in 16-B slot (g + 2 ((row >> 2) & 3)) & 3 of its 64 B.  ds_read_b128 serves a wave
+  // in the 16-lane groups {0-3,12-15,20-27}, {4-11,16-19,28-31} (+32); with row = lane & 15 and
+  // g = lane >> 4 every group then hits 16 distinct 16-B slots of the 256-B bank row (the XOR form
+  // g ^ ((row >> 2) & 3) paired lanes 0-3 with 20-23: 2-way conflicts)
   uint32_t boff[ND];
 #pragma unroll
-  for (int i = 0; i < ND; ++i) {
-    const int piece = wave_s * ND + i;
-    const int p = piece >> 2, row = (piece & 3) * 16 + prow;
-    boff[i] = (uint32_t)(p * planeB + (int64_t)row * a.kstride + 16 * (((lane & 3) + 2 * ((row >> 2) & 3)) & 3));
-  }
+  for (int i = 0; i < ND; ++i) boff[i] = (uint32_t)((wave_s * ND + i) * 1024 + lane * 16);  // plane p at p 4 KiB
   auto tile_s = [&](int i) { return (s0 + (j0 + i * per) / nye) * kGTileS; };
   auto tile_e = [&](int i) { return (a.e_tile0 + e0 + (j0 + i * per) % nye) * kGTileE; };
   // global K step gs = tile i, step ks: B DMA into buffer buf and A loads into registers r
   auto prefetch = [&](int gs, v4i (&r)[2][ND], int buf) {
     const int i = gs / nks, ks = gs - i * nks;
     const int e_tile = tile_e(i);
-    const uint8_t* B0 = a.bdig + (int64_t)e_tile * a.kstride + ks * 64;
+    const uint8_t* B0 = a.bdig + ((int64_t)(e_tile >> 6) * nksmax + ks) * 4 * 4096;
 #pragma unroll
     for (int pi = 0; pi < ND; ++pi)
       dma_piece(B0, boff[pi], bs_base + (uint32_t)(buf * (ND * kGTileE * 64) + (wave_s * ND + pi) * 1024));

@@ -11,9 +11,7 @@ sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 from gp_dla_detection_amd.build import build
 
 VARIANTS: dict = {
-    "wide3": {},
-    "wide2": {"GPDLA_WIDE_STAGES": 2},
-    "narrow": {"GPDLA_GEMM_WIDE": 0},
+    "base": {},
 }
 if __name__ == "__main__":
     names = sys.argv[1:] or list(VARIANTS)
