@@ -144,11 +144,15 @@ __global__ __launch_bounds__(256) void weights_i8_kernel(WeightsI8Args a) {
   double w3 = raw(lamp[3]), w4 = raw(lamp[4]), w5 = raw(lamp[5]);
   double q1 = 0.0, pm = 1.0;
   int pe = 0;
-  const int64_t plane = a.rows * a.kstride;
-  // A planes are stored [16-slot group][sample][16 B]: a lane's 16-byte store per group sits next to
-  // its neighbours' (coalesced rows of 1 KiB per wave)
-  uint8_t* ag = a.adig + (int64_t)sl * 16 + (int64_t)(g * Ls16 / 16) * a.rows * 16;
-  uint8_t* au = ag + 4 * plane;
+  // A layout (tile-major, like B): [type 2][sample tile 128][K step][plane 4][group 4][sample 128][16 B];
+  // one K step of a sample tile is a contiguous 32 KiB (a lane's 16-byte store per group sits next to
+  // its neighbours': coalesced runs of 1 KiB per wave)
+  const int64_t nksmax = a.kstride / 64;
+  const int64_t type_bytes = a.rows * a.kstride * 4;
+  uint8_t* ag = a.adig + (((int64_t)(sl >> 7) * nksmax * 16) * 128 + (sl & 127)) * 16;
+  uint8_t* au = ag + type_bytes;
+  // byte offset of 16-slot group G (= K index / 16), plane i
+  auto goff = [&](int G, int i) { return ((int64_t)((G >> 2) * 4 + i) * 4 + (G & 3)) * 2048; };
   for (int tg = t0; tg < t1; tg += 16) {
     // per slot as the fp64 weights kernel (its core branch is coherent: a block's 64 samples are
     // consecutive in z), 16 slots' quantised weights collected for the digit planes
@@ -193,8 +197,9 @@ __global__ __launch_bounds__(256) void weights_i8_kernel(WeightsI8Args a) {
     if (active) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        if (i < a.nd) *reinterpret_cast<v4i*>(ag + i * plane + (int64_t)(tg / 16) * a.rows * 16) = digit_plane(xg, i);
-        *reinterpret_cast<v4i*>(au + i * plane + (int64_t)(tg / 16) * a.rows * 16) = digit_plane(xu, i);  // 4 u digits
+        const int G = (g * Ls16 + tg) >> 4;
+        if (i < a.nd) *reinterpret_cast<v4i*>(ag + goff(G, i)) = digit_plane(xg, i);
+        *reinterpret_cast<v4i*>(au + goff(G, i)) = digit_plane(xu, i);  // 4 u digits
       }
     }
   }
@@ -265,10 +270,11 @@ __global__ __launch_bounds__(256, ND == 3 ? 3 : 2) void gemm_i8_kernel(GemmI8Arg
   const int ntile = (nloc - j0 + per - 1) / per;
   const int nks = (16 * ((inf.L + 15) / 16)) / 16;  // 64-slot K steps: 4 Ls16 / 64
   const int nsteps = ntile * nks;
-  const int64_t planeA = a.rows * a.kstride, nksmax = a.kstride / 64;
+  const int64_t nksmax = a.kstride / 64, type_bytes = a.rows * a.kstride * 4;
   const int g = lane >> 4;
-  // A: lane (row lane & 15, 16-slot group g of the K step); planes stored [group][sample][16 B]
-  const int64_t a_lane = ((int64_t)g * a.rows + 32 * wave_s + (lane & 15)) * 16;
+  // A: lane (row lane & 15, 16-slot group g of the K step) in the tile-major layout of
+  // weights_i8_kernel: [type][sample tile][K step][plane 4][group 4][sample 128][16 B]
+  const int64_t a_lane = ((int64_t)g * 128 + 32 * wave_s + (lane & 15)) * 16;
   const uint32_t bs_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)&Bs[0][0];
   // B pieces (16 entry rows x 64 B per 1 KiB piece, 4 per plane; ND pieces per wave per K step) are
   // contiguous 1 KiB runs of the pre-swizzled global image (convert_gemm_i8_kernel): K granule g of
@@ -289,12 +295,12 @@ __global__ __launch_bounds__(256, ND == 3 ? 3 : 2) void gemm_i8_kernel(GemmI8Arg
 #pragma unroll
     for (int pi = 0; pi < ND; ++pi)
       dma_piece(B0, boff[pi], bs_base + (uint32_t)(buf * (ND * kGTileE * 64) + (wave_s * ND + pi) * 1024));
-    const uint8_t* A0 = a.adig + (e_tile >= Ep ? 4 * planeA : 0) + (int64_t)tile_s(i) * 16 + a_lane +
-                        (int64_t)ks * 4 * a.rows * 16;
+    const uint8_t* A0 = a.adig + (e_tile >= Ep ? type_bytes : 0) +
+                        ((int64_t)(tile_s(i) >> 7) * nksmax + ks) * 16 * 2048 + a_lane;
 #pragma unroll
     for (int rt = 0; rt < 2; ++rt)
 #pragma unroll
-      for (int p = 0; p < ND; ++p) r[rt][p] = *reinterpret_cast<const v4i*>(A0 + p * planeA + rt * 256);
+      for (int p = 0; p < ND; ++p) r[rt][p] = *reinterpret_cast<const v4i*>(A0 + p * 8192 + rt * 256);
     __builtin_amdgcn_sched_barrier(0);  // the prefetch goes out before the step's MFMAs
   };
   v4i acc[ND][2][4];
