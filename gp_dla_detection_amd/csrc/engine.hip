@@ -449,9 +449,10 @@ int gpdla_engine_process(gpdla_engine* e, const gpdla_spectra* sp, const gpdla_r
   // panel-GEMM sample chunks: the S + 1 samples (null model included) in equal chunks of at most
   // kMaxChunk.  configs[4] (S + 1 = 100,001) measured 46.2 Mevals/s with 16,384-sample chunks (6
   // full + a 1,697-sample tail that fills a sixth of the GPU), 47.4 with 7 equal chunks, 48.5 with
-  // 2 and 49.1 with one (profiles/r2l): larger launches keep the weights kernel's and the GEMM's
-  // grids full, and the workspaces (A digits 8 B, Gram 8 k(k+1)/2 B per sample and slot / entry)
-  // stay a few GB in 288 GB of HBM.
+  // 2 and 49.1 with one (profiles/r2l); again after the round-2 GEMM work: 53.5 (6 equal chunks),
+  // 58.8 (4), 61.7 (2), 63.1 (one; profiles/r2/c5_ab): smaller chunks keep the A digits in the
+  // Infinity Cache (GEMM -10%) but cost more in the weights and LDL^T launches.  The workspaces (A
+  // digits 8 B, Gram 8 k(k+1)/2 B per sample and slot / entry) stay a few GB in 288 GB of HBM.
   constexpr int64_t kMaxChunk = 131072;
   const int64_t nchunk = (e->S + 1 + kMaxChunk - 1) / kMaxChunk;
   const int64_t sc_max = (e->S + 1 + nchunk - 1) / nchunk;

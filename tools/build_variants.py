@@ -12,6 +12,9 @@ from gp_dla_detection_amd.build import build
 
 VARIANTS: dict = {
     "base": {},
+    "ch50k": {"GPDLA_MAX_CHUNK": 50001},
+    "ch25k": {"GPDLA_MAX_CHUNK": 25001},
+    "ch16k": {"GPDLA_MAX_CHUNK": 16667},
 }
 if __name__ == "__main__":
     names = sys.argv[1:] or list(VARIANTS)
