@@ -385,6 +385,9 @@ static int run_panel_gemm(gpdla_engine* e, bool i8, int64_t nq, const int64_t* h
         gi.info = e->d_info; gi.q = (int32_t)q; gi.k = K; gi.kstride = ks; gi.rows = rows; gi.sc = sc; gi.nd = e->i8_nd;
         gi.adig = adig; gi.bdig = e->d_pi8 + h_cb[q];
         gi.ent = e->d_pent + q * 2 * (int64_t)i8_gemm_entries(K); gi.G = G; gi.U = U;
+        // the 24-bit path stores the Gram in fp32 (half the GEMM -> LDL^T round trip; adds ~1e-8
+        // to its ~2e-7 from fp64, tests/support/emulate_i8.py), in the same workspace
+        gi.G32 = e->i8_nd == 3 ? reinterpret_cast<float*>(G) : nullptr;
         TimedLaunch tg{};
         int rc;
         if ((rc = record_start(e, &tg, 3))) return rc;
@@ -414,6 +417,7 @@ static int run_panel_gemm(gpdla_engine* e, bool i8, int64_t nq, const int64_t* h
       LdlArgs da{};
       da.info = e->d_info; da.q = (int32_t)q; da.k = K;
       da.G = G; da.U = U; da.q1p = q1p; da.ldp = ldp;
+      da.G32 = (i8 && e->i8_nd == 3) ? reinterpret_cast<const float*>(G) : nullptr;
       da.S = e->S; da.s0 = s0; da.sc = sc; da.perm = e->d_perm;
       da.sample_ll = o_sll ? o_sll + q * ld : nullptr; da.ll_null = o_null + q; da.status = e->d_status;
       HIP_TRY(launch_ldl_batch(da, st));

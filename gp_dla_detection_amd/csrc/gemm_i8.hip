@@ -355,6 +355,7 @@ __global__ __launch_bounds__(256, ND == 3 ? 3 : 2) void gemm_i8_kernel(GemmI8Arg
           for (int l = ND - 2; l >= 0; --l) val = fma((double)acc[l][rt][ct][r], __builtin_ldexp(1.0, 48 - 8 * l), val);
           val = (val + off0) * sc;
           if (u_tile) a.U[(int64_t)sl * K + col] = val;
+          else if (a.G32) a.G32[(int64_t)sl * E + col] = (float)val;
           else a.G[(int64_t)sl * E + col] = val;
         }
       }

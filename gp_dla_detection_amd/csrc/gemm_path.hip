@@ -144,7 +144,11 @@ __device__ inline void wave_sync() {
 // B[k][j] at 16k + 4b + j, D[i][j] at 16i + 4b + j -- so a D-layout register passed as B is the
 // tile itself and passed as A is its transpose, which is what both products need.  After the NT
 // block steps log det B = sum_{p<k} log D_p and r'K^-1 r = D_k (log_mvnpdf_low_rank.m:24-32).
-template <int NT>
+template <typename GT> __device__ inline const GT* gram_of(const LdlArgs& a);
+template <> __device__ inline const double* gram_of<double>(const LdlArgs& a) { return a.G; }
+template <> __device__ inline const float* gram_of<float>(const LdlArgs& a) { return a.G32; }
+
+template <int NT, typename GT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT <= 13 ? 2 : 1))) void ldl_mfma_kernel(LdlArgs a) {
   constexpr int NTT = NT * (NT + 1) / 2;
   __shared__ __attribute__((aligned(16))) double diag_all[4][2][64];  // double-buffered by J parity
@@ -167,7 +171,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT <= 13 ? 
   }
   const int64_t E = (int64_t)K * (K + 1) / 2;
   const int slc = live ? sl : 0;  // idle samples of the last wave compute on sample 0, discarded
-  const double* Gs = a.G + (int64_t)slc * E;
+  const GT* Gs = gram_of<GT>(a) + (int64_t)slc * E;  // fp64, or fp32 on the 24-bit int8 path
   const double* Us = a.U + (int64_t)slc * K;
   const double q1 = sum_parts(a.q1p + (int64_t)slc * kWeightParts);
   const double logdet_d = sum_parts(a.ldp + (int64_t)slc * kWeightParts);
@@ -189,19 +193,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT <= 13 ? 
       double v;
       if (I < NT - 1) {
         const int tb = 10 * L + 16 * (L * (NT - 2) - L * (L - 1) / 2) + (I == L ? 0 : 10 + 16 * (I - L - 1));
-        v = I == L ? Gs[tb + ldiag] + done : Gs[tb + loff];   // B = I + Gram
+        v = I == L ? (double)Gs[tb + ldiag] + done : (double)Gs[tb + loff];   // B = I + Gram
       } else if (L < NT - 1) {
         // rows 4L + ti < k, column c = 4 (NT - 1) + tj: Gram if tj < w, u if tj == w, padding after
         const int r = 4 * L + ti;
-        const double g = Gs[base2 + L * 4 * w + ti * w + min(tj, max(w - 1, 0))], u = Us[r];
+        const double g = (double)Gs[base2 + L * 4 * w + ti * w + min(tj, max(w - 1, 0))], u = Us[r];
         v = tj < w ? g : (tj == w ? u : 0.0);
       } else {
         // corner tile: Gram (di <= dj < w), then u (dj == w, di < w), r'D^-1 r (di == dj == w),
         // identity padding
         const int r = 4 * L + di;
         const int cw = max(w, 1);
-        const double g = Gs[base2 + L * 4 * w + min(di, cw - 1) * w - min(di, cw - 1) * (min(di, cw - 1) - 1) / 2 +
-                            (min(dj, cw - 1) - min(di, cw - 1))];
+        const double g = (double)Gs[base2 + L * 4 * w + min(di, cw - 1) * w - min(di, cw - 1) * (min(di, cw - 1) - 1) / 2 +
+                                    (min(dj, cw - 1) - min(di, cw - 1))];
         const double u = Us[min(r, K - 1)];
         v = dj < w ? g + done : (dj == w ? (di < w ? u : q1) : done);
       }
@@ -300,7 +304,11 @@ hipError_t launch_ldl_batch(const LdlArgs& a, hipStream_t s) {
   // matrix-core LDL^T: 16 samples per block, NT = ceil((k + 1) / 4) tiles per side
   const dim3 grid((unsigned)((a.sc + 15) / 16)), blk(256);
   switch ((a.k + 1 + 3) / 4) {
-#define NT_CASE(n) case n: hipLaunchKernelGGL(ldl_mfma_kernel<n>, grid, blk, 0, s, a); break;
+#define NT_CASE(n)                                                              \
+  case n:                                                                       \
+    if (a.G32) hipLaunchKernelGGL((ldl_mfma_kernel<n, float>), grid, blk, 0, s, a);  \
+    else hipLaunchKernelGGL((ldl_mfma_kernel<n, double>), grid, blk, 0, s, a);       \
+    break;
     NT_CASE(1) NT_CASE(2) NT_CASE(3) NT_CASE(4) NT_CASE(5) NT_CASE(6) NT_CASE(7) NT_CASE(8) NT_CASE(9)
     NT_CASE(10) NT_CASE(11) NT_CASE(12) NT_CASE(13) NT_CASE(14) NT_CASE(15) NT_CASE(16) NT_CASE(17)
 #undef NT_CASE

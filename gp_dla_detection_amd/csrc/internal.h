@@ -158,6 +158,7 @@ struct LdlArgs {
   int32_t q;
   int32_t k;
   const double* G;               // [sc][k(k+1)/2] Gram per sample, entries in gram_tile_index order
+  const float* G32;              // the same in fp32 (panel_gemm_i8_24), or nullptr: then G is read
   const double* U;               // [sc][k]
   const double* q1p;
   const double* ldp;
@@ -321,6 +322,7 @@ struct GemmI8Args {
   const uint8_t* bdig;           // this spectrum's B planes
   const double* ent;             // this spectrum's [2][entries]
   double* G;                     // [sc][E]
+  float* G32;                    // if set, the Gram goes here in fp32 instead (24-bit path)
   double* U;                     // [sc][k]
 };
 
