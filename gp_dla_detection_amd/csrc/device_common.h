@@ -275,7 +275,11 @@ __device__ inline double ldl_factor(double (&A)[(K + 3) / 4][4 * ((K + 3) / 4)],
   for (int p = 0; p < K; ++p) {
     const double Dp = quad_bcast(A[p >> 2][p], p & 3);
     bad |= !(Dp > 0.0) || !(Dp < INFINITY);
-    const double invD = 1.0 / Dp;
+    // v_rcp_f64 + two Newton steps (within an ulp of 1/Dp) instead of the IEEE division sequence;
+    // a pivot that is not positive and finite is flagged above and the result discarded
+    double invD = __builtin_amdgcn_rcp(Dp);
+    invD = fma(invD, fma(-Dp, invD, 1.0), invD);
+    invD = fma(invD, fma(-Dp, invD, 1.0), invD);
     pb *= Dp;
     if ((p & 3) == 3) {
       int ex;

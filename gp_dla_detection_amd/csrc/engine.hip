@@ -255,18 +255,21 @@ int gpdla_engine_create(int32_t device, const gpdla_model* model, const gpdla_sa
   int rc = check_device(device);
   if (rc) return rc;
   if ((rc = validate_params(params))) return rc;
-  const bool fused_ok = rank_supported(model->k);
+  // fused paths: a rank between the compiled ones runs on the next compiled rank, M zero-padded
+  // (fused_rank, kernels.hip: exact)
+  const int k_fused = fused_rank(model->k), k_i8 = i8_fused_rank(model->k);
+  const bool fused_ok = k_fused > 0;
   const bool gemm_i8 = params->path == GPDLA_PATH_PANEL_GEMM_I8 || params->path == GPDLA_PATH_PANEL_GEMM_I8_24;
   const bool use_gemm = params->path == GPDLA_PATH_PANEL_GEMM || gemm_i8 ||
                         (params->path == GPDLA_PATH_AUTO && !fused_ok);
   const bool use_i8 = params->path == GPDLA_PATH_FUSED_I8 || gemm_i8;
   if (gemm_i8 && params->num_lines != 3)
     return set_error(GPDLA_EUNSUPPORTED, "int8 panel-GEMM path needs num_lines=3 (num_lines=%d)", params->num_lines);
-  if (params->path == GPDLA_PATH_FUSED_I8 && (!i8_supported(model->k) || params->num_lines != 3))
-    return set_error(GPDLA_EUNSUPPORTED, "int8 fused path needs k=20 and num_lines=3 (k=%d, num_lines=%d)",
+  if (params->path == GPDLA_PATH_FUSED_I8 && (k_i8 == 0 || params->num_lines != 3))
+    return set_error(GPDLA_EUNSUPPORTED, "int8 fused path needs k<=20 and num_lines=3 (k=%d, num_lines=%d)",
                      model->k, params->num_lines);
   if (!use_gemm && !fused_ok)
-    return set_error(GPDLA_EUNSUPPORTED, "rank k=%d not compiled for the fused path (4 8 10 12 16 20 24)", model->k);
+    return set_error(GPDLA_EUNSUPPORTED, "rank k=%d above the fused path's compiled ranks (<= 24)", model->k);
   if (use_gemm && (model->k < 1 || model->k > kGemmMaxK))
     return set_error(GPDLA_EUNSUPPORTED, "rank k=%d outside the panel-GEMM path's 1..%d", model->k, kGemmMaxK);
   if (model->num_rest < 2 || !model->rest_wavelengths || !model->mu || !model->M || !model->log_omega)
@@ -280,7 +283,7 @@ int gpdla_engine_create(int32_t device, const gpdla_model* model, const gpdla_sa
   HIP_TRY(hipSetDevice(device));
   gpdla_engine* e = new gpdla_engine();
   e->device = device;
-  e->K = model->k;
+  e->K = use_gemm ? model->k : (use_i8 ? k_i8 : k_fused);  // the rank the kernels run at
   e->S = samples->num_samples;
   e->gemm = use_gemm;
   e->i8 = use_i8;
@@ -301,10 +304,10 @@ int gpdla_engine_create(int32_t device, const gpdla_model* model, const gpdla_sa
     return fail(set_error(GPDLA_EDEVICE, "rocblas_create_handle failed"));
 
 
-  const size_t G = model->num_rest, K = model->k;
-  std::vector<double> Mrow(G * K);
+  const size_t G = model->num_rest, K = e->K, k_model = model->k;
+  std::vector<double> Mrow(G * K, 0.0);  // columns k_model..K-1: the fused paths' zero padding
   for (size_t g = 0; g < G; ++g)
-    for (size_t c = 0; c < K; ++c) Mrow[g * K + c] = model->M[g + c * G];  // col-major -> row-major
+    for (size_t c = 0; c < k_model; ++c) Mrow[g * K + c] = model->M[g + c * G];  // col-major -> row-major
   size_t dummy = 0;
   TRY_E(grow(&e->d_rest, &dummy, G)); dummy = 0;
   TRY_E(grow(&e->d_mu, &dummy, G)); dummy = 0;

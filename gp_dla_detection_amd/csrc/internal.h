@@ -331,6 +331,7 @@ hipError_t launch_weights_i8(const WeightsI8Args& a, hipStream_t s);
 hipError_t launch_gemm_i8(const GemmI8Args& a, hipStream_t s);
 
 bool i8_supported(int K);
+int i8_fused_rank(int k);
 int i8_chunk_bytes(int K);
 int i8_entries(int K);
 hipError_t launch_convert_i8(int K, const ConvertI8Args& a, hipStream_t s);
@@ -358,6 +359,7 @@ hipError_t launch_mvn_single(const double* y, const double* mu, const double* M_
                              const double* d, int64_t n, int32_t k, double* out,
                              int32_t* status, hipStream_t s);
 bool rank_supported(int K);
+int fused_rank(int k);
 int panel_row_doubles(int K);
 int panel_lds_row_doubles(int K);
 int scratch_doubles(int K);

@@ -662,6 +662,18 @@ bool rank_supported(int K) {
   return false;
 }
 
+// smallest compiled rank >= k (0: none).  The engine runs a rank k between the compiled ones on it
+// with M padded by zero columns: those add Gram rows/columns that are exactly 0, diagonal 1 (B = I +
+// M' D^-1 M) and u entries 0, so their LDL^T pivots are exactly 1 (log 1 = 0) and every update they
+// make subtracts an exact 0 -- the log-likelihood is the rank-k one, bit for bit.
+int fused_rank(int k) {
+  if (k < 1) return 0;
+#define X(kk) if (k <= kk) return kk;
+  GPDLA_FOR_EACH_RANK(X)
+#undef X
+  return 0;
+}
+
 int scratch_doubles(int K) {
 #define X(k) if (K == k) return Layout<k>::kES;
   GPDLA_FOR_EACH_RANK(X)

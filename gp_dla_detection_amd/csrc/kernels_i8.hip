@@ -514,6 +514,16 @@ bool i8_supported(int K) {
   return false;
 }
 
+// smallest compiled int8 fused rank >= k (0: none); lower ranks run zero-padded (fused_rank, kernels.hip;
+// a zero panel column quantises to zero digits, so the padding stays exact here too)
+int i8_fused_rank(int k) {
+  if (k < 1) return 0;
+#define X(kk) if (k <= kk) return kk;
+  GPDLA_FOR_EACH_I8_RANK(X)
+#undef X
+  return 0;
+}
+
 int i8_chunk_bytes(int K) {
 #define X(k) if (K == k) return I8Layout<k>::kChunkBytes;
   GPDLA_FOR_EACH_I8_RANK(X)

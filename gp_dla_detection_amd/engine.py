@@ -42,9 +42,9 @@ def _params_struct(p: Parameters, max_batch_spectra: int = 0, path: str = "auto"
 class Engine:
     """One engine per device: resident model, DLA samples and line-profile tables.
 
-    ``path``: "auto" (fused single-kernel sweep for the compiled ranks 4 8 10 12 16 20 24, else the
-    panel-GEMM path), "fused", or "panel_gemm" (weights kernel + dgemm + batched LDL^T; ranks
-    1..64)."""
+    ``path``: "auto" (fused single-kernel sweep for ranks 1..24 -- compiled for 4 8 10 12 16 20 24, a
+    rank in between runs on the next one with M zero-padded, exactly -- else the panel-GEMM path),
+    "fused", or "panel_gemm" (weights kernel + dgemm + batched LDL^T; ranks 1..64)."""
 
     def __init__(self, model: dict, samples: dict, params: Parameters | None = None,
                  device: int = 0, max_batch_spectra: int = 0, path: str = "auto"):

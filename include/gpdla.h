@@ -47,14 +47,16 @@ extern "C" {
 /* absorption-index handling (process_qsos.m:180,189) */
 #define GPDLA_ABSORPTION_REFERENCE 0 /* reproduce the quirk: absorption(1:n) of the m in-range values */
 #define GPDLA_ABSORPTION_UNMASKED 1  /* pair every unmasked pixel with its own profile value */
-/* Likelihood path.  AUTO = the fused single-kernel sweep for the compiled ranks
- * (4 8 10 12 16 20 24), otherwise the panel-GEMM path (weights kernel + dgemm + batched LDL^T),
- * which takes any rank 1..64 (BASELINE configs[4]: k = 50). */
+/* Likelihood path.  AUTO = the fused single-kernel sweep for ranks 1..24 (compiled for 4 8 10 12 16
+ * 20 24; a rank in between runs on the next compiled one with M padded by zero columns, which is
+ * exact: pivots 1, zero updates), otherwise the panel-GEMM path (weights kernel + dgemm + batched
+ * LDL^T), which takes any rank 1..64 (BASELINE configs[4]: k = 50). */
 #define GPDLA_PATH_AUTO 0
 #define GPDLA_PATH_FUSED 1
 #define GPDLA_PATH_PANEL_GEMM 2
 /* Fused sweep with the Gram/u contraction on the int8 matrix cores (Ozaki digit slicing, exact
- * integer accumulation, fp64 everywhere else); k = 20 with num_lines = 3.  Spectra with more than
+ * integer accumulation, fp64 everywhere else); k <= 20 (compiled for 20, lower ranks zero-padded) with
+ * num_lines = 3.  Spectra with more than
  * 30,000 pixels fall back to the fp64 fused kernel.  Agrees with the fp64 path to ~1e-10 relative. */
 #define GPDLA_PATH_FUSED_I8 3
 /* Panel-GEMM path with the Gram/u GEMMs on the int8 matrix cores (same Ozaki scheme as

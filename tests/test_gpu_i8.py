@@ -106,13 +106,26 @@ def test_i8_edge_cases():
 
 
 def test_i8_unsupported_configurations_rejected():
-    model = syn.make_model(k=16)
+    model = syn.make_model(k=21)  # above the int8 fused kernel's rank 20 (lower ranks run zero-padded)
     samples = syn.make_samples(8)
     with pytest.raises(L.GpdlaError):
-        Engine(model, samples, set_parameters(k=16), path="fused_i8")
+        Engine(model, samples, set_parameters(k=21), path="fused_i8")
     model = syn.make_model(k=20)
     with pytest.raises(L.GpdlaError):
         Engine(model, samples, set_parameters(k=20, num_lines=4), path="fused_i8")
+
+
+def test_i8_fused_lower_rank_runs_zero_padded():
+    """k = 16 on the int8 fused kernel (compiled for 20): M padded by zero columns, whose panel entries
+    quantise to zero digits -- agrees with the fp64 fused path like rank 20 does."""
+    model = syn.make_model(k=16, seed=16)
+    samples = syn.make_samples(130)
+    spectra = syn.make_dr12q_like_spectra(model, 3, seed=16, mask_fraction=0.05)
+    packed = syn.pack_spectra(spectra)
+    ref = _run(model, samples, packed, "fused")
+    out = _run(model, samples, packed, "fused_i8")
+    for key in KEYS:
+        assert _rel_err(out[key], ref[key]) < I8_TOL, (key, _rel_err(out[key], ref[key]))
 
 
 def test_i8_long_spectrum_batch_falls_back_to_fp64():

@@ -162,6 +162,46 @@ def test_other_ranks(k):
         assert _rel_err(out["log_likelihoods_no_dla"][q], ref["log_likelihood_no_dla"]) < 1e-9
 
 
+@pytest.mark.parametrize("k", [1, 3, 7, 9, 13, 17, 23])
+def test_ranks_between_compiled_ones_run_fused_zero_padded(k):
+    """A rank the fused kernel is not compiled for runs on the next compiled rank with M padded by
+    zero columns (engine.hip, fused_rank): against the oracle, and against the fp64 panel-GEMM path
+    that runs the rank natively."""
+    from oracle import gpdla_oracle as O
+    model = syn.make_model(k=k, seed=200 + k)
+    samples = syn.make_samples(40)
+    spectra = syn.make_dr12q_like_spectra(model, 2, seed=k, mask_fraction=0.05)
+    packed = syn.pack_spectra(spectra)
+    with Engine(model, samples, set_parameters(k=k)) as eng:
+        out = eng.process(packed)
+    with Engine(model, samples, set_parameters(k=k), path="panel_gemm") as eng:
+        gemm = eng.process(packed)
+    for key in ("sample_log_likelihoods_dla", "log_likelihoods_no_dla", "log_likelihoods_dla"):
+        assert _rel_err(out[key], gemm[key]) < 1e-11, key
+    for q, s in enumerate(spectra):
+        ref = O.process_spectrum(s["wavelengths"], s["flux"], s["noise_variance"], s["pixel_mask"],
+                                 s["z_qso"], model, samples["offset_samples"], samples["nhi_samples"])
+        assert _rel_err(out["sample_log_likelihoods_dla"][q], ref["sample_log_likelihoods_dla"]) < 1e-9
+        assert _rel_err(out["log_likelihoods_no_dla"][q], ref["log_likelihood_no_dla"]) < 1e-9
+
+
+def test_zero_padded_rank_is_bitwise_the_native_rank():
+    """The padding is exact: rank 8 on likelihood_kernel<8> and the same model with two zero columns
+    appended (rank 10, likelihood_kernel<10>) give bit-identical outputs."""
+    model = syn.make_model(k=8, seed=88)
+    padded = dict(model)
+    padded["M"] = np.asfortranarray(np.concatenate([model["M"], np.zeros((model["M"].shape[0], 2))], axis=1))
+    samples = syn.make_samples(70)
+    spectra = syn.make_dr12q_like_spectra(model, 3, seed=8, mask_fraction=0.05)
+    packed = syn.pack_spectra(spectra)
+    with Engine(model, samples, set_parameters(k=8), path="fused") as eng:
+        a = eng.process(packed)
+    with Engine(padded, samples, set_parameters(k=10), path="fused") as eng:
+        b = eng.process(packed)
+    for key in ("sample_log_likelihoods_dla", "log_likelihoods_no_dla", "log_likelihoods_dla"):
+        assert np.array_equal(a[key], b[key]), key
+
+
 # ------------------------------------------------------------------ full-size properties
 def test_full_size_config_properties():
     """BASELINE configs[1] shape (n = 800, k = 20, S = 10^4): oracle spot checks on a sample subset,
