@@ -24,9 +24,11 @@ adaptive quadrature otherwise; the inverse CDF is solved to full double precisio
 Newton steps, where MATLAB's fzero/integral stop at their default tolerances.  This is one-off host
 preprocessing (10^4 roots, milliseconds): it stays in numpy.
 
-Parity: the reference holds no sample file or catalogue (its data are downloaded), so the
-generator is pinned by the published definitions (RR2 digits, the MAD bandwidth rule, the
-mixture's CDF and its inverse) in tests/test_dla_samples.py, not by reference outputs.
+Parity: the reference holds no sample file or catalogue (its data are downloaded).  The RR2 Halton
+points are pinned against MATLAB's own documented output (the haltonset/scramble example: Skip 1e3,
+Leap 1e2, RR2, bases 2, 3, 5 -- reproduced to its 4 printed decimals); the density fit and inverse CDF
+by the published definitions (the MAD bandwidth rule, the mixture's CDF and its inverse), not by
+reference outputs (tests/test_dla_samples.py).
 """
 from __future__ import annotations
 

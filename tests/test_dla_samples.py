@@ -28,6 +28,22 @@ def test_halton_rr2_first_points():
     assert np.array_equal(D.halton_rr2(5, start=2), h[2:7])
 
 
+def test_halton_rr2_matches_matlab_documented_output():
+    """Pinned against MATLAB's own published output of the generator generate_dla_samples.m:8-9 calls:
+    the MathWorks documentation example for haltonset/scramble,
+
+        p = haltonset(3, 'Skip', 1e3, 'Leap', 1e2); p = scramble(p, 'RR2'); X0 = net(p, 4)
+
+    prints (4 decimals) the rows below.  Skip 1e3 drops points 0..999 (point 0 is the origin) and Leap
+    1e2 keeps every 101st point, i.e. points 1000, 1101, 1202, 1303 of the sequence in bases 2, 3, 5."""
+    documented = np.array([[0.0928, 0.6950, 0.0029],
+                           [0.6958, 0.2958, 0.8269],
+                           [0.3013, 0.6497, 0.4141],
+                           [0.9087, 0.7883, 0.2166]])
+    pts = np.vstack([D.halton_rr2(1, bases=(2, 3, 5), start=1000 + 101 * j) for j in range(4)])
+    assert np.array_equal(np.round(pts, 4), documented)
+
+
 def test_ksdensity_matches_gaussian_kde_at_the_matlab_bandwidth():
     rng = np.random.default_rng(4)
     x = rng.normal(20.6, 0.35, 500)
