@@ -30,6 +30,8 @@ What h5py sees in a file written here matches what it sees in MATLAB's: a Q-vect
 """
 from __future__ import annotations
 
+import math
+import mmap
 import os
 import struct
 import time
@@ -69,6 +71,7 @@ class LazyArray:
     shape: tuple
     dtype: np.dtype
     fill: Callable[[np.ndarray], None] | None = None
+    src: np.ndarray | None = None   # set instead of fill: written by write_transposed (pwrite, no map)
 
 
 def _dt_message(dt: np.dtype) -> bytes:
@@ -178,15 +181,10 @@ def _matlab_node(name: str, value, refs: list) -> _Node:
             arr = arr.reshape(-1, 1)                          # MATLAB column vector (oned_as column)
     if arr.size == 0:
         return _empty_node(name, arr.shape, cls, extra=attrs)
-    if arr.nbytes >= _STREAM_BYTES:
-        # large: copy straight into the file map (no transposed host copy), tile by tile in threads
-        src = arr
-
-        def fill(view, src=src):
-            fill_transposed(view, src)
-
+    if arr.nbytes >= _STREAM_BYTES and arr.ndim == 2:
+        # large: transposed band by band into the file with pwrite (write_transposed), no full host copy
         return _Node(name, "dataset", dims=tuple(reversed(arr.shape)), dtype=arr.dtype, data=None,
-                     lazy=LazyArray(arr.shape, arr.dtype, fill), attrs=[("MATLAB_class", cls)] + attrs)
+                     lazy=LazyArray(arr.shape, arr.dtype, src=arr), attrs=[("MATLAB_class", cls)] + attrs)
     data = np.asfortranarray(arr)
     return _Node(name, "dataset", dims=tuple(reversed(arr.shape)), dtype=data.dtype, data=data, lazy=None,
                  attrs=[("MATLAB_class", cls)] + attrs)
@@ -213,6 +211,39 @@ def fill_transposed(view, src, tile_rows: int = 512, tile_cols: int = 2048, thre
 
     with ThreadPoolExecutor(threads) as ex:
         list(ex.map(band, range(0, R, tile_rows)))
+
+
+def write_transposed(path: str, offset: int, src: np.ndarray, row0: int = 0, rows_total: int | None = None,
+                     band: int = 32, threads: int | None = None):
+    """Write the MATLAB-shaped 2-D array ``src`` (R x C) in column-major order -- the file's C-order
+    (C, rows_total) dataset at byte ``offset``, rows row0 .. row0 + R of the MATLAB array (one rank's
+    spectra; all of them by default) -- band by band: each thread transposes src[:, c0:c0+band] into its
+    own buffer and pwrite()s it (one write per band when the rows are all of the file's, else one per
+    file row).  No memory map of the output: a first-touch page fault per 4 KiB of a 13 GB map cost
+    more than the copy (the map-based fill ran at ~1.4 GB/s on the full-DR12Q sample array)."""
+    from concurrent.futures import ThreadPoolExecutor
+    R, C = src.shape
+    Rt = R if rows_total is None else rows_total
+    dt = np.dtype(src.dtype).newbyteorder("<")
+    if threads is None:
+        threads = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else 1))
+    fd = os.open(path, os.O_WRONLY)
+    try:
+        def run(c0):
+            c1 = min(C, c0 + band)
+            buf = np.empty((c1 - c0, R), dtype=dt)
+            buf[...] = src[:, c0:c1].T
+            runs = [(memoryview(buf).cast("B"), offset + c0 * Rt * dt.itemsize)] if Rt == R else \
+                   [(memoryview(buf[c - c0]).cast("B"), offset + (c * Rt + row0) * dt.itemsize) for c in range(c0, c1)]
+            for mv, pos in runs:
+                while len(mv):
+                    n = os.pwrite(fd, mv, pos)
+                    mv, pos = mv[n:], pos + n
+
+        with ThreadPoolExecutor(threads) as ex:
+            list(ex.map(run, range(0, C, band)))
+    finally:
+        os.close(fd)
 
 
 def _empty_node(name, shape, cls, extra=()):
@@ -395,6 +426,9 @@ def savemat73(path: str, variables: dict, created: str | None = None) -> dict:
     for n in lazies:
         reg = Region(USERBLOCK + data_addr[id(n)], tuple(int(d) for d in n.dims), np.dtype(n.dtype).str)
         regions[n.name] = reg
+        if n.lazy.src is not None:
+            write_transposed(path, reg.offset, n.lazy.src)
+            continue
         if n.lazy.fill is None:
             continue                                         # deferred: filled later via open_region
         mm = open_region(path, reg)
@@ -427,16 +461,23 @@ def open_region(path: str, region: Region, mode: str = "r+") -> np.ndarray:
 class _Reader:
     def __init__(self, path: str):
         self.f = open(path, "rb")
-        self.mm = np.memmap(path, dtype=np.uint8, mode="r")
+        # a plain mmap: slicing it returns bytes without numpy-subclass overhead (4 x 162,861 cell
+        # headers are parsed at full DR12Q); self.mm is a uint8 view of it for the superblock scan
+        self.buf = mmap.mmap(self.f.fileno(), 0, access=mmap.ACCESS_READ)
+        self.mm = np.frombuffer(self.buf, dtype=np.uint8)
         self.base = self._find_superblock()
 
     def close(self):
         del self.mm
+        try:
+            self.buf.close()
+        except BufferError:  # arrays decoded without a copy still view the map; it closes with them
+            pass
         self.f.close()
 
     def read(self, addr: int, n: int, absolute: bool = False) -> bytes:
         a = addr if absolute else self.base + addr
-        return self.mm[a:a + n].tobytes()
+        return self.buf[a:a + n]
 
     def _find_superblock(self) -> int:
         off = 0
@@ -663,7 +704,7 @@ class _Reader:
                 p += dslen
             dt, kind = self._datatype(dtb)
             dims = self._dataspace(dsb)
-            n = int(np.prod(dims)) if dims else 1
+            n = math.prod(dims) if dims else 1
             raw = body[p:p + n * dt.itemsize]
             val = np.frombuffer(raw, dtype=dt, count=n)
             if kind == "string":
@@ -672,8 +713,9 @@ class _Reader:
                 attrs[name] = val[0] if not dims else val.reshape(dims)
         return attrs
 
-    def dataset(self, addr: int):
-        msgs = self.messages(addr)
+    def dataset(self, addr: int, msgs=None):
+        if msgs is None:
+            msgs = self.messages(addr)
         dims = dt = layout = None
         filters = []
         kind = None
@@ -689,7 +731,7 @@ class _Reader:
         attrs = self._attributes(msgs)
         if dims is None:
             return np.zeros(0, dtype=dt), attrs, kind
-        n = int(np.prod(dims)) if dims else 1
+        n = math.prod(dims) if dims else 1
         raw = self._read_layout(layout, dims, dt, filters)
         arr = np.frombuffer(raw, dtype=dt, count=n).reshape(dims if dims else ())
         return arr, attrs, kind
@@ -720,7 +762,7 @@ class _Reader:
         if ver not in (3, 4):
             raise NotImplementedError(f"data layout version {ver}")
         cls = body[1]
-        nbytes = (int(np.prod(dims)) if dims else 1) * dt.itemsize
+        nbytes = (math.prod(dims) if dims else 1) * dt.itemsize
         if cls == 0:
             size = struct.unpack("<H", body[2:4])[0]
             return body[4:4 + size]
@@ -740,7 +782,7 @@ class _Reader:
             for offs, caddr, csize, fmask in self._walk_chunk_btree(btree, ndims):
                 raw = self.read(caddr, csize)
                 raw = self._unfilter(raw, filters, fmask, dt.itemsize)
-                block = np.frombuffer(raw, dtype=out.dtype, count=int(np.prod(chunk))).reshape(chunk)
+                block = np.frombuffer(raw, dtype=out.dtype, count=math.prod(chunk)).reshape(chunk)
                 sl = tuple(slice(o, min(o + c, d)) for o, c, d in zip(offs, chunk, dims))
                 out[sl] = block[tuple(slice(0, s.stop - s.start) for s in sl)]
             return out.tobytes()
@@ -781,16 +823,17 @@ class _Reader:
                 raise NotImplementedError(f"HDF5 filter {fid}")
         return raw
 
-    def is_group(self, addr: int) -> bool:
-        return any(t in (0x11, 0x06, 0x02) for t, _ in self.messages(addr))
+    def is_group(self, addr: int, msgs=None) -> bool:
+        return any(t in (0x11, 0x06, 0x02) for t, _ in (self.messages(addr) if msgs is None else msgs))
 
 
 def _decode(r: _Reader, addr: int):
     """An HDF5 object in MATLAB terms."""
-    if r.is_group(addr):
+    msgs = r.messages(addr)  # parsed once for both checks
+    if r.is_group(addr, msgs):
         # MATLAB struct: a group whose members are the fields
         return {name: _decode(r, a) for name, a in r.group_links(addr).items() if not name.startswith("#")}
-    arr, attrs, kind = r.dataset(addr)
+    arr, attrs, kind = r.dataset(addr, msgs)
     cls = attrs.get("MATLAB_class", None)
     if isinstance(cls, bytes):
         cls = cls.decode()
@@ -931,7 +974,7 @@ def update_variable(path: str, name: str, value) -> bool:
             return False
         addr, size = struct.unpack("<QQ", layout[2:18])
         val = np.asarray(value)
-        n = int(np.prod(dims)) if dims else 1
+        n = math.prod(dims) if dims else 1
         if addr == UNDEF or val.size != n or size != n * dt.itemsize:
             return False
         conv = val.astype(dt.newbyteorder("="))

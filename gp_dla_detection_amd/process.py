@@ -294,7 +294,7 @@ def run_process_qsos(base_directory: str, training_release: str, training_set_na
     v7.3 file, :222-249).
     Rank 0 returns the saved scalars; other ranks their local results."""
     import time
-    from .matv73 import LazyArray, loadmat, open_region
+    from .matv73 import LazyArray, loadmat, write_transposed
     from .shard import contiguous_shards, merge_shards
     compute = compute or _engine_compute
     tm = timings if timings is not None else {}
@@ -358,10 +358,9 @@ def run_process_qsos(base_directory: str, training_release: str, training_set_na
             del out["sample_log_likelihoods_dla"]
     if save:
         dist.broadcast_object_list(region, src=0)
-        view = open_region(path, region[0])
-        if mine.size:
-            view[mine[0]:mine[-1] + 1] = res["sample_log_likelihoods_dla"]      # this rank's rows
-        del view                                                     # (page cache; no msync, as matv73)
+        if mine.size:  # this rank's rows, straight into the file (page cache; no msync, as matv73)
+            write_transposed(path, region[0].offset, np.asarray(res["sample_log_likelihoods_dla"]),
+                             row0=int(mine[0]), rows_total=int(region[0].dims[1]))
         dist.barrier()
     tm["write_s"] = time.perf_counter() - t_comp
     return out if rank == 0 else res

@@ -76,6 +76,21 @@ def test_large_array_streams_in_blocks(tmp_path):
     assert np.array_equal(M.loadmat73(str(path))["big"], a)
 
 
+def test_deferred_region_written_in_row_blocks(tmp_path):
+    """process.run_process_qsos with world > 1: rank 0 lays out a deferred Q x S region, then every
+    rank pwrites its own spectra (rows) of it with write_transposed; uneven blocks, S not a multiple
+    of the band."""
+    rng = np.random.default_rng(5)
+    Q, S = 203, 77
+    full = rng.standard_normal((Q, S))
+    path = str(tmp_path / "d.mat")
+    reg = M.savemat73(path, dict(x=np.arange(3.0), sample_log_likelihoods_dla=M.LazyArray((Q, S), np.float64)))
+    reg = reg["sample_log_likelihoods_dla"]
+    for r0, r1 in ((0, 70), (70, 71), (71, Q)):
+        M.write_transposed(path, reg.offset, full[r0:r1], row0=r0, rows_total=Q, band=8, threads=3)
+    assert np.array_equal(M.loadmat73(path)["sample_log_likelihoods_dla"], full)
+
+
 @pytest.mark.parametrize("tag", ["earliest", "latest"])
 def test_reads_libhdf5_written_matlab_files(tag):
     """Files written by libhdf5 the way MATLAB -v7.3 does (chunked + deflate + shuffle, cells in

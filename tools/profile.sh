@@ -12,5 +12,5 @@ ARGS="--steps 3 --warmup 1 --cpu-budget 0 --no-alt $*"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o trace --output-format csv -- python3 bench.py $ARGS > "$OUT/bench_trace.json"
 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/fetch" -o fetch --output-format csv -- python3 bench.py $ARGS > "$OUT/bench_fetch.json"
 timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/write" -o write --output-format csv -- python3 bench.py $ARGS > "$OUT/bench_write.json"
-timeout -k 10 600 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES -d "$OUT/sq" -o sq --output-format csv -- python3 bench.py $ARGS > "$OUT/bench_sq.json"
+timeout -k 10 600 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE -d "$OUT/sq" -o sq --output-format csv -- python3 bench.py $ARGS > "$OUT/bench_sq.json"
 echo profile-done

@@ -19,6 +19,8 @@ def load_counters(path):
     agg = collections.defaultdict(list)
     for r in csv.DictReader(open(path)):
         agg[(r["Kernel_Name"], r["Counter_Name"])].append(float(r["Counter_Value"]))
+        if r["Counter_Name"] == "GRBM_GUI_ACTIVE":  # with the dispatch's own duration: the clock
+            agg[(r["Kernel_Name"], "_dispatch_ns")].append(float(r["End_Timestamp"]) - float(r["Start_Timestamp"]))
     return agg
 
 
@@ -46,10 +48,22 @@ def main(src: str, tag: str, dst: str = "profiles"):
             ent["write_size_kib"] = w_kib
             ent["hbm_bytes_per_launch"] = (2 * f_kib + w_kib) * 1024
             ent["hbm_gbs"] = ent["hbm_bytes_per_launch"] / (ent["avg_ms"] * 1e-3) / 1e9
-        for cn in ("SQ_INSTS_VALU", "SQ_INSTS_MFMA", "SQ_INSTS_LDS", "SQ_WAVES", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES"):
+        for cn in ("SQ_INSTS_VALU", "SQ_INSTS_MFMA", "SQ_INSTS_LDS", "SQ_WAVES", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES",
+                   "GRBM_GUI_ACTIVE"):
             k = (name, cn)
             if k in sq:
                 ent[cn] = sum(sq[k]) / len(sq[k])
+        # effective clock (MI355X_MICROARCH.md, DVFS give-back: GRBM_GUI_ACTIVE / 8 XCDs / dispatch time;
+        # reads high below ~0.3 ms) and, for f64-MFMA kernels, the share of the SIMDs' DP-pipe cycles
+        # their instructions need (v_mfma_f64_4x4x4_4b 16 cycles, other VALU 4; gfx950 counts MFMAs
+        # inside SQ_INSTS_VALU)
+        kd = (name, "_dispatch_ns")
+        if kd in sq and "GRBM_GUI_ACTIVE" in ent:
+            ns = sum(sq[kd]) / len(sq[kd])
+            ent["eff_clock_ghz"] = ent["GRBM_GUI_ACTIVE"] / 8 / ns
+            if "likelihood_kernel" in short and all(c in ent for c in ("SQ_INSTS_VALU", "SQ_INSTS_MFMA")):
+                need = 16 * ent["SQ_INSTS_MFMA"] + 4 * (ent["SQ_INSTS_VALU"] - ent["SQ_INSTS_MFMA"])
+                ent["dp_pipe_busy_frac"] = need / (1024 * ent["GRBM_GUI_ACTIVE"] / 8)
         out["kernels"].append(ent)
     # per batch (one gpdla_engine_process batch = one prep launch): the HBM bytes of every kernel
     # with counters, for the panel paths whose "launch" is a batch of many kernels
@@ -62,15 +76,21 @@ def main(src: str, tag: str, dst: str = "profiles"):
     (dst / f"{tag}_summary.json").write_text(json.dumps(out, indent=1))
     lines = [f"# rocprofv3 summary `{tag}`", "",
              f"bench under trace: {bench['value']:.4g} {bench['unit']}, {bench['ms_per_step']:.2f} ms/step", "",
-             "| kernel | calls | avg ms | % | HBM GB/launch (2*FETCH+WRITE) | HBM GB/s | VALU/wave | MFMA/wave | LDS/wave |",
-             "|---|---|---|---|---|---|---|---|---|"]
+             "| kernel | calls | avg ms | % | HBM GB/launch (2*FETCH+WRITE) | HBM GB/s | VALU/wave | MFMA/wave | LDS/wave | clock GHz |",
+             "|---|---|---|---|---|---|---|---|---|---|"]
     for e in out["kernels"]:
         w = e.get("SQ_WAVES") or 0
         per = lambda c: f"{e[c] / w:.0f}" if w and c in e else "-"
         gb = f"{e['hbm_bytes_per_launch'] / 1e9:.3f}" if "hbm_bytes_per_launch" in e else "-"
         gbs = f"{e['hbm_gbs']:.0f}" if "hbm_gbs" in e else "-"
         lines.append(f"| {e['kernel']} | {e['calls']} | {e['avg_ms']:.3f} | {e['pct']:.2f} | {gb} | {gbs} | "
-                     f"{per('SQ_INSTS_VALU')} | {per('SQ_INSTS_MFMA')} | {per('SQ_INSTS_LDS')} |")
+                     f"{per('SQ_INSTS_VALU')} | {per('SQ_INSTS_MFMA')} | {per('SQ_INSTS_LDS')} | "
+                     f"{e['eff_clock_ghz']:.2f} |" if "eff_clock_ghz" in e else
+                     f"| {e['kernel']} | {e['calls']} | {e['avg_ms']:.3f} | {e['pct']:.2f} | {gb} | {gbs} | "
+                     f"{per('SQ_INSTS_VALU')} | {per('SQ_INSTS_MFMA')} | {per('SQ_INSTS_LDS')} | - |")
+        if "dp_pipe_busy_frac" in e:
+            lines.append(f"|  ↳ DP pipe: its f64 MFMA + VALU issue needs {100 * e['dp_pipe_busy_frac']:.1f}% of the "
+                         f"SIMDs' cycles at the measured clock | | | | | | | | | |")
     if "per_batch" in out:
         pb = out["per_batch"]
         lines += ["", f"per batch ({pb['batches']} batches): {pb['hbm_bytes_per_batch'] / 1e9:.2f} GB of HBM traffic, "
