@@ -386,7 +386,12 @@ __global__ __launch_bounds__(256, (K <= 20 ? 2 : 1)) void likelihood_kernel(Like
               const double x = fma(lamc[tt], afac[j], -kC2);
               const double ax = fabs(x);
               double f = wing_eval(wing_lds + j * kWingStride, x);
-              if (ax < kCoreX) f = core_eval(core_lds + j * kCoreTable, ax);
+              // the core polynomial only where a lane of the wave is in this line's core (usually
+              // one line of the three): a wave-uniform branch, same values as the plain select
+              if (__builtin_amdgcn_ballot_w64(ax < kCoreX)) {
+                const double fc = core_eval(core_lds + j * kCoreTable, ax);
+                if (ax < kCoreX) f = fc;
+              }
               t -= f;
             }
             tot[tt] = t;
@@ -398,6 +403,10 @@ __global__ __launch_bounds__(256, (K <= 20 ? 2 : 1)) void likelihood_kernel(Like
         rwv[tt] = exp_tab64(N * tot[tt], exp_lds);
       }
     }
+    // the chunk's per-pixel weights first -- 4 independent 7-tap + weight chains the scheduler can
+    // interleave (one step at a time they were serial dependent chains of ~16 DP ops in front of each
+    // step's MFMAs) -- then the 4 steps' MFMAs
+    double wgs[kChunkSteps], wus[kChunkSteps];
 #pragma unroll
     for (int tt = 0; tt < kChunkSteps; ++tt) {
       const double* row = cur + (tt * 4 + g) * kRowS;
@@ -434,13 +443,17 @@ __global__ __launch_bounds__(256, (K <= 20 ? 2 : 1)) void likelihood_kernel(Like
       const double d = fma(om2, a2, noise);
       const double dinv = rcp_sweep(d);
       const double rd = r * dinv;
-      const double wg = a2 * dinv;
-      const double wu = ab * rd;
+      wgs[tt] = a2 * dinv;
+      wus[tt] = ab * rd;
       q1 = fma(r, rd, q1);
       pm *= d;
-      __builtin_amdgcn_sched_barrier(0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int tt = 0; tt < kChunkSteps; ++tt) {
+      const double wg = wgs[tt], wu = wus[tt];
       // B operands: tile t, entry 4t + (lane & 3) of this lane's segment row
-      const double* brow = row + (lane & 3) * kJS;
+      const double* brow = cur + (tt * 4 + g) * kRowS + (lane & 3) * kJS;
 #pragma unroll
       for (int tp = 0; tp < kTiles; tp += 2) {
         if (tp + 1 < kTiles) {
@@ -451,6 +464,7 @@ __global__ __launch_bounds__(256, (K <= 20 ? 2 : 1)) void likelihood_kernel(Like
           acc[tp] = __builtin_amdgcn_mfma_f64_4x4x4f64(tp < kGT ? wg : wu, brow[tp], acc[tp], 0, 0, 0);
         }
       }
+      __builtin_amdgcn_sched_barrier(0);
     }
     {  // keep the running product in range
       int ex;
