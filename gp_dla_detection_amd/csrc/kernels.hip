@@ -386,12 +386,7 @@ __global__ __launch_bounds__(256, (K <= 20 ? 2 : 1)) void likelihood_kernel(Like
               const double x = fma(lamc[tt], afac[j], -kC2);
               const double ax = fabs(x);
               double f = wing_eval(wing_lds + j * kWingStride, x);
-              // the core polynomial only where a lane of the wave is in this line's core (usually
-              // one line of the three): a wave-uniform branch, same values as the plain select
-              if (__builtin_amdgcn_ballot_w64(ax < kCoreX)) {
-                const double fc = core_eval(core_lds + j * kCoreTable, ax);
-                if (ax < kCoreX) f = fc;
-              }
+              if (ax < kCoreX) f = core_eval(core_lds + j * kCoreTable, ax);
               t -= f;
             }
             tot[tt] = t;
