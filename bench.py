@@ -221,6 +221,8 @@ def run_e2e(args, world: int, rank: int, local_rank: int, dist) -> None:
                                    f"fp64 -> processed_qsos v7.3 ({out_bytes / 1e9:.1f} GB)",
                        "spectra": Q, "num_samples": S, "parallelism": f"spectrum-shard x{world}"},
             "e2e": {"total_s": total, "load_s": load_s, "compute_s": compute_s, "write_s": write_s,
+                    "compute_split_rank0": {k: tm[k] for k in ("engine_create_s", "host_alloc_s", "engine_process_s")
+                                            if k in tm},
                     "setup_untimed_s": setup_s, "output_bytes": out_bytes, "output_dir": base,
                     "projection_8_ranks_s": {"load+compute scaled, write scaled": proj8 + write_s * world / 8,
                                              "load+compute scaled, write as measured": proj8 + write_s},

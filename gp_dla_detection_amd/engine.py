@@ -2,6 +2,7 @@
 from __future__ import annotations
 
 import ctypes as C
+import time
 
 import numpy as np
 
@@ -39,6 +40,24 @@ def _params_struct(p: Parameters, max_batch_spectra: int = 0, path: str = "auto"
                     max_batch_spectra=max_batch_spectra, path=_PATHS[path])
 
 
+def host_empty(shape: tuple, dtype=np.float64) -> np.ndarray:
+    """An uninitialised host array for outputs the engine writes in full: the 13 GB full-DR12Q Q x S
+    sample array is not NaN-filled first (a whole extra pass over it; the D2H copies touch each page
+    once).  From 256 MB up it is an anonymous map advised for transparent huge pages where the host
+    enables them (fewer first-touch faults)."""
+    import math
+    import mmap
+    nbytes = math.prod(shape) * np.dtype(dtype).itemsize
+    if nbytes < (1 << 28):
+        return np.empty(shape, dtype=dtype)
+    m = mmap.mmap(-1, nbytes, flags=mmap.MAP_PRIVATE | mmap.MAP_ANONYMOUS)
+    try:
+        m.madvise(mmap.MADV_HUGEPAGE)
+    except (AttributeError, OSError):  # no THP on this host: plain pages
+        pass
+    return np.frombuffer(m, dtype=dtype).reshape(shape)
+
+
 class Engine:
     """One engine per device: resident model, DLA samples and line-profile tables.
 
@@ -69,8 +88,11 @@ class Engine:
         self.device = device
 
     # -------------------------------------------------------------------------------- host path
-    def process(self, packed: dict, want_samples: bool = True, raise_numeric: bool = False) -> dict:
-        """Run the hot path on CSR-packed host spectra (see synthetic.pack_spectra)."""
+    def process(self, packed: dict, want_samples: bool = True, raise_numeric: bool = False,
+                timings: dict | None = None) -> dict:
+        """Run the hot path on CSR-packed host spectra (see synthetic.pack_spectra).  ``timings``
+        (optional) receives the host output allocation and the engine call times."""
+        t0 = time.perf_counter()
         offsets = np.ascontiguousarray(packed["offsets"], dtype=np.int64)
         Q = offsets.size - 1
         wl = np.ascontiguousarray(packed["wavelengths"], dtype=np.float64)
@@ -83,8 +105,8 @@ class Engine:
         out = dict(log_likelihoods_no_dla=np.full(Q, np.nan), log_likelihoods_dla=np.full(Q, np.nan),
                    min_z_dlas=np.full(Q, np.nan), max_z_dlas=np.full(Q, np.nan),
                    num_pixels=np.zeros(Q, dtype=np.int32))
-        if want_samples:
-            out["sample_log_likelihoods_dla"] = np.full((Q, self.num_samples), np.nan)
+        if want_samples:  # every row is written by the engine (NaN rows for unusable spectra)
+            out["sample_log_likelihoods_dla"] = host_empty((Q, self.num_samples))
         sp = L.Spectra(memory=L.MEM_HOST, num_spectra=Q, offsets=L.ptr(offsets, C.c_int64),
                        wavelengths=L.ptr(wl), flux=L.ptr(fl), noise_variance=L.ptr(nv),
                        pixel_mask=L.ptr(mk, C.c_uint8), z_qsos=L.ptr(zq))
@@ -94,7 +116,11 @@ class Engine:
                        log_likelihoods_dla=L.ptr(out["log_likelihoods_dla"]),
                        min_z_dlas=L.ptr(out["min_z_dlas"]), max_z_dlas=L.ptr(out["max_z_dlas"]),
                        num_pixels=L.ptr(out["num_pixels"], C.c_int32))
+        t1 = time.perf_counter()
         rc = self.lib.gpdla_engine_process(self._h, C.byref(sp), C.byref(rs))
+        if timings is not None:
+            timings["host_alloc_s"] = t1 - t0
+            timings["engine_process_s"] = time.perf_counter() - t1
         if rc == L.GPDLA_ENUMERIC and not raise_numeric:
             out["numeric_warning"] = self.lib.gpdla_last_error().decode()
         else:

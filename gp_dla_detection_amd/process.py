@@ -323,7 +323,15 @@ def run_process_qsos(base_directory: str, training_release: str, training_set_na
         pixel_mask=np.zeros(0, np.uint8), z_qsos=np.zeros(0))
     t_load = time.perf_counter()
     tm["load_s"] = t_load - t_start
-    res = compute(model, samples, packed, params, device)
+    if compute is _engine_compute:  # the compute phase split: engine creation, then the batches
+        eng = Engine(model, samples, params, device=device)
+        tm["engine_create_s"] = time.perf_counter() - t_load
+        try:
+            res = eng.process(packed, want_samples=True, timings=tm)
+        finally:
+            eng.close()
+    else:
+        res = compute(model, samples, packed, params, device)
     t_comp = time.perf_counter()
     tm["compute_s"] = t_comp - t_load
     meta = dict(training_release=training_release, training_set_name=training_set_name,
