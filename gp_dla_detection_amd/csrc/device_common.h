@@ -256,6 +256,28 @@ __device__ inline double raw_profile3(double lam, const double (&afac)[3], doubl
   return exp_tab64(N * total, exp_lds);
 }
 
+// raw_profile3 with the three damping-wing T_j = 1/x_j^2 from ONE v_rcp_f64 (wing_T3) instead of
+// three (+ their Newton steps); lanes with |x_j| < kCoreX take the core polynomial as before (their
+// T_j may be inf/NaN and are discarded by the select)
+__device__ inline double raw_profile3_t3(double lam, const double (&afac)[3], double N,
+                                         const double* __restrict__ core_lds,
+                                         const double* __restrict__ wing_lds,
+                                         const double* __restrict__ exp_lds) {
+  double x[3], T[3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) x[j] = fma(lam, afac[j], -kC2);
+  wing_T3(x[0], x[1], x[2], T[0], T[1], T[2]);
+  double total = 0.0;
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const double ax = fabs(x[j]);
+    double f = wing_poly(wing_lds + j * kWingStride, T[j]);
+    if (ax < kCoreX) f = core_eval(core_lds + j * kCoreTable, ax);
+    total -= f;
+  }
+  return exp_tab64(N * total, exp_lds);
+}
+
 // ---------------------------------------------------------------------------------------------
 // Per-sample augmented LDL^T in registers, one quad of lanes per sample.
 //   Lane jq of the quad owns Gram columns c = 4jj + jq (rows 0..4jj+3, A[jj][i]) and u rows

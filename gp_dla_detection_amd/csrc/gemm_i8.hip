@@ -138,7 +138,7 @@ __global__ __launch_bounds__(256) void weights_i8_kernel(WeightsI8Args a) {
   double afac[3];
 #pragma unroll
   for (int j = 0; j < 3; ++j) afac[j] = a.lines.buf[kLineBufFac + j] * zfac;
-  auto raw = [&](double lam) { return raw_profile3(lam, afac, N, core_lds, wing_lds, exp_lds); };
+  auto raw = [&](double lam) { return raw_profile3_t3(lam, afac, N, core_lds, wing_lds, exp_lds); };
   const double* lamp = a.lam_pad + (int64_t)g * L + t0;  // padded positions g L + t0 + 0..5
   double w0 = raw(lamp[0]), w1 = raw(lamp[1]), w2 = raw(lamp[2]);
   double w3 = raw(lamp[3]), w4 = raw(lamp[4]), w5 = raw(lamp[5]);

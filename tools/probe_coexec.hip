@@ -1,6 +1,7 @@
 // Probe: do fp64 MFMA and fp64 VALU from DIFFERENT waves on one SIMD overlap?
 // 512-thread blocks (8 waves, 2 per SIMD): waves 0-3 run role R0, waves 4-7 role R1.
-// role 0 = idle, 1 = MFMA f64 4x4x4 chain x8, 2 = VALU f64 FMA chains x8.
+// role 0 = idle, 1 = MFMA f64 4x4x4 chain x8, 2 = VALU f64 FMA chains x8, 3 = VALU int32 chains x8
+// (16 v_xad/v_add-class ops per iteration), 4 = VALU f32 FMA chains x8 (16 per iteration).
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <vector>
@@ -22,6 +23,23 @@ __global__ __launch_bounds__(512) void probe(double* out, int iters, int r0, int
 #pragma unroll
       for (int i = 0; i < 8; ++i) { acc[i] = fma(acc[i], a, b); acc[i] = fma(acc[i], b, a); }
     }
+  } else if (role == 3) {
+    unsigned u[8];
+    for (int i = 0; i < 8; ++i) u[i] = threadIdx.x * 7u + i;
+    for (int it = 0; it < iters; ++it) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) { u[i] = (u[i] ^ 0x9e3779b9u) + (unsigned)it; u[i] = (u[i] << 3) ^ (u[i] >> 5); }
+    }
+    for (int i = 0; i < 8; ++i) acc[i] += (double)u[i];
+  } else if (role == 4) {
+    float f[8];
+    const float fa = 1.0f + threadIdx.x * 1e-7f, fb = 1.0f - threadIdx.x * 1e-7f;
+    for (int i = 0; i < 8; ++i) f[i] = i * 1e-3f;
+    for (int it = 0; it < iters; ++it) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) { f[i] = fmaf(f[i], fa, fb); f[i] = fmaf(f[i], fb, fa); }
+    }
+    for (int i = 0; i < 8; ++i) acc[i] += f[i];
   }
   unsigned long long t1 = __builtin_amdgcn_s_memtime();
   double s = 0;
@@ -37,7 +55,8 @@ int main() {
   const int iters = 4000;
   struct C { int r0, r1; const char* name; } cs[] = {
       {1, 0, "MFMA x1 wave/SIMD"}, {1, 1, "MFMA x2 waves/SIMD"}, {2, 0, "VALU x1 wave/SIMD"},
-      {2, 2, "VALU x2 waves/SIMD"}, {1, 2, "MFMA wave + VALU wave"}};
+      {2, 2, "VALU x2 waves/SIMD"}, {1, 2, "MFMA wave + VALU wave"}, {3, 0, "INT x1 wave/SIMD"},
+      {1, 3, "MFMA wave + INT wave"}, {4, 0, "F32 x1 wave/SIMD"}, {1, 4, "MFMA wave + F32 wave"}};
   for (auto& c : cs) {
     hipLaunchKernelGGL(probe, dim3(blocks), dim3(512), 0, 0, out, iters, c.r0, c.r1, cyc);
     hipDeviceSynchronize();
