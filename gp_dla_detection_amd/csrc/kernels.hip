@@ -24,6 +24,12 @@ __global__ __launch_bounds__(256) void prep_kernel(PrepArgs a) {
   using Lay = Layout<K>;
   __shared__ int s_i4[4];
   __shared__ double s_d4[4];
+  // pass 3 scratch: each wave's interpolated M row of its current slot, and the Gram pair (r, c) of
+  // every Khatri-Rao entry (fused layout)
+  constexpr int kMaxKK = K > 0 ? K : kGemmMaxK;
+  constexpr int kNPairs = K > 0 ? Lay::kNGram : 1;
+  __shared__ double s_M[4][kMaxKK];
+  __shared__ uint16_t s_rc[kNPairs];
   const int q = blockIdx.x;
   const int tid = threadIdx.x;
   const int64_t pb = a.offsets[q];
@@ -121,6 +127,27 @@ __global__ __launch_bounds__(256) void prep_kernel(PrepArgs a) {
   const int lane = tid & 63, wave = tid >> 6;
   const double* rest_g = a.rest;
   const int G = a.num_rest;
+  if constexpr (K > 0) {
+    for (int e = tid; e < Lay::kNGram; e += 256) {
+      int r, c;
+      gram_pair<K>(e, r, c);
+      s_rc[e] = (uint16_t)(r | (c << 8));
+    }
+    __syncthreads();
+  }
+  // interpolation index (interp_index: the largest gi in [0, G - 2] with rest_g[gi] <= x, else 0) by
+  // two rounds of a 64-way search over the lanes -- two dependent loads instead of log2 G
+  const int s1 = (G - 1 + 63) / 64;
+  auto search = [&](double x) {
+    if (s1 > 64) return interp_index(rest_g, G, x);  // grids over 4,097 points: binary search
+    const int i1 = lane * s1;
+    const bool p1 = i1 < G - 1 && rest_g[i1] <= x;
+    int lo = max(0, (int)__builtin_popcountll(__ballot(p1)) - 1) * s1;
+    const int i2 = lo + lane;
+    const bool p2 = lane < s1 && i2 < G - 1 && rest_g[i2] <= x;
+    const int c2 = (int)__builtin_popcountll(__ballot(p2));
+    return c2 > 0 ? lo + c2 - 1 : lo;
+  };
   // Slot j holds segment gg = j / Ls, step t = j % Ls, i.e. pixel-order position gg L + t; the
   // steps t >= L that round each segment up to whole chunks are neutral rows (like masked pixels).
   const int Ls = L > 0 ? ((L + kChunkSteps - 1) / kChunkSteps) * kChunkSteps : kChunkSteps;
@@ -131,19 +158,27 @@ __global__ __launch_bounds__(256) void prep_kernel(PrepArgs a) {
     const double lam_lead = lam_pad[(pos >= 0 ? pos : j) + 2 * kWidth];  // any finite value if neutral
     const int KK = K > 0 ? K : a.k;  // K == 0: panel-GEMM layout at runtime rank a.k
     double sc[6] = {lam_lead, 0.0, 1.0, 0.0, 0.0, 0.0};  // lam, y, noise, mu, om2, valid (neutral)
-    const double* M0 = nullptr;
-    const double* M1 = nullptr;
-    double rest = 0.0, x0 = 0.0, x1 = 1.0;
-    bool at_end = false;
+    double* sM = s_M[wave];
     if (pix >= 0) {
       const double lam = wl[pix];
-      rest = lam / (1 + z);
-      const int gi = interp_index(rest_g, G, rest);
-      at_end = rest >= rest_g[G - 1];
-      M0 = a.M_rowmajor + (int64_t)gi * KK;
-      M1 = a.M_rowmajor + (int64_t)(at_end ? gi : gi + 1) * KK;
-      x0 = rest_g[gi];
-      x1 = rest_g[at_end ? gi : gi + 1];
+      const double rest = lam / (1 + z);
+      const int gi = search(rest);
+      const bool at_end = rest >= rest_g[G - 1];
+      const double* M0 = a.M_rowmajor + (int64_t)gi * KK;
+      const double* M1 = a.M_rowmajor + (int64_t)(at_end ? gi : gi + 1) * KK;
+      const double x0 = rest_g[gi], x1 = rest_g[at_end ? gi : gi + 1];
+      // M row at this pixel, process_qsos.m:140 (griddedInterpolant 'linear', per column), once per
+      // column into this wave's LDS row
+      for (int col = lane; col < KK; col += 64) {
+        double v;
+        if (at_end) {
+          v = a.M_rowmajor[(int64_t)(G - 1) * KK + col];
+        } else {
+          const double slope = (M1[col] - M0[col]) / (x1 - x0);
+          v = slope * (rest - x0) + M0[col];
+        }
+        sM[col] = v;
+      }
       if (lane == 0) {
         const double mu = interp_eval(rest_g, a.mu, G, gi, rest);             // :139
         const double lom = interp_eval(rest_g, a.log_omega, G, gi, rest);     // :142
@@ -158,21 +193,18 @@ __global__ __launch_bounds__(256) void prep_kernel(PrepArgs a) {
         sc[5] = 1.0;
       }
     }
-    // M row at this pixel, process_qsos.m:140 (griddedInterpolant 'linear', per column)
-    auto Mi = [&](int col) {
-      if (at_end) return a.M_rowmajor[(int64_t)(G - 1) * KK + col];
-      const double slope = (M1[col] - M0[col]) / (x1 - x0);
-      return slope * (rest - x0) + M0[col];
-    };
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the wave's LDS row before its reads
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    auto Mi = [&](int col) { return sM[col]; };
     if constexpr (K > 0) {
       double* row = a.panel + (sb + j) * Lay::kRow;
       for (int e = lane; e < 4 * Lay::kTiles; e += 64) {
         double v = 0.0;
         if (pix >= 0) {
           if (e < Lay::kNGram) {
-            int r, c;
-            gram_pair<K>(e, r, c);
-            v = Mi(r) * Mi(c);
+            const int rc = s_rc[e];
+            v = Mi(rc & 255) * Mi(rc >> 8);
           } else if (e >= 4 * Lay::kGT && e - 4 * Lay::kGT < K) {
             v = Mi(e - 4 * Lay::kGT);
           }
@@ -213,6 +245,9 @@ __global__ __launch_bounds__(256) void prep_kernel(PrepArgs a) {
         sr[7] = (sc[4] + sc[2]) * kI8ScaleG;
       }
     }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // reads of this slot's row done before
+    __builtin_amdgcn_wave_barrier();                         // the next slot overwrites it
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
 }
 
@@ -641,8 +676,12 @@ __global__ __launch_bounds__(256) void mvn_single_kernel(const double* __restric
 template <int K>
 hipError_t launch_prep_k(const PrepArgs& a, hipStream_t s) {
   // the panel-GEMM layout (K == 0) writes k(k+1)/2 doubles per slot for few spectra per batch:
-  // spread each spectrum's slots over 16 blocks
-  hipLaunchKernelGGL(prep_kernel<K>, dim3(a.q_count, K == 0 ? 16 : 1), dim3(256), 0, s, a);
+  // spread each spectrum's slots over 16 blocks; the fused layout over GPDLA_PREP_Y (each wave's
+  // slots are a chain of dependent loads -- pixel map, wavelength, grid search, M rows)
+#ifndef GPDLA_PREP_Y
+#define GPDLA_PREP_Y 1
+#endif
+  hipLaunchKernelGGL(prep_kernel<K>, dim3(a.q_count, K == 0 ? 16 : GPDLA_PREP_Y), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 
