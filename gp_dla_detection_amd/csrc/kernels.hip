@@ -676,12 +676,9 @@ __global__ __launch_bounds__(256) void mvn_single_kernel(const double* __restric
 template <int K>
 hipError_t launch_prep_k(const PrepArgs& a, hipStream_t s) {
   // the panel-GEMM layout (K == 0) writes k(k+1)/2 doubles per slot for few spectra per batch:
-  // spread each spectrum's slots over 16 blocks; the fused layout over GPDLA_PREP_Y (each wave's
-  // slots are a chain of dependent loads -- pixel map, wavelength, grid search, M rows)
-#ifndef GPDLA_PREP_Y
-#define GPDLA_PREP_Y 1
-#endif
-  hipLaunchKernelGGL(prep_kernel<K>, dim3(a.q_count, K == 0 ? 16 : GPDLA_PREP_Y), dim3(256), 0, s, a);
+  // spread each spectrum's slots over 16 blocks (the fused layout: one block per spectrum; 4 or 8
+  // gained < 7% of prep's 1.08 ms, profiles/r2w)
+  hipLaunchKernelGGL(prep_kernel<K>, dim3(a.q_count, K == 0 ? 16 : 1), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 

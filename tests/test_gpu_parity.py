@@ -162,6 +162,33 @@ def test_other_ranks(k):
         assert _rel_err(out["log_likelihoods_no_dla"][q], ref["log_likelihood_no_dla"]) < 1e-9
 
 
+@pytest.mark.parametrize("G", [300, 1217, 5000])
+@pytest.mark.parametrize("path", ["auto", "panel_gemm"])
+def test_nonuniform_rest_grids(G, path):
+    """prep_kernel's interpolation index (a two-round 64-way lane search for grids up to 4,097
+    points, the binary search above) on jittered, non-uniform rest grids of 300, 1,217 and 5,000
+    points, against the oracle's np.interp (process_qsos.m:66-71,139-142)."""
+    from oracle import gpdla_oracle as O
+    rng = np.random.default_rng(G)
+    base = syn.make_model(k=20, seed=G)
+    lo, hi = base["rest_wavelengths"][0], base["rest_wavelengths"][-1]
+    grid = np.concatenate(([lo], np.sort(rng.uniform(lo, hi, G - 2)), [hi]))
+    model = dict(base, rest_wavelengths=grid,
+                 mu=np.interp(grid, base["rest_wavelengths"], base["mu"]),
+                 M=np.asfortranarray(np.stack([np.interp(grid, base["rest_wavelengths"], base["M"][:, j])
+                                               for j in range(20)], axis=1)),
+                 log_omega=np.interp(grid, base["rest_wavelengths"], base["log_omega"]))
+    samples = syn.make_samples(40)
+    spectra = syn.make_dr12q_like_spectra(model, 2, seed=G, mask_fraction=0.05)
+    with Engine(model, samples, set_parameters(k=20), path=path) as eng:
+        out = eng.process(syn.pack_spectra(spectra))
+    for q, s in enumerate(spectra):
+        ref = O.process_spectrum(s["wavelengths"], s["flux"], s["noise_variance"], s["pixel_mask"],
+                                 s["z_qso"], model, samples["offset_samples"], samples["nhi_samples"])
+        assert _rel_err(out["sample_log_likelihoods_dla"][q], ref["sample_log_likelihoods_dla"]) < 1e-9
+        assert _rel_err(out["log_likelihoods_no_dla"][q], ref["log_likelihood_no_dla"]) < 1e-9
+
+
 @pytest.mark.parametrize("k", [1, 3, 7, 9, 13, 17, 23])
 def test_ranks_between_compiled_ones_run_fused_zero_padded(k):
     """A rank the fused kernel is not compiled for runs on the next compiled rank with M padded by
