@@ -151,13 +151,65 @@ __global__ __launch_bounds__(256) void prep_kernel(PrepArgs a) {
   // Slot j holds segment gg = j / Ls, step t = j % Ls, i.e. pixel-order position gg L + t; the
   // steps t >= L that round each segment up to whole chunks are neutral rows (like masked pixels).
   const int Ls = L > 0 ? ((L + kChunkSteps - 1) / kChunkSteps) * kChunkSteps : kChunkSteps;
-  for (int64_t j = wave + 4 * (int64_t)blockIdx.y; j < cap; j += 4 * (int64_t)gridDim.y) {
+  auto slot_pixel = [&](int64_t j, int& pos) {
     const int gg = (int)(j / Ls), t = (int)(j - (int64_t)gg * Ls);
-    const int pos = (gg < 4 && t < L) ? gg * L + t : -1;
-    const int pix = (pos >= 0 && pos < J) ? smap[pos] : -1;
-    const double lam_lead = lam_pad[(pos >= 0 ? pos : j) + 2 * kWidth];  // any finite value if neutral
-    const int KK = K > 0 ? K : a.k;  // K == 0: panel-GEMM layout at runtime rank a.k
-    double sc[6] = {lam_lead, 0.0, 1.0, 0.0, 0.0, 0.0};  // lam, y, noise, mu, om2, valid (neutral)
+    pos = (gg < 4 && t < L) ? gg * L + t : -1;
+    return (pos >= 0 && pos < J) ? smap[pos] : -1;
+  };
+  const int KK = K > 0 ? K : a.k;  // K == 0: panel-GEMM layout at runtime rank a.k
+
+  // pass 3a: slot scalars, one thread per slot (the interpolation of mu, log omega and the pow / exp
+  // of process_qsos.m:139-147 at full SIMD width; they were one lane's work per slot-wave)
+  for (int64_t j = tid + 256 * (int64_t)blockIdx.y; j < cap; j += 256 * (int64_t)gridDim.y) {
+    int pos;
+    const int pix = slot_pixel(j, pos);
+    double sc[6] = {lam_pad[(pos >= 0 ? pos : j) + 2 * kWidth],  // lam (any finite value if neutral),
+                    0.0, 1.0, 0.0, 0.0, 0.0};                     // y, noise, mu, om2, valid (neutral)
+    if (pix >= 0) {
+      const double lam = wl[pix];
+      const double rest = lam / (1 + z);
+      const int gi = interp_index(rest_g, G, rest);
+      const double mu = interp_eval(rest_g, a.mu, G, gi, rest);             // :139
+      const double lom = interp_eval(rest_g, a.log_omega, G, gi, rest);     // :142
+      const double lya_z = (lam - a.lya) / a.lya;                           // :118-120
+      double om2 = exp(2 * lom);                                            // :143
+      const double sf = 1 - exp(-a.tau_0 * pow(1 + lya_z, a.beta)) + a.c_0;  // :145
+      om2 = om2 * (sf * sf);                                                // :147
+      sc[1] = a.flux[pb + pix];
+      sc[2] = a.noise[pb + pix];
+      sc[3] = mu;
+      sc[4] = om2;
+      sc[5] = 1.0;
+    }
+    if constexpr (K > 0) {
+      double* row = a.panel + (sb + j) * Lay::kRow;
+      row[Lay::kLam] = sc[0];
+      row[Lay::kY] = sc[1];
+      row[Lay::kNoise] = sc[2];
+      row[Lay::kMu] = sc[3];
+      row[Lay::kOmega2] = sc[4];
+      row[Lay::kValid] = sc[5];
+      // the remaining spare words
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+        for (int t2 = Lay::kTiles; t2 < Lay::kJS; ++t2)
+          if (!(jj < 3 && t2 < Lay::kTiles + 2)) row[jj * Lay::kJS + t2] = 0.0;
+    } else {
+      double* sr = a.srow + (sb + j) * 8;
+#pragma unroll
+      for (int w = 0; w < 6; ++w) sr[w] = sc[w];
+      // the int8 path's per-slot quantisation scales (gemm_i8.hip weights_i8_kernel), hoisted out
+      // of the per-sample loop: u~ scale 2^31 / beta and Gram scale (omega^2 + sigma^2) 2^32
+      sr[6] = kI8ScaleU / u_bound(sc[1], sc[3], sc[2]);
+      sr[7] = (sc[4] + sc[2]) * kI8ScaleG;
+    }
+  }
+
+  // pass 3b: Khatri-Rao rows, one wave per slot
+  for (int64_t j = wave + 4 * (int64_t)blockIdx.y; j < cap; j += 4 * (int64_t)gridDim.y) {
+    int pos;
+    const int pix = slot_pixel(j, pos);
     double* sM = s_M[wave];
     if (pix >= 0) {
       const double lam = wl[pix];
@@ -179,19 +231,6 @@ __global__ __launch_bounds__(256) void prep_kernel(PrepArgs a) {
         }
         sM[col] = v;
       }
-      if (lane == 0) {
-        const double mu = interp_eval(rest_g, a.mu, G, gi, rest);             // :139
-        const double lom = interp_eval(rest_g, a.log_omega, G, gi, rest);     // :142
-        const double lya_z = (lam - a.lya) / a.lya;                           // :118-120
-        double om2 = exp(2 * lom);                                            // :143
-        const double sf = 1 - exp(-a.tau_0 * pow(1 + lya_z, a.beta)) + a.c_0;  // :145
-        om2 = om2 * (sf * sf);                                                // :147
-        sc[1] = a.flux[pb + pix];
-        sc[2] = a.noise[pb + pix];
-        sc[3] = mu;
-        sc[4] = om2;
-        sc[5] = 1.0;
-      }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the wave's LDS row before its reads
     __builtin_amdgcn_wave_barrier();
@@ -211,22 +250,9 @@ __global__ __launch_bounds__(256) void prep_kernel(PrepArgs a) {
         }
         row[(e & 3) * Lay::kJS + (e >> 2)] = v;
       }
-      if (lane == 0) {
-        row[Lay::kLam] = sc[0];
-        row[Lay::kY] = sc[1];
-        row[Lay::kNoise] = sc[2];
-        row[Lay::kMu] = sc[3];
-        row[Lay::kOmega2] = sc[4];
-        row[Lay::kValid] = sc[5];
-      }
-      // zero the remaining spare words
-      for (int w = lane; w < Lay::kRow; w += 64) {
-        const int jj = w / Lay::kJS, t2 = w % Lay::kJS;
-        if (t2 >= Lay::kTiles && !((jj == 0 || jj == 1 || jj == 2) && t2 < Lay::kTiles + 2)) row[w] = 0.0;
-      }
     } else {
-      // panel-GEMM layout: Khatri-Rao row (entry (r, c) at gram_tile_index(r, c), internal.h), M
-      // row, and 8 slot scalars; all zero / neutral for masked and padding slots
+      // panel-GEMM layout: Khatri-Rao row (entry (r, c) at gram_tile_index(r, c), internal.h) and M
+      // row (the 8 slot scalars come from pass 3a); all zero for masked and padding slots
       const int64_t E = (int64_t)KK * (KK + 1) / 2;
       double* pg = a.panel + (sb + j) * E;
       double* pm = a.panel_m + (sb + j) * KK;
@@ -235,15 +261,6 @@ __global__ __launch_bounds__(256) void prep_kernel(PrepArgs a) {
         for (int c = r + lane; c < KK; c += 64) pg[gram_tile_index(r, c, KK)] = pix >= 0 ? mr * Mi(c) : 0.0;
       }
       for (int c = lane; c < KK; c += 64) pm[c] = pix >= 0 ? Mi(c) : 0.0;
-      if (lane == 0) {
-        double* sr = a.srow + (sb + j) * 8;
-#pragma unroll
-        for (int w = 0; w < 6; ++w) sr[w] = sc[w];
-        // the int8 path's per-slot quantisation scales (gemm_i8.hip weights_i8_kernel), hoisted out
-        // of the per-sample loop: u~ scale 2^31 / beta and Gram scale (omega^2 + sigma^2) 2^32
-        sr[6] = kI8ScaleU / u_bound(sc[1], sc[3], sc[2]);
-        sr[7] = (sc[4] + sc[2]) * kI8ScaleG;
-      }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // reads of this slot's row done before
     __builtin_amdgcn_wave_barrier();                         // the next slot overwrites it
