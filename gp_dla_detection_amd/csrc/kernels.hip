@@ -27,7 +27,7 @@ __global__ __launch_bounds__(256) void prep_kernel(PrepArgs a) {
   // pass 3 scratch: each wave's interpolated M row of its current slot, and the Gram pair (r, c) of
   // every Khatri-Rao entry (fused layout)
   constexpr int kMaxKK = K > 0 ? K : kGemmMaxK;
-  constexpr int kNPairs = K > 0 ? Lay::kNGram : 1;
+  constexpr int kNPairs = K > 0 ? Lay::kNGram : kGemmMaxK * (kGemmMaxK + 1) / 2;
   __shared__ double s_M[4][kMaxKK];
   __shared__ uint16_t s_rc[kNPairs];
   const int q = blockIdx.x;
@@ -127,14 +127,19 @@ __global__ __launch_bounds__(256) void prep_kernel(PrepArgs a) {
   const int lane = tid & 63, wave = tid >> 6;
   const double* rest_g = a.rest;
   const int G = a.num_rest;
+  // entry -> (r, c): fused layout e = row-major upper-triangle pair; panel-GEMM layout e =
+  // gram_tile_index(r, c, k) (internal.h)
   if constexpr (K > 0) {
     for (int e = tid; e < Lay::kNGram; e += 256) {
       int r, c;
       gram_pair<K>(e, r, c);
       s_rc[e] = (uint16_t)(r | (c << 8));
     }
-    __syncthreads();
+  } else {
+    for (int r = 0; r < a.k; ++r)
+      for (int c = r + tid; c < a.k; c += 256) s_rc[gram_tile_index(r, c, a.k)] = (uint16_t)(r | (c << 8));
   }
+  __syncthreads();
   // interpolation index (interp_index: the largest gi in [0, G - 2] with rest_g[gi] <= x, else 0) by
   // two rounds of a 64-way search over the lanes -- two dependent loads instead of log2 G
   const int s1 = (G - 1 + 63) / 64;
@@ -256,9 +261,9 @@ __global__ __launch_bounds__(256) void prep_kernel(PrepArgs a) {
       const int64_t E = (int64_t)KK * (KK + 1) / 2;
       double* pg = a.panel + (sb + j) * E;
       double* pm = a.panel_m + (sb + j) * KK;
-      for (int r = 0; r < KK; ++r) {
-        const double mr = pix >= 0 ? Mi(r) : 0.0;
-        for (int c = r + lane; c < KK; c += 64) pg[gram_tile_index(r, c, KK)] = pix >= 0 ? mr * Mi(c) : 0.0;
+      for (int64_t e = lane; e < E; e += 64) {
+        const int rc = s_rc[e];
+        pg[e] = pix >= 0 ? Mi(rc & 255) * Mi(rc >> 8) : 0.0;
       }
       for (int c = lane; c < KK; c += 64) pm[c] = pix >= 0 ? Mi(c) : 0.0;
     }
