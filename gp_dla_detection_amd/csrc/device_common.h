@@ -257,8 +257,9 @@ __device__ inline double raw_profile3(double lam, const double (&afac)[3], doubl
 }
 
 // raw_profile3 with the three damping-wing T_j = 1/x_j^2 from ONE v_rcp_f64 (wing_T3) instead of
-// three (+ their Newton steps); lanes with |x_j| < kCoreX take the core polynomial as before (their
-// T_j may be inf/NaN and are discarded by the select)
+// three (+ their Newton steps) and the outer wing polynomial; lanes with |x_j| < kOuterX take the
+// inner wing, lanes with |x_j| < kCoreX the core polynomial (their T_j may be inf/NaN and are
+// discarded by the select)
 __device__ inline double raw_profile3_t3(double lam, const double (&afac)[3], double N,
                                          const double* __restrict__ core_lds,
                                          const double* __restrict__ wing_lds,
@@ -271,8 +272,11 @@ __device__ inline double raw_profile3_t3(double lam, const double (&afac)[3], do
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
     const double ax = fabs(x[j]);
-    double f = wing_poly(wing_lds + j * kWingStride, T[j]);
-    if (ax < kCoreX) f = core_eval(core_lds + j * kCoreTable, ax);
+    double f = outer_poly(wing_lds + j * kWingStride, T[j]);
+    if (ax < kOuterX) {
+      f = wing_poly(wing_lds + j * kWingStride, T[j]);
+      if (ax < kCoreX) f = core_eval(core_lds + j * kCoreTable, ax);
+    }
     total -= f;
   }
   return exp_tab64(N * total, exp_lds);

@@ -13,6 +13,7 @@
 //     truncated at its smallest term (relative error < exp(-x^2) ~ 1e-62 at x = 12).
 // Only Im z >= 0 with small Im z is needed (Lyman-series y_j <= 4.8e-4); the standalone API
 // documents |y| <= 1.
+#include <algorithm>
 #include <cmath>
 #include <complex>
 #include <mutex>
@@ -157,38 +158,33 @@ void line_scale(int j, long double* scale, long double* y) {
   *scale = (long double)kLeadingConstants[j] / (sig * std::sqrt(2.0L * kPiL));
 }
 
-}  // namespace
-
-// Wing polynomial of line j: f_j(x) x^2 = sum_n wing[n] T^n on T = 1/x^2 in (0, 1/kCoreX^2]
-// (Chebyshev interpolation at kWingDeg + 1 first-kind nodes, then monomials in T).
-void fit_wing_line(int j, double* wing) {
+// f_j(x) x^2 = sum_n c[n] T^n on T = 1/x^2 in (0, 1/xmin^2] at degree deg (Chebyshev
+// interpolation at deg + 1 first-kind nodes, then monomials in T), zero-padded to len.
+void fit_T_poly(int j, long double xmin, int deg, int len, double* c) {
   long double scale, y;
   line_scale(j, &scale, &y);
-  const long double Tmax = 1.0L / ((long double)kCoreX * kCoreX);
-  const int N = kWingDeg + 1;
+  const long double Tmax = 1.0L / (xmin * xmin);
+  const int N = deg + 1;
   std::vector<long double> fv(N);
   for (int k = 0; k < N; ++k) {
     const long double T = Tmax * (std::cos(kPiL * (k + 0.5L) / N) + 1.0L) / 2.0L;
     fv[k] = scale * faddeeva_w(1.0L / std::sqrt(T), y).real() / T;
   }
   const std::vector<long double> t = shift_to_T(cheb_fit_monomial(fv), 2.0L / Tmax, -1.0L);
-  for (int n = 0; n < kWingStride; ++n) wing[n] = n < N ? (double)t[n] : 0.0;
+  for (int n = 0; n < len; ++n) c[n] = n < N ? (double)t[n] : 0.0;
+}
+
+}  // namespace
+
+// Wing block of line j (kWingStride doubles): the wing polynomial for |x| >= kCoreX at 0, the
+// outer polynomial for |x| >= kOuterX at kOuterOff.
+void fit_wing_line(int j, double* wing) {
+  fit_T_poly(j, (long double)kCoreX, kWingDeg, kOuterOff, wing);
+  fit_T_poly(j, (long double)kOuterX, kOuterDeg, kWingStride - kOuterOff, wing + kOuterOff);
 }
 
 // Far-wing polynomial of line j on T in (0, kFarT] (|x| >= kFarX), degree kFarDeg.
-void fit_far_line(int j, double* far) {
-  long double scale, y;
-  line_scale(j, &scale, &y);
-  const long double Tmax = 1.0L / ((long double)kFarX * kFarX);
-  const int N = kFarDeg + 1;
-  std::vector<long double> fv(N);
-  for (int k = 0; k < N; ++k) {
-    const long double T = Tmax * (std::cos(kPiL * (k + 0.5L) / N) + 1.0L) / 2.0L;
-    fv[k] = scale * faddeeva_w(1.0L / std::sqrt(T), y).real() / T;
-  }
-  const std::vector<long double> t = shift_to_T(cheb_fit_monomial(fv), 2.0L / Tmax, -1.0L);
-  for (int n = 0; n < kFarStride; ++n) far[n] = n < N ? (double)t[n] : 0.0;
-}
+void fit_far_line(int j, double* far) { fit_T_poly(j, (long double)kFarX, kFarDeg, kFarStride, far); }
 
 // Max relative error of the far-wing polynomial (|x| from kFarX geometrically out to 2e6).
 double far_profile_error(int j) {
@@ -240,7 +236,9 @@ double line_profile_error(int j) {
     const double x = (i < 36000) ? i * (kCoreX / 36000.0) : kCoreX * std::pow(1.0004, i - 36000);
     const double got = line_profile_eval(core.data(), wing.data(), x);
     const long double ref = scale * faddeeva_w((long double)x, y).real();
-    const double rel = (double)std::fabs((got - ref) / ref);
+    double rel = (double)std::fabs((got - ref) / ref);
+    if (x >= kOuterX)  // the batched sweeps' outer polynomial
+      rel = std::max(rel, (double)std::fabs((outer_poly(wing.data(), 1.0 / (x * x)) - ref) / ref));
     if (rel > maxrel) maxrel = rel;
   }
   return maxrel;

@@ -401,9 +401,9 @@ __global__ __launch_bounds__(256, (K <= 20 ? 2 : 1)) void likelihood_kernel(Like
     double* cur = lds + (c & 1) * kBuf;
     if (c + 1 < nchunks)
       stage_chunk<K>(panel, Ls, c + 1, lds_base + (uint32_t)(((c + 1) & 1) * kBuf * 8), wave_s, voff);
-    // raw profiles of the chunk's 4 steps first: branch-free damping wings (one basic block, so
-    // the 4 chains interleave), a rare core fix-up for lanes with |x| < kCoreX (raw_profile3's
-    // order: bit-identical), then the 4 table exps
+    // raw profiles of the chunk's 4 steps first: branch-free outer damping wings (one basic block,
+    // so the 4 chains interleave), a rare fix-up for lanes with |x| < kOuterX (core or inner wing,
+    // raw_profile3's evaluation), then the 4 table exps
     double rwv[kChunkSteps];
     if constexpr (NL == 3) {
       double tot[kChunkSteps], lamc[kChunkSteps];
@@ -418,7 +418,7 @@ __global__ __launch_bounds__(256, (K <= 20 ? 2 : 1)) void likelihood_kernel(Like
       for (int tt = 0; tt < kChunkSteps; ++tt) {
         const double x0 = fma(lamc[tt], afac[0], -kC2), x1 = fma(lamc[tt], afac[1], -kC2),
                      x2 = fma(lamc[tt], afac[2], -kC2);
-        cm |= (((fabs(x0) < kCoreX) | (fabs(x1) < kCoreX) | (fabs(x2) < kCoreX)) ? 1u : 0u) << tt;
+        cm |= (((fabs(x0) < kOuterX) | (fabs(x1) < kOuterX) | (fabs(x2) < kOuterX)) ? 1u : 0u) << tt;
         wing_T3(x0, x1, x2, Tj[0][tt], Tj[1][tt], Tj[2][tt]);
       }
       // line-outer order (same per-step summation order): one line's 9 coefficients live at a
@@ -430,7 +430,7 @@ __global__ __launch_bounds__(256, (K <= 20 ? 2 : 1)) void likelihood_kernel(Like
         const double* wl = wing_lds + zoff + j * kWingStride;
 #pragma unroll
         for (int tt = 0; tt < kChunkSteps; ++tt) {
-          tot[tt] -= wing_poly(wl, Tj[j][tt]);
+          tot[tt] -= outer_poly(wl, Tj[j][tt]);
         }
       }
       if (cm) {

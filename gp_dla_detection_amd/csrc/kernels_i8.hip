@@ -298,16 +298,16 @@ __global__ __launch_bounds__(256, 1) void likelihood_i8_kernel(LikelihoodI8Args 
       const double lam = rec[e * I::kScal];
       double t = 0.0;
       const double x0 = fma(lam, afac[0], -kC2), x1 = fma(lam, afac[1], -kC2), x2 = fma(lam, afac[2], -kC2);
-      cm |= (((fabs(x0) < kCoreX) | (fabs(x1) < kCoreX) | (fabs(x2) < kCoreX)) ? 1u : 0u) << e;
+      cm |= (((fabs(x0) < kOuterX) | (fabs(x1) < kOuterX) | (fabs(x2) < kOuterX)) ? 1u : 0u) << e;
       double T0, T1, T2;
       wing_T3(x0, x1, x2, T0, T1, T2);
-      t -= wing_poly(wing_g, T0);
-      t -= wing_poly(wing_g + kWingStride, T1);
-      t -= wing_poly(wing_g + 2 * kWingStride, T2);
+      t -= outer_poly(wing_g, T0);
+      t -= outer_poly(wing_g + kWingStride, T1);
+      t -= outer_poly(wing_g + 2 * kWingStride, T2);
       tot[e] = t;
     }
-    // (2) rare fix-up (z-sorted samples: a few % of wave-chunks): the core polynomial for the
-    //     lanes whose x falls in a line core, in raw_profile3's order (bit-identical result)
+    // (2) rare fix-up (z-sorted samples: a few % of wave-chunks): the lanes with some |x| < kOuterX
+    //     recomputed in raw_profile3's evaluation (core polynomial or inner wing)
     if (cm) {
 #pragma unroll
       for (int e = 0; e < 16; ++e) {

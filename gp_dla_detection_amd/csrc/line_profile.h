@@ -13,6 +13,10 @@
 //                   one Chebyshev fit per line of f_j(x) x^2 (smooth in T, -> lc_j y_j/pi^.5/(sigma
 //                   sqrt(2 pi)) as T -> 0); the factored T keeps the RELATIVE error at rounding
 //                   level however far out the wing is (max 5.6e-16 over |x| in [9, 3e7]).
+//   |x| >= kOuterX: the same function fitted again on T in (0, 1/kOuterX^2] at degree kOuterDeg
+//                   (same accuracy, 2 FMAs fewer per line): the batched sweeps evaluate it
+//                   branch-free and recompute the rare lanes with |x| < kOuterX (core or wing).
+//   Both wing polynomials of line j share one kWingStride block: wing at 0, outer at kOuterOff.
 //
 // All coefficients are fitted on the host from a long-double Faddeeva function
 // (faddeeva_host.cpp) at engine creation; accuracy is checked in the tests against
@@ -38,7 +42,10 @@ constexpr int kCoreDeg = 15;
 constexpr int kCoreStride = 16;  // kCoreDeg + 1
 constexpr int kCoreTable = kPieces * kCoreStride;  // doubles per line
 constexpr int kWingDeg = 8;      // wing polynomial degree in T
-constexpr int kWingStride = 10;  // doubles per line (kWingDeg + 1, padded to 16-byte pairs)
+constexpr double kOuterX = 14.0;  // outer wing: degree 6 on T <= 1/196 (max 5.9e-16 relative)
+constexpr int kOuterDeg = 6;
+constexpr int kOuterOff = 10;    // kWingDeg + 1, padded to 16-byte pairs
+constexpr int kWingStride = 18;  // doubles per line: wing (10) + outer (kOuterDeg + 1, padded)
 // far wing |x| >= kFarX (T <= 1e-4): the same function, degree kFarDeg (the batched sweeps take it
 // when a whole wave's chunk is that far from every line centre)
 constexpr double kFarX = 100.0;
@@ -74,6 +81,15 @@ GPDLA_HD double wing_poly(const double* __restrict__ c, double T) {
   double f = c[kWingDeg];
 #pragma unroll
   for (int n = kWingDeg - 1; n >= 0; --n) f = fma(f, T, c[n]);
+  return T * f;
+}
+
+// Outer wing (|x| >= kOuterX) from T = 1/x^2; c is the line's kWingStride block.
+GPDLA_HD double outer_poly(const double* __restrict__ c, double T) {
+  c += kOuterOff;
+  double f = c[kOuterDeg];
+#pragma unroll
+  for (int n = kOuterDeg - 1; n >= 0; --n) f = fma(f, T, c[n]);
   return T * f;
 }
 
