@@ -61,7 +61,6 @@ const HostLineData& host_line_data() {
     for (int j = 0; j < kMaxLines; ++j) {
       fit_core_table(j, d.buf.data() + (size_t)j * kCoreTable);
       fit_wing_line(j, d.buf.data() + kLineBufWing + (size_t)j * kWingStride);
-      fit_far_line(j, d.buf.data() + kLineBufFar + (size_t)j * kFarStride);
     }
     for (int j = 0; j < kMaxLines; ++j) {
       // fac_j = c / (lambda_j 1e8) / (sigma sqrt 2): x_j = lambda fac_j / (1+z) - c / (sigma sqrt 2)
@@ -223,7 +222,7 @@ int gpdla_diag_faddeeva_w(double x, double y, double* re, double* im);  // fadde
 
 int gpdla_diag_line_table_error(int32_t line, double* max_rel_err) {
   if (line < 0 || line >= kMaxLines || !max_rel_err) return set_error(GPDLA_EINVAL, "bad line");
-  *max_rel_err = std::max(line_profile_error(line), far_profile_error(line));  // incl. far wing
+  *max_rel_err = line_profile_error(line);  // core, wing and outer wing
   return GPDLA_OK;
 }
 

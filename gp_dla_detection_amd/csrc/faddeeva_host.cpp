@@ -183,27 +183,6 @@ void fit_wing_line(int j, double* wing) {
   fit_T_poly(j, (long double)kOuterX, kOuterDeg, kWingStride - kOuterOff, wing + kOuterOff);
 }
 
-// Far-wing polynomial of line j on T in (0, kFarT] (|x| >= kFarX), degree kFarDeg.
-void fit_far_line(int j, double* far) { fit_T_poly(j, (long double)kFarX, kFarDeg, kFarStride, far); }
-
-// Max relative error of the far-wing polynomial (|x| from kFarX geometrically out to 2e6).
-double far_profile_error(int j) {
-  std::vector<double> far(kFarStride);
-  fit_far_line(j, far.data());
-  long double scale, y;
-  line_scale(j, &scale, &y);
-  double maxrel = 0;
-  for (int i = 0; i <= 12000; ++i) {
-    const double x = kFarX * std::pow(1.00025, i);
-    const double T = 1.0 / (x * x);
-    const double got = far_poly(far.data(), T);
-    const long double ref = scale * faddeeva_w((long double)x, y).real();
-    const double rel = (double)std::fabs((got - ref) / ref);
-    if (rel > maxrel) maxrel = rel;
-  }
-  return maxrel;
-}
-
 // Core table of line j (kPieces x kCoreStride, polynomial in u = |x| - centre).
 void fit_core_table(int j, double* core) {
   long double scale, y;

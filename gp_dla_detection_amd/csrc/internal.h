@@ -117,14 +117,13 @@ struct PrepArgs {
 
 // Line-profile data.  Device buffer layout (doubles):
 //   [kMaxLines][kCoreTable] core tables | [kMaxLines][kWingStride] wing polynomials |
-//   fac[kMaxLines] | 2^(j/64)[64] | [kMaxLines][kFarStride] far-wing polynomials
+//   fac[kMaxLines] | 2^(j/64)[64]
 // fac_j = c / (lambda_j 1e8) / (sigma sqrt 2), so x_j = lambda * fac_j / (1 + z) - c / (sigma sqrt 2)
 // (voigt.c:278-279,287 divided by sigma sqrt 2).
 constexpr size_t kLineBufWing = (size_t)kMaxLines * kCoreTable;
 constexpr size_t kLineBufFac = kLineBufWing + (size_t)kMaxLines * kWingStride;
 constexpr size_t kLineBufExp2 = kLineBufFac + kMaxLines;  // 2^(j/64), j = 0..63 (exp_tab64)
-constexpr size_t kLineBufFar = kLineBufExp2 + 64;           // [kMaxLines][kFarStride] far wings
-constexpr size_t kLineBufDoubles = kLineBufFar + (size_t)kMaxLines * kFarStride;
+constexpr size_t kLineBufDoubles = kLineBufExp2 + 64;
 
 struct LineArgs {
   const double* buf;   // device line buffer (layout above)
@@ -367,8 +366,6 @@ int scratch_doubles(int K);
 // host-side table fitting (faddeeva_host.cpp)
 void fit_core_table(int line, double* core);
 void fit_wing_line(int line, double* wing);
-void fit_far_line(int line, double* far);
-double far_profile_error(int line);
 double line_profile_error(int line);
 
 }  // namespace gpdla

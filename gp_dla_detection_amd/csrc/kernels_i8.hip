@@ -158,12 +158,10 @@ __global__ __launch_bounds__(256, 1) void likelihood_i8_kernel(LikelihoodI8Args 
   constexpr int kWingLds = 4 * ((3 * kWingStride + 3) / 4);
   constexpr int kSBuf = I::kChunkSlots * I::kScal;  // doubles per slot-record buffer
   __shared__ __attribute__((aligned(16))) uint8_t ldsb[2 * I::kChunkBytes];
-  constexpr int kFarLds = 4 * ((3 * kFarStride + 3) / 4);
-  __shared__ __attribute__((aligned(16))) double ldss[2 * kSBuf + 3 * kCoreTable + kWingLds + 64 + kFarLds];
+  __shared__ __attribute__((aligned(16))) double ldss[2 * kSBuf + 3 * kCoreTable + kWingLds + 64];
   double* core_lds = ldss + 2 * kSBuf;
   double* wing_lds = core_lds + 3 * kCoreTable;
   double* exp_lds = wing_lds + kWingLds;
-  double* far_lds = exp_lds + 64;
 
   // XCD-aware block order, as likelihood_kernel
   const int64_t blocks_x = (a.S + 1 + kSamplesPerBlock - 1) / kSamplesPerBlock;
@@ -214,7 +212,6 @@ __global__ __launch_bounds__(256, 1) void likelihood_i8_kernel(LikelihoodI8Args 
   for (int i = threadIdx.x; i < 3 * kCoreTable; i += 256) core_lds[i] = a.lines.buf[i];
   if (threadIdx.x < 64) exp_lds[threadIdx.x] = a.lines.buf[kLineBufExp2 + threadIdx.x];
   if (threadIdx.x < 3 * kWingStride) wing_lds[threadIdx.x] = a.lines.buf[kLineBufWing + threadIdx.x];
-  if (threadIdx.x < 3 * kFarStride) far_lds[threadIdx.x] = a.lines.buf[kLineBufFar + threadIdx.x];
 
   const int g = lane >> 4;
   const int64_t s = s_base + (lane & 15);
@@ -268,31 +265,6 @@ __global__ __launch_bounds__(256, 1) void likelihood_i8_kernel(LikelihoodI8Args 
     //     interleaves the 16 independent chains), coefficients in SGPRs (uniform global loads)
     double tot[16];
     uint32_t cm = 0;
-    // |x| is monotone over a lane's 16 consecutive slots: test the two ends against kFarX; a wave
-    // entirely in the far wings of all three lines (most chunks) takes the degree-4 polynomials
-    bool far_ok = true;
-    {
-      const double la = rec[0], lb = rec[15 * I::kScal];
-#pragma unroll
-      for (int j = 0; j < 3; ++j) {
-        const double xa = fma(la, afac[j], -kC2), xb = fma(lb, afac[j], -kC2);
-        far_ok = far_ok && ((xa >= kFarX && xb >= kFarX) || (xa <= -kFarX && xb <= -kFarX));
-      }
-    }
-    if (__all(far_ok)) {
-#pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const double lam = rec[e * I::kScal];
-        const double x0 = fma(lam, afac[0], -kC2), x1 = fma(lam, afac[1], -kC2), x2 = fma(lam, afac[2], -kC2);
-        double T0, T1, T2;
-        wing_T3(x0, x1, x2, T0, T1, T2);
-        double t = 0.0;
-        t -= far_poly(far_lds, T0);
-        t -= far_poly(far_lds + kFarStride, T1);
-        t -= far_poly(far_lds + 2 * kFarStride, T2);
-        tot[e] = t;
-      }
-    } else
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
       const double lam = rec[e * I::kScal];

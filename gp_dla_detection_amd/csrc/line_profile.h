@@ -14,7 +14,7 @@
 //                   sqrt(2 pi)) as T -> 0); the factored T keeps the RELATIVE error at rounding
 //                   level however far out the wing is (max 5.6e-16 over |x| in [9, 3e7]).
 //   |x| >= kOuterX: the same function fitted again on T in (0, 1/kOuterX^2] at degree kOuterDeg
-//                   (same accuracy, 2 FMAs fewer per line): the batched sweeps evaluate it
+//                   (max 9.9e-16 relative, 4 FMAs fewer per line): the batched sweeps evaluate it
 //                   branch-free and recompute the rare lanes with |x| < kOuterX (core or wing).
 //   Both wing polynomials of line j share one kWingStride block: wing at 0, outer at kOuterOff.
 //
@@ -42,17 +42,13 @@ constexpr int kCoreDeg = 15;
 constexpr int kCoreStride = 16;  // kCoreDeg + 1
 constexpr int kCoreTable = kPieces * kCoreStride;  // doubles per line
 constexpr int kWingDeg = 8;      // wing polynomial degree in T
-constexpr double kOuterX = 14.0;  // outer wing: degree 6 on T <= 1/196 (max 5.9e-16 relative)
-constexpr int kOuterDeg = 6;
+// outer wing: degree 4 on T <= 1/32^2.  A/B on configs[1] (profiles/r3e): degree 6 beyond 14,
+// 5 beyond 20, 4 beyond 32 -> 78.64, 77.95, 77.40 ms (the wider fix-up zone costs less than the
+// FMAs saved); degree 3 needs |x| >= 64 for 2e-15
+constexpr double kOuterX = 32.0;
+constexpr int kOuterDeg = 4;
 constexpr int kOuterOff = 10;    // kWingDeg + 1, padded to 16-byte pairs
-constexpr int kWingStride = 18;  // doubles per line: wing (10) + outer (kOuterDeg + 1, padded)
-// far wing |x| >= kFarX (T <= 1e-4): the same function, degree kFarDeg (the batched sweeps take it
-// when a whole wave's chunk is that far from every line centre)
-constexpr double kFarX = 100.0;
-constexpr double kFarT = 1.0 / (kFarX * kFarX);
-constexpr int kFarDeg = 4;
-constexpr int kFarStride = 6;
-
+constexpr int kWingStride = 16;  // doubles per line: wing (10) + outer (kOuterDeg + 1, padded)
 GPDLA_HD double wing_eval(const double* __restrict__ c, double x) {
   const double x2 = x * x;
 #ifdef __HIP_DEVICE_COMPILE__
@@ -65,13 +61,6 @@ GPDLA_HD double wing_eval(const double* __restrict__ c, double x) {
   double f = c[kWingDeg];
 #pragma unroll
   for (int n = kWingDeg - 1; n >= 0; --n) f = fma(f, T, c[n]);
-  return T * f;
-}
-
-GPDLA_HD double far_poly(const double* __restrict__ c, double T) {
-  double f = c[kFarDeg];
-#pragma unroll
-  for (int n = kFarDeg - 1; n >= 0; --n) f = fma(f, T, c[n]);
   return T * f;
 }
 
