@@ -235,9 +235,9 @@ def run_e2e(args, world: int, rank: int, local_rank: int, dist) -> None:
 
 
 # rocprofv3 summaries of the bench workloads (tools/profile.sh + tools/summarize_profile.py), committed
-PROFILE_SUMMARY = ROOT / "profiles" / "r2x_summary.json"        # configs[1], fused fp64
+PROFILE_SUMMARY = ROOT / "profiles" / "r3i_summary.json"        # configs[1], fused fp64
 PROFILE_SUMMARY_C5 = {"panel-GEMM-int8": ROOT / "profiles" / "r2a_c5_summary.json",      # configs[4], 32-bit
-                      "panel-GEMM-int8-24": ROOT / "profiles" / "r2x_c5_summary.json"}   # configs[4], 24-bit
+                      "panel-GEMM-int8-24": ROOT / "profiles" / "r3i_c5_summary.json"}   # configs[4], 24-bit
 
 
 def profiled_traffic(Q: int, S: int, k: int, path: str = "fused"):

@@ -92,10 +92,13 @@ __device__ inline double exp_tab64(double v, const double* __restrict__ tab) {
 }
 
 // T_j = 1/x_j^2 of the three Lyman lines with ONE v_rcp_f64 (+ Newton step) on x0^2 x1^2 x2^2
-// (< 1e26 over the spectral range) instead of three.  Lanes with a tiny x (line cores) may get
-// inf/NaN here; their line sums are recomputed by the core fix-up.
+// (< 1e26 over the spectral range) instead of three.  a_j = x_j^2 + 2^-1000 (an fma, as cheap as
+// the multiply): bit-identical to x_j^2 for every x_j != 0 (|x_j| >= ~4e-12 on the path), and a lane
+// exactly on a line centre (x_j = 0) still gets finite T of the other two lines instead of
+// 0 * inf = NaN.  The core lanes' own T_j (huge) are discarded by the fix-up's core select.
 __device__ inline void wing_T3(double x0, double x1, double x2, double& T0, double& T1, double& T2) {
-  const double a0 = x0 * x0, a1 = x1 * x1, a2 = x2 * x2;
+  constexpr double kTiny = 0x1p-1000;
+  const double a0 = fma(x0, x0, kTiny), a1 = fma(x1, x1, kTiny), a2 = fma(x2, x2, kTiny);
   const double p01 = a0 * a1;
   const double q = p01 * a2;
   double R = __builtin_amdgcn_rcp(q);

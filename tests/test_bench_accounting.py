@@ -46,11 +46,11 @@ def test_i8_roofline_uses_the_gemm_launches(bench):
 
 def test_profiled_traffic_lookup(bench):
     t, src = bench.profiled_traffic(1024, 10000, 20, "fused")
-    assert t is not None and t > 0 and "r2x_summary" in src
+    assert t is not None and t > 0 and "r3i_summary" in src
     t24, src24 = bench.profiled_traffic(128, 100000, 50, "panel-GEMM-int8-24")
-    rows = json.loads((ROOT / "profiles" / "r2x_c5_summary.json").read_text())["kernels"]
+    rows = json.loads((ROOT / "profiles" / "r3i_c5_summary.json").read_text())["kernels"]
     assert t24 == sum(e["hbm_bytes_per_launch"] for e in rows if "gemm_i8_kernel" in e["kernel"])
-    assert "r2x_c5_summary" in src24
+    assert "r3i_c5_summary" in src24
     t5, src5 = bench.profiled_traffic(128, 100000, 50, "panel-GEMM-int8")
     rows = json.loads((ROOT / "profiles" / "r2a_c5_summary.json").read_text())["kernels"]
     want = sum(e["hbm_bytes_per_launch"] for e in rows if "gemm_i8_kernel" in e["kernel"])
