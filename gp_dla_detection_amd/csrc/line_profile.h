@@ -4,7 +4,7 @@
 //     V_j(v) = libcerf voigt(v, sigma, gamma_j) = Re w((v + i gamma_j) / (sigma sqrt 2)) / (sigma sqrt(2 pi))
 // and accumulates  total -= lc_j * V_j(v).  With x = v / (sigma sqrt 2) and the line's fixed
 // y_j = gamma_j / (sigma sqrt 2) (4.7e-4 ... 7e-8), f_j(x) = lc_j V_j is a 1-D function of x.
-// A GPU lane evaluates it with ~15 FMAs and no complex arithmetic:
+// A GPU lane evaluates it with 5 to 16 FMAs and no complex arithmetic:
 //
 //   |x| <  kCoreX : per-line piecewise polynomial (kPieces pieces of width kPieceW),
 //                   u = |x| - (p + 1/2) kPieceW,   f = sum_{n <= kCoreDeg} core_j[p][n] u^n
@@ -49,6 +49,7 @@ constexpr double kOuterX = 32.0;
 constexpr int kOuterDeg = 4;
 constexpr int kOuterOff = 10;    // kWingDeg + 1, padded to 16-byte pairs
 constexpr int kWingStride = 16;  // doubles per line: wing (10) + outer (kOuterDeg + 1, padded)
+
 GPDLA_HD double wing_eval(const double* __restrict__ c, double x) {
   const double x2 = x * x;
 #ifdef __HIP_DEVICE_COMPILE__
