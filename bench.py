@@ -283,15 +283,21 @@ def timed_steps(step, synchronize, steps: int, dist=None) -> float:
     return elapsed
 
 
-def dr12q_shard(pool_pixels, total: int, rank: int, world: int, split: bool):
-    """Pool indices of this rank's DR12Q-shaped spectra: spectrum i is pool entry i % len(pool).
-    configs[2] (``split`` False) keeps all on one GPU; configs[3] splits them by LPT on pixel
-    count (shard.py), so ranks get equal sweep work although n ranges over 270..1,250."""
+def dr12q_shard_ids(pool_pixels, total: int, rank: int, world: int, split: bool = True) -> np.ndarray:
+    """Spectrum ids (0..total-1, ascending) of this rank's share of the DR12Q-shaped workload, where
+    spectrum i is pool entry i % len(pool).  configs[2] (``split`` False) keeps all on one GPU;
+    configs[3] splits them by LPT on pixel count (shard.py), so ranks get equal sweep work although
+    n ranges over 270..1,250."""
     from gp_dla_detection_amd.shard import lpt_shards
-    idx = np.arange(total) % len(pool_pixels)
     if not split or world == 1:
-        return idx
-    return idx[lpt_shards(np.asarray(pool_pixels, dtype=np.float64)[idx], world)[rank]]
+        return np.arange(total)
+    idx = np.arange(total) % len(pool_pixels)
+    return lpt_shards(np.asarray(pool_pixels, dtype=np.float64)[idx], world)[rank]
+
+
+def dr12q_shard(pool_pixels, total: int, rank: int, world: int, split: bool):
+    """Pool indices of this rank's DR12Q-shaped spectra (dr12q_shard_ids modulo the pool size)."""
+    return dr12q_shard_ids(pool_pixels, total, rank, world, split) % len(pool_pixels)
 
 
 class _stdout_to_stderr:

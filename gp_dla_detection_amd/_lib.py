@@ -10,7 +10,7 @@ import ctypes as C
 import os
 from pathlib import Path
 
-LIB_PATH = Path(os.environ.get("GPDLA_LIB", Path(__file__).resolve().parent / "libgpdla.so"))
+LIB_PATH = Path(os.environ.get("GPDLA_LIB") or Path(__file__).resolve().parent / "libgpdla.so")
 
 GPDLA_OK = 0
 GPDLA_ENUMERIC = 1

@@ -10,7 +10,11 @@ directly:
 writer (``savemat73``)
   superblock v0 at file offset 512 (base address 512, the layout libhdf5 itself writes for a
   user block), old-style groups (v1 B-tree + symbol-table nodes + local heap), v1 object
-  headers, contiguous datasets.  Every variable carries MATLAB's ``MATLAB_class`` attribute
+  headers, contiguous datasets -- and chunked ones (v1 B-tree index) for large 2-D arrays, as
+  MATLAB's own v7.3 saves are chunked: a chunk is a block of whole MATLAB rows (all S columns of
+  ``chunk_rows`` spectra), so one process per GPU writes whole chunks of its own spectra with
+  one ``pwrite`` each instead of pieces of every file row.  Every variable carries MATLAB's
+  ``MATLAB_class`` attribute
   (plus ``MATLAB_int_decode`` for logical/char, ``MATLAB_empty`` for empties); cell arrays are
   object-reference datasets into ``#refs#`` as MATLAB writes them.  Array data is laid out
   MATLAB-style: a MATLAB r x c matrix is HDF5 dims (c, r), column-major bytes.  A variable may be
@@ -46,6 +50,8 @@ SIGNATURE = b"\x89HDF\r\n\x1a\n"
 USERBLOCK = 512
 LEAF_K = 4          # group leaf node K: a symbol-table node holds 2K entries (libhdf5 default)
 INTERNAL_K = 16     # group internal node K: a B-tree node holds 2K children (libhdf5 default)
+CHUNK_K = 32        # chunk B-tree K (indexed-storage K; a v0 superblock implies libhdf5's default 32)
+CHUNK_TARGET = 4 << 20   # bytes per chunk of a large 2-D array (auto_chunk_rows)
 _STREAM_BYTES = 1 << 26  # arrays at least this large are streamed into the file map
 
 _MATLAB_CLASS = {np.dtype(np.float64): "double", np.dtype(np.float32): "single",
@@ -67,11 +73,24 @@ class LazyArray:
 
     ``shape`` is the MATLAB shape (e.g. (Q, S)); ``fill(view)`` receives a writable
     array of that MATLAB shape and dtype (a Fortran-ordered view of the file's bytes) and must
-    assign every element.  ``fill=None`` defers the bytes to other writers (``open_region``)."""
+    assign every element.  ``fill=None`` defers the bytes to other writers (``open_region`` for a
+    contiguous variable, ``write_chunks`` for a chunked one).  ``chunk_rows`` makes the 2-D
+    variable chunked: HDF5 chunks of (columns, chunk_rows), i.e. blocks of whole MATLAB rows."""
     shape: tuple
     dtype: np.dtype
     fill: Callable[[np.ndarray], None] | None = None
-    src: np.ndarray | None = None   # set instead of fill: written by write_transposed (pwrite, no map)
+    src: np.ndarray | None = None   # set instead of fill: written by write_chunks / write_transposed
+    chunk_rows: int | None = None
+
+
+def auto_chunk_rows(cols: int, itemsize: int = 8, rows: int | None = None) -> int:
+    """MATLAB rows per chunk of a large R x ``cols`` array: ~CHUNK_TARGET bytes, a multiple of 8
+    rows, at most ``rows``.  It depends on the column count only, so every rank can shard its
+    spectra chunk-aligned before the file exists."""
+    row_bytes = max(cols * itemsize, 1)
+    r = max(8, int(round(CHUNK_TARGET / row_bytes / 8)) * 8)
+    r = min(r, max(1, 0xFFFFFFFF // row_bytes))            # chunk bytes < 4 GiB (32-bit B-tree key)
+    return max(1, min(r, rows)) if rows else r
 
 
 def _dt_message(dt: np.dtype) -> bytes:
@@ -125,6 +144,7 @@ class _Node:
 
     def __init__(self, name, kind, **kw):
         self.name, self.kind = name, kind
+        self.chunk = None
         self.__dict__.update(kw)
         self.addr = None
 
@@ -135,7 +155,7 @@ def _matlab_node(name: str, value, refs: list) -> _Node:
     if isinstance(value, LazyArray):
         dt = np.dtype(value.dtype)
         return _Node(name, "dataset", dims=tuple(reversed(value.shape)), dtype=dt, data=None,
-                     lazy=value, attrs=[("MATLAB_class", _MATLAB_CLASS[dt])])
+                     lazy=value, chunk=_chunk_dims(value), attrs=[("MATLAB_class", _MATLAB_CLASS[dt])])
     if isinstance(value, dict):
         # MATLAB scalar struct: a group with MATLAB_class "struct", one member per field (this is
         # also the side format for the catalogue's containers.Map variables, SURVEY.md 7 viii)
@@ -182,12 +202,24 @@ def _matlab_node(name: str, value, refs: list) -> _Node:
     if arr.size == 0:
         return _empty_node(name, arr.shape, cls, extra=attrs)
     if arr.nbytes >= _STREAM_BYTES and arr.ndim == 2:
-        # large: transposed band by band into the file with pwrite (write_transposed), no full host copy
+        # large: chunked (blocks of whole rows), each chunk transposed and pwritten (write_chunks)
+        lazy = LazyArray(arr.shape, arr.dtype, src=arr,
+                         chunk_rows=auto_chunk_rows(arr.shape[1], arr.dtype.itemsize, arr.shape[0]))
         return _Node(name, "dataset", dims=tuple(reversed(arr.shape)), dtype=arr.dtype, data=None,
-                     lazy=LazyArray(arr.shape, arr.dtype, src=arr), attrs=[("MATLAB_class", cls)] + attrs)
+                     lazy=lazy, chunk=_chunk_dims(lazy), attrs=[("MATLAB_class", cls)] + attrs)
     data = np.asfortranarray(arr)
     return _Node(name, "dataset", dims=tuple(reversed(arr.shape)), dtype=data.dtype, data=data, lazy=None,
                  attrs=[("MATLAB_class", cls)] + attrs)
+
+
+def _chunk_dims(lazy: LazyArray):
+    """HDF5 chunk dims (C order: columns, rows) of a chunked LazyArray, or None."""
+    if not lazy.chunk_rows:
+        return None
+    if len(lazy.shape) != 2:
+        raise ValueError("a chunked LazyArray must be 2-D")
+    R, C = (int(d) for d in lazy.shape)
+    return (C, int(min(lazy.chunk_rows, max(R, 1))))
 
 
 def fill_transposed(view, src, tile_rows: int = 512, tile_cols: int = 2048, threads: int | None = None):
@@ -246,6 +278,41 @@ def write_transposed(path: str, offset: int, src: np.ndarray, row0: int = 0, row
         os.close(fd)
 
 
+def write_chunks(path: str, region: "Region", src: np.ndarray, row0: int = 0, threads: int | None = None):
+    """Write MATLAB rows row0 .. row0 + R of a chunked region (savemat73 with a ``chunk_rows``
+    LazyArray).  ``src`` is R x C, spectrum-major like the engine's output, and must cover whole
+    chunks: row0 a multiple of chunk_rows, and R too unless the block ends at the last row.  Each
+    chunk is transposed into its own buffer (the chunk's C-order (C, chunk_rows) bytes, the last one
+    zero-padded) and written with one ``pwrite``.  Chunks are disjoint 4 KiB-aligned file ranges,
+    so processes can write their own chunks concurrently."""
+    from concurrent.futures import ThreadPoolExecutor
+    cr, stride = region.chunk_rows, region.chunk_stride
+    C, Rt = region.dims
+    R = src.shape[0]
+    if not cr:
+        raise ValueError("region is not chunked (use write_transposed)")
+    if src.ndim != 2 or src.shape[1] != C or row0 % cr or row0 + R > Rt or (R % cr and row0 + R != Rt):
+        raise ValueError(f"rows {row0}..{row0 + R} of a {Rt} x {C} array are not whole {cr}-row chunks")
+    dt = np.dtype(region.dtype)
+    if threads is None:
+        threads = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else 1))
+    fd = os.open(path, os.O_WRONLY)
+    try:
+        def run(r0):
+            r1 = min(R, r0 + cr)
+            buf = np.zeros((C, cr), dtype=dt)
+            buf[:, : r1 - r0] = src[r0:r1].T
+            mv, pos = memoryview(buf).cast("B"), region.offset + (row0 + r0) // cr * stride
+            while len(mv):
+                n = os.pwrite(fd, mv, pos)
+                mv, pos = mv[n:], pos + n
+
+        with ThreadPoolExecutor(threads) as ex:
+            list(ex.map(run, range(0, R, cr)))
+    finally:
+        os.close(fd)
+
+
 def _empty_node(name, shape, cls, extra=()):
     # MATLAB stores an empty array as its dimensions (uint64) plus MATLAB_empty = 1
     dims = np.array(shape if len(shape) >= 2 else (0, 0), dtype=np.uint64)
@@ -264,13 +331,19 @@ def _refname(i: int) -> str:
 
 
 def _dataset_header(node: _Node, data_addr: int) -> bytes:
+    """v1 object header of a dataset.  ``data_addr`` is the data (contiguous layout) or the root
+    node of the chunk B-tree (chunked: layout message v3 class 2, the chunk dims + element size)."""
     if getattr(node, "ref_targets", None) is not None:
         dt, nbytes = _DT_OBJREF, 8 * len(node.ref_targets)
     else:
         dt = _dt_message(node.dtype)
         nbytes = int(np.prod(node.dims)) * node.dtype.itemsize
-    msgs = [(0x0001, _pad8(_dataspace(node.dims))), (0x0003, _pad8(dt)),
-            (0x0008, _pad8(bytes([3, 1]) + struct.pack("<QQ", data_addr, nbytes)))]
+    if node.chunk is not None:
+        layout = bytes([3, 2, len(node.chunk) + 1]) + struct.pack("<Q", data_addr) \
+            + struct.pack(f"<{len(node.chunk) + 1}I", *node.chunk, node.dtype.itemsize)
+    else:
+        layout = bytes([3, 1]) + struct.pack("<QQ", data_addr, nbytes)
+    msgs = [(0x0001, _pad8(_dataspace(node.dims))), (0x0003, _pad8(dt)), (0x0008, _pad8(layout))]
     msgs += [(0x000C, _attr_message(k, v)) for k, v in node.attrs]
     return _object_header(msgs)
 
@@ -303,6 +376,59 @@ def _group_blocks(entries: list[_Node]):
             break
         count = n_nodes
     return entries, bytes(heap_data), name_off, snods, snod_size, node_size, levels
+
+
+def _chunk_plan(node: _Node) -> dict:
+    """Sizes of a chunked 2-D dataset: its chunks (whole blocks of rows, each at a 4 KiB-aligned
+    stride) and its v1 B-tree (type 1, raw-data chunks): 2K children per node, levels until one
+    root.  Node size as libhdf5 computes it from K, so its reader finds every key."""
+    C, Rt = node.dims
+    cr = node.chunk[1]
+    nchunks = max(1, -(-Rt // cr))
+    chunk_bytes = C * cr * node.dtype.itemsize
+    key_size = 8 + 8 * (len(node.chunk) + 1)
+    levels, count = [], nchunks
+    while True:
+        count = -(-count // (2 * CHUNK_K))
+        levels.append(count)
+        if count == 1:
+            break
+    return dict(nchunks=nchunks, rows=cr, chunk_bytes=chunk_bytes, stride=-(-chunk_bytes // 4096) * 4096,
+                key_size=key_size, node_size=24 + 2 * CHUNK_K * 8 + (2 * CHUNK_K + 1) * key_size, levels=levels)
+
+
+def _chunk_btree(node: _Node, plan: dict, node_addrs: list, chunk_base: int) -> list[tuple[int, bytes]]:
+    """Encode the chunk B-tree: key i = (chunk bytes, filter mask 0, offsets (0, i * rows, 0)) in
+    front of child i; the key after the last chunk is the right bound libhdf5 writes (every scaled
+    coordinate + 1, zero size).  Internal nodes carry their children's first keys and the right key
+    of their last child."""
+    C = node.dims[0]
+    n, cr, isz = plan["nchunks"], plan["rows"], node.dtype.itemsize
+
+    def key(i):
+        if i < n:
+            return struct.pack("<II3Q", plan["chunk_bytes"], 0, 0, i * cr, 0)
+        return struct.pack("<II3Q", 0, 0, C, n * cr, isz)
+
+    out = []
+    per = 2 * CHUNK_K
+    # spans[j] = (first chunk, end chunk) under child j of the current level
+    children = [chunk_base + i * plan["stride"] for i in range(n)]
+    spans = [(i, i + 1) for i in range(n)]
+    for level, addrs in enumerate(node_addrs):
+        new_spans = []
+        for j, addr in enumerate(addrs):
+            ch, sp = children[j * per:(j + 1) * per], spans[j * per:(j + 1) * per]
+            left = addrs[j - 1] if j > 0 else UNDEF
+            right = addrs[j + 1] if j + 1 < len(addrs) else UNDEF
+            b = b"TREE" + bytes([1, level]) + struct.pack("<HQQ", len(ch), left, right)
+            for c, (lo, _) in zip(ch, sp):
+                b += key(lo) + struct.pack("<Q", c)
+            b += key(sp[-1][1])
+            out.append((addr, b.ljust(plan["node_size"], b"\0")))
+            new_spans.append((sp[0][0], sp[-1][1]))
+        children, spans = addrs, new_spans
+    return out
 
 
 class _Layout:
@@ -351,6 +477,10 @@ def savemat73(path: str, variables: dict, created: str | None = None) -> dict:
     rg = gmeta[0]
     for n in datasets:
         n.addr = L.alloc(len(_dataset_header(n, 0)))
+    for n in datasets:                      # chunk B-trees (metadata; the chunks go with the lazy data)
+        if n.chunk is not None:
+            n.plan = _chunk_plan(n)
+            n.tree = [[L.alloc(n.plan["node_size"]) for _ in range(cnt)] for cnt in n.plan["levels"]]
     data_addr = {}
 
     def nbytes(n):
@@ -364,7 +494,8 @@ def savemat73(path: str, variables: dict, created: str | None = None) -> dict:
     meta_end = L.pos
     for n in datasets:
         if n.lazy is not None:
-            data_addr[id(n)] = L.alloc(max(nbytes(n), 1), align=4096)
+            size = n.plan["nchunks"] * n.plan["stride"] if n.chunk is not None else max(nbytes(n), 1)
+            data_addr[id(n)] = L.alloc(size, align=4096)
     eof = L.pos
     # pass 2: encode the metadata and the eager data
     img = bytearray(meta_end)
@@ -407,6 +538,11 @@ def savemat73(path: str, variables: dict, created: str | None = None) -> dict:
                 new_last.append(lk[-1])
             children, child_last = nodes, new_last
     for n in datasets:
+        if n.chunk is not None:
+            put(n.addr, _dataset_header(n, n.tree[-1][0]))
+            for addr, b in _chunk_btree(n, n.plan, n.tree, data_addr[id(n)]):
+                put(addr, b)
+            continue
         put(n.addr, _dataset_header(n, data_addr[id(n)]))
         if getattr(n, "ref_targets", None) is not None:
             put(data_addr[id(n)], np.array([t.addr for t in n.ref_targets], dtype="<u8").tobytes())
@@ -424,13 +560,20 @@ def savemat73(path: str, variables: dict, created: str | None = None) -> dict:
         f.truncate(USERBLOCK + eof)     # lazy regions: sparse until filled through the memory map
     regions = {}
     for n in lazies:
-        reg = Region(USERBLOCK + data_addr[id(n)], tuple(int(d) for d in n.dims), np.dtype(n.dtype).str)
+        chunked = n.chunk is not None
+        reg = Region(USERBLOCK + data_addr[id(n)], tuple(int(d) for d in n.dims), np.dtype(n.dtype).str,
+                     n.plan["rows"] if chunked else 0, n.plan["stride"] if chunked else 0)
         regions[n.name] = reg
         if n.lazy.src is not None:
-            write_transposed(path, reg.offset, n.lazy.src)
+            if chunked:
+                write_chunks(path, reg, n.lazy.src)
+            else:
+                write_transposed(path, reg.offset, n.lazy.src)
             continue
         if n.lazy.fill is None:
-            continue                                         # deferred: filled later via open_region
+            continue                          # deferred: filled later via open_region / write_chunks
+        if chunked:
+            raise ValueError(f"{n.name}: a chunked LazyArray takes src= or is deferred, not fill=")
         mm = open_region(path, reg)
         n.lazy.fill(mm)
         # no msync: like MATLAB's save (plain writes), the data is in the page cache and visible
@@ -442,16 +585,22 @@ def savemat73(path: str, variables: dict, created: str | None = None) -> dict:
 @dataclass(frozen=True)
 class Region:
     """Where a variable's bytes live in a written file: absolute byte offset, HDF5 (C-order) dims
-    and numpy dtype string.  A ``LazyArray`` with ``fill=None`` is left for other writers (e.g.
-    one process per GPU, each writing its own spectra) to fill through ``open_region``."""
+    and numpy dtype string; for a chunked variable, MATLAB rows per chunk and the byte stride
+    between chunks (``offset`` is then the first chunk).  A ``LazyArray`` with ``fill=None`` is
+    left for other writers (e.g. one process per GPU, each writing its own spectra) to fill
+    through ``open_region`` (contiguous) or ``write_chunks`` (chunked)."""
     offset: int
     dims: tuple
     dtype: str
+    chunk_rows: int = 0
+    chunk_stride: int = 0
 
 
 def open_region(path: str, region: Region, mode: str = "r+") -> np.ndarray:
-    """A writable view of a variable's data in MATLAB shape (the transpose of a memory map of
-    the HDF5 C-order dims).  Several processes may fill disjoint parts of it concurrently."""
+    """A writable view of a contiguous variable's data in MATLAB shape (the transpose of a memory
+    map of the HDF5 C-order dims).  Several processes may fill disjoint parts of it concurrently."""
+    if region.chunk_rows:
+        raise ValueError("chunked region: write it with write_chunks")
     mm = np.memmap(path, dtype=np.dtype(region.dtype).newbyteorder("<"), mode=mode,
                    offset=region.offset, shape=region.dims)
     return mm.T

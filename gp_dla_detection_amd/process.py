@@ -267,7 +267,8 @@ def _indices(sel, n: int) -> np.ndarray:
 def run_process_qsos(base_directory: str, training_release: str, training_set_name: str,
                      dla_catalog_name: str, prior_ind, release: str, test_set_name: str, test_ind,
                      params: Parameters | None = None, device: int = 0, save: bool = True,
-                     rank: int = 0, world: int = 1, compute=None, timings: dict | None = None) -> dict:
+                     rank: int = 0, world: int = 1, compute=None, timings: dict | None = None,
+                     chunk_rows: int | None = None) -> dict:
     """The whole ``process_qsos`` script (process_qsos.m:1-249) on files laid out as the reference
     lays them out (set_parameters.m:79-86):
 
@@ -284,18 +285,22 @@ def run_process_qsos(base_directory: str, training_release: str, training_set_na
 
     Multi-GPU (``world`` > 1; one process per GPU with a torch.distributed process group already
     initialised, gloo suffices): rank r decodes and evaluates only its contiguous shard of the
-    test spectra on ``device``.  Rank 0 gathers the per-spectrum scalars (not the sample
-    arrays), computes priors and posteriors, and writes the file with the Q x S sample array as a
-    deferred region; every rank then writes its own rows of that region in place (disjoint
-    parts of one memory-mapped file), so the 13 GB full-DR12Q array is never gathered.
-    ``compute(model, samples, packed, params, device) -> dict`` replaces the engine (tests).
+    test spectra on ``device``.  The Q x S sample array is a chunked HDF5 dataset whose chunks
+    are blocks of whole rows (``matv73.auto_chunk_rows`` spectra each, ~4 MB), and the shards are
+    whole chunk blocks, LPT-balanced on the expected pixel count of each block (``shard.py``), so
+    ranks get equal sweep work and each writes only whole chunks of its own.  Rank 0 gathers the
+    per-spectrum scalars (not the sample arrays), computes priors and posteriors, and writes the
+    file with the sample array deferred; every rank then pwrites its own chunks (disjoint 4 KiB-
+    aligned ranges of the one file), so the 13 GB full-DR12Q array is never gathered.
+    ``compute(model, samples, packed, params, device) -> dict`` replaces the engine (tests);
+    ``chunk_rows`` overrides the sharded file's rows per chunk (tests).
     ``timings`` (a dict) receives this rank's wall seconds per phase: load (the four input files,
     process_qsos.m:1-63), compute (the engine, :88-212) and write (priors / posteriors and the
     v7.3 file, :222-249).
     Rank 0 returns the saved scalars; other ranks their local results."""
     import time
-    from .matv73 import LazyArray, loadmat, write_transposed
-    from .shard import contiguous_shards, merge_shards
+    from .matv73 import LazyArray, auto_chunk_rows, loadmat, write_chunks
+    from .shard import block_lpt_shards, expected_pixels, merge_shards
     compute = compute or _engine_compute
     tm = timings if timings is not None else {}
     t_start = time.perf_counter()
@@ -313,7 +318,9 @@ def run_process_qsos(base_directory: str, training_release: str, training_set_na
     tind = evaluate_index(test_ind, catalog=catalog).astype(bool).ravel()
     tidx = np.flatnonzero(tind)
     z_all = np.asarray(catalog["z_qsos"], dtype=np.float64).ravel()[tidx]
-    shards = contiguous_shards(tidx.size, world)
+    S = np.asarray(samples["nhi_samples"]).size
+    chunk_rows = chunk_rows or auto_chunk_rows(S, 8, tidx.size)
+    shards = block_lpt_shards(expected_pixels(z_all), chunk_rows, world)
     mine = shards[rank]
     spectra = load_preloaded_qsos(f"{rdir}/preloaded_qsos.mat", tidx[mine])
     for sp, z in zip(spectra, z_all[mine]):
@@ -359,16 +366,19 @@ def run_process_qsos(base_directory: str, training_release: str, training_set_na
             merged["numeric_warning"] = "; ".join(warns)
         out = _finish(merged, z_all, prior, params, meta)
         out["test_ind"] = tind
-        if save:
-            S = np.asarray(samples["nhi_samples"]).size
-            out["sample_log_likelihoods_dla"] = LazyArray((tidx.size, S), np.float64)   # deferred
+        if save:   # deferred, chunked by the rows the shards were cut on
+            out["sample_log_likelihoods_dla"] = LazyArray((tidx.size, S), np.float64, chunk_rows=chunk_rows)
             region[0] = save_processed_qsos(path, out)["sample_log_likelihoods_dla"]
             del out["sample_log_likelihoods_dla"]
     if save:
         dist.broadcast_object_list(region, src=0)
-        if mine.size:  # this rank's rows, straight into the file (page cache; no msync, as matv73)
-            write_transposed(path, region[0].offset, np.asarray(res["sample_log_likelihoods_dla"]),
-                             row0=int(mine[0]), rows_total=int(region[0].dims[1]))
+        # this rank's chunks, straight into the file (page cache; no msync, as matv73): one call per
+        # run of consecutive blocks
+        sll = np.asarray(res["sample_log_likelihoods_dla"])
+        breaks = np.flatnonzero(np.diff(mine) != 1) + 1
+        for lo, hi in zip(np.r_[0, breaks], np.r_[breaks, mine.size]):
+            if hi > lo:
+                write_chunks(path, region[0], sll[lo:hi], row0=int(mine[lo]))
         dist.barrier()
     tm["write_s"] = time.perf_counter() - t_comp
     return out if rank == 0 else res

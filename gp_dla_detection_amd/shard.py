@@ -34,6 +34,32 @@ def lpt_shards(costs, world: int) -> list[np.ndarray]:
     return [np.flatnonzero(owner == r) for r in range(world)]
 
 
+def block_lpt_shards(costs, block: int, world: int) -> list[np.ndarray]:
+    """LPT over blocks of ``block`` consecutive spectra (the last block may be short): each rank
+    gets whole blocks, so with ``block`` = the output file's chunk rows (matv73.auto_chunk_rows) every
+    rank writes whole chunks of the Q x S sample array and no two ranks share a file range.  Each
+    shard is returned sorted."""
+    costs = np.asarray(costs, dtype=np.float64)
+    n = costs.size
+    if n == 0:
+        return [np.zeros(0, np.int64) for _ in range(world)]
+    starts = np.arange(0, n, block)
+    owners = lpt_shards(np.add.reduceat(costs, starts), world)
+    return [np.concatenate([np.arange(starts[b], min(n, starts[b] + block)) for b in blk]).astype(np.int64)
+            if blk.size else np.zeros(0, np.int64) for blk in owners]
+
+
+def expected_pixels(z_qsos, blue_limit: float = 3600.0) -> np.ndarray:
+    """Sweep-cost proxy before any spectrum is decoded: the 1e-4 dex pixels a spectrum at z_QSO has
+    in the modelled rest range (set_parameters.m:33-35, 59-60), observed-frame clipped at the
+    spectrograph's blue edge (BOSS: 3600 A).  Only balances shards; it never changes a result."""
+    from .parameters import MAX_LAMBDA, MIN_LAMBDA, PIXEL_SPACING
+    z = np.asarray(z_qsos, dtype=np.float64)
+    top = np.log10(MAX_LAMBDA * (1 + z))
+    bottom = np.maximum(np.log10(MIN_LAMBDA * (1 + z)), np.log10(blue_limit))
+    return np.maximum((top - bottom) / PIXEL_SPACING, 1.0)
+
+
 def subset_packed(packed: dict, idx: np.ndarray) -> dict:
     """CSR subset of packed spectra (see synthetic.pack_spectra)."""
     off = packed["offsets"]

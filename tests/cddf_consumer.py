@@ -7,6 +7,8 @@ import json
 import sys
 import warnings
 
+sys.dont_write_bytecode = True   # never write __pycache__ into the read-only reference tree
+
 warnings.filterwarnings("ignore")
 import numpy as np  # noqa: E402
 

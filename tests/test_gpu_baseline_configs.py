@@ -119,38 +119,67 @@ def test_config4_panel_gemm_i8_k50_100k():
         assert np.all(tol_ok(lln, nref)) and _rel(lln, nref) < bar, (path, _rel(lln, nref))
 
 
-def test_config2_full_dr12q_count_one_gpu():
-    """configs[2]: 162,861 DR12Q-shaped spectra (n = 270..1,250; a seeded pool of 4,096 distinct
-    spectra tiled to the count, as bench.py's c3 workload) x 10^4 samples on one GPU, outputs
-    resident in HBM (13 GB).  The invariant on every spectrum, oracle spot checks on sampled
-    spectra, and the tiled copies of a pool spectrum agree bitwise (position independence)."""
+def _dr12q_device_inputs(pool_packed, idx):
+    """Device CSR inputs for spectra ``idx`` of the tiled DR12Q-shaped pool (spectrum i = pool entry
+    idx[i]), built from the packed pool without materialising per-spectrum host copies."""
+    pp = pool_packed
+    lens = np.diff(pp["offsets"])
+    offsets = np.zeros(idx.size + 1, np.int64)
+    np.cumsum(lens[idx], out=offsets[1:])
+    starts = pp["offsets"][idx]
+    pix = (np.repeat(starts - offsets[:-1], lens[idx]) + np.arange(offsets[-1])).astype(np.int64)
+    dev = {key: L.DeviceArray.from_numpy(pp[key][pix]) for key in ("wavelengths", "flux", "noise_variance",
+                                                                     "pixel_mask")}
+    dev["z_qsos"] = L.DeviceArray.from_numpy(pp["z_qsos"][idx])
+    return offsets, dev
+
+
+def _run_device(eng, offsets, dev, S):
+    Q = offsets.size - 1
+    o_null, o_dla = L.DeviceArray(0, Q, np.float64), L.DeviceArray(0, Q, np.float64)
+    o_s = L.DeviceArray(0, (Q, S), np.float64)
+    o_n = L.DeviceArray(0, Q, np.int32)
+    eng.process_device(offsets, dev["wavelengths"].ptr, dev["flux"].ptr, dev["noise_variance"].ptr,
+                       dev["pixel_mask"].ptr, dev["z_qsos"].ptr, o_null.ptr, o_dla.ptr, o_s.ptr, S,
+                       npix_ptr=o_n.ptr)
+    eng.synchronize()
+    return o_null, o_dla, o_s, o_n
+
+
+@pytest.fixture(scope="module")
+def dr12q_full():
+    """configs[2]'s workload on one GPU: 162,861 DR12Q-shaped spectra (n = 270..1,250; a seeded pool
+    of 4,096 distinct spectra tiled to the count, as bench.py's c3/c4 workloads) x 10^4 samples,
+    outputs resident in HBM (13 GB).  Shared by the configs[2] and configs[3] tests."""
     t0 = time.time()
     Q, S, P = 162861, 10000, 4096
     model = syn.make_model(k=20)
     samples = syn.make_samples(S)
     pool = syn.make_dr12q_like_spectra(model, P, seed=12, mask_fraction=0.0)
     pp = syn.pack_spectra(pool)
-    lens = np.diff(pp["offsets"])
-    reps = -(-Q // P)
     idx = np.arange(Q) % P
-    offsets = np.zeros(Q + 1, np.int64)
-    np.cumsum(lens[idx], out=offsets[1:])
-    dev = {}
-    for key in ("wavelengths", "flux", "noise_variance", "pixel_mask"):
-        dev[key] = L.DeviceArray.from_numpy(np.tile(pp[key], reps)[: offsets[-1]])
-    dev["z_qsos"] = L.DeviceArray.from_numpy(pp["z_qsos"][idx])
-    o_null, o_dla = L.DeviceArray(0, Q, np.float64), L.DeviceArray(0, Q, np.float64)
-    o_s = L.DeviceArray(0, (Q, S), np.float64)
-    o_n = L.DeviceArray(0, Q, np.int32)
+    offsets, dev = _dr12q_device_inputs(pp, idx)
     print(f"setup {time.time() - t0:.1f} s", flush=True)
     with Engine(model, samples, set_parameters(k=20)) as eng:
         t1 = time.time()
-        eng.process_device(offsets, dev["wavelengths"].ptr, dev["flux"].ptr, dev["noise_variance"].ptr,
-                           dev["pixel_mask"].ptr, dev["z_qsos"].ptr, o_null.ptr, o_dla.ptr, o_s.ptr, S,
-                           npix_ptr=o_n.ptr)
-        eng.synchronize()
+        o_null, o_dla, o_s, o_n = _run_device(eng, offsets, dev, S)
         print(f"engine {time.time() - t1:.1f} s", flush=True)
-    lld, lln, npix = o_dla.numpy(), o_null.numpy(), o_n.numpy()
+    del dev
+    yield dict(Q=Q, S=S, P=P, model=model, samples=samples, pool=pool, pp=pp, idx=idx,
+               o_null=o_null, o_dla=o_dla, o_s=o_s, o_n=o_n)
+    for a in (o_null, o_dla, o_s, o_n):
+        a.free()
+
+
+def test_config2_full_dr12q_count_one_gpu(dr12q_full):
+    """configs[2]: the full DR12Q count on one GPU.  The invariant on every spectrum, oracle spot
+    checks on sampled spectra, and the tiled copies of a pool spectrum agree bitwise (position
+    independence)."""
+    t0 = time.time()
+    F = dr12q_full
+    Q, S, P, idx, pool = F["Q"], F["S"], F["P"], F["idx"], F["pool"]
+    model, samples, o_s = F["model"], F["samples"], F["o_s"]
+    lld, lln, npix = F["o_dla"].numpy(), F["o_null"].numpy(), F["o_n"].numpy()
     assert np.isfinite(lld).all() and np.isfinite(lln).all()
     assert npix.min() >= 250 and npix.max() <= 1300
     # the invariant on every spectrum, streamed back in row blocks
@@ -177,3 +206,46 @@ def test_config2_full_dr12q_count_one_gpu():
     assert np.all(tol_ok(got, ref)) and _rel(got, ref) < 1e-9, _rel(got, ref)
     assert _rel(lln[list(rows)], nref) < 1e-9
     print(f"total {time.time() - t0:.1f} s", flush=True)
+
+
+def test_config3_dr12q_8way_lpt_split_bitwise(dr12q_full):
+    """configs[3]: the same full DR12Q count split 8 ways by bench.py's LPT shard (dr12q_shard with
+    split=True, the c4 workload; process_qsos.m:88's serial spectrum loop sharded).  Each of the 8
+    shards runs through its own Engine (in sequence on the one GPU, as 8 ranks would on 8 GPUs) and
+    the reassembled outputs are bitwise equal to the unsharded configs[2] run on every spectrum and
+    every sample; the invariant holds on every spectrum of every shard."""
+    import bench
+    F = dr12q_full
+    Q, S, P, pp = F["Q"], F["S"], F["P"], F["pp"]
+    world = 8
+    pix = np.diff(pp["offsets"])
+    full_dla, full_null, full_n = F["o_dla"].numpy(), F["o_null"].numpy(), F["o_n"].numpy()
+    full_s = F["o_s"].numpy()          # 13 GB on the host (the box has ~270 GB)
+    seen = np.zeros(Q, bool)
+    loads = []
+    for rank in range(world):
+        mine = bench.dr12q_shard(pix, Q, rank, world, split=True)   # pool indices of this rank
+        ids = bench.dr12q_shard_ids(pix, Q, rank, world)
+        assert np.array_equal(ids % P, mine)
+        assert not seen[ids].any()
+        seen[ids] = True
+        loads.append(int(pix[mine].sum()))
+        t1 = time.time()
+        offsets, dev = _dr12q_device_inputs(pp, mine)
+        with Engine(F["model"], F["samples"], set_parameters(k=20)) as eng:
+            o_null, o_dla, o_s, o_n = _run_device(eng, offsets, dev, S)
+        del dev
+        got_s = o_s.numpy()
+        np.testing.assert_array_equal(got_s, full_s[ids])
+        np.testing.assert_array_equal(o_dla.numpy(), full_dla[ids])
+        np.testing.assert_array_equal(o_null.numpy(), full_null[ids])
+        np.testing.assert_array_equal(o_n.numpy(), full_n[ids])
+        inv = _invariant(got_s, o_dla.numpy())
+        assert float(np.max(np.abs(inv - 1.0))) < 1e-12
+        for a in (o_null, o_dla, o_s, o_n):
+            a.free()
+        del got_s
+        print(f"rank {rank}: {ids.size} spectra, {loads[-1]} pixels, {time.time() - t1:.1f} s", flush=True)
+    assert seen.all()
+    # LPT balance: every shard's sweep work within 0.1% of the mean
+    assert max(loads) / (sum(loads) / world) < 1.001, loads

@@ -76,6 +76,54 @@ def test_large_array_streams_in_blocks(tmp_path):
     assert np.array_equal(M.loadmat73(str(path))["big"], a)
 
 
+@pytest.mark.parametrize("chunk_rows", [1, 7, 64])
+def test_chunked_deferred_region_written_by_blocks(tmp_path, chunk_rows):
+    """Sharded saves: a deferred chunked Q x S region (chunks = blocks of whole rows, a multi-level
+    chunk B-tree when there are > 64 chunks), filled by several writers with write_chunks in
+    arbitrary block order, each a run of whole chunks; the last chunk is partial.  Misaligned
+    blocks are refused."""
+    rng = np.random.default_rng(6)
+    Q, S = 203, 77
+    full = rng.standard_normal((Q, S))
+    path = str(tmp_path / "c.mat")
+    reg = M.savemat73(path, dict(x=np.arange(3.0), sample_log_likelihoods_dla=M.LazyArray(
+        (Q, S), np.float64, chunk_rows=chunk_rows)))["sample_log_likelihoods_dla"]
+    assert reg.chunk_rows == chunk_rows and reg.chunk_stride % 4096 == 0
+    nb = -(-Q // chunk_rows)
+    blocks = np.array_split(rng.permutation(nb), 3)
+    for blk in blocks:
+        for b in sorted(blk):
+            r0, r1 = b * chunk_rows, min(Q, (b + 1) * chunk_rows)
+            M.write_chunks(path, reg, full[r0:r1], row0=r0, threads=2)
+    assert np.array_equal(M.loadmat73(path)["sample_log_likelihoods_dla"], full)
+    if chunk_rows > 1:
+        with pytest.raises(ValueError):
+            M.write_chunks(path, reg, full[1:chunk_rows + 1], row0=1)
+    with pytest.raises(ValueError):
+        M.open_region(path, reg)
+
+
+@needs_h5py
+def test_h5py_reads_chunked_sample_array(tmp_path):
+    """libhdf5 (h5py) reads the chunked layout: 251 chunks of 8 rows (a two-level chunk B-tree),
+    the (S, Q) shape and (S, 8) chunk shape MATLAB-style, whole-array, column (one spectrum,
+    calc_cddf.py:240) and partial-last-chunk reads."""
+    rng = np.random.default_rng(7)
+    Q, S = 2003, 50
+    full = rng.standard_normal((Q, S))
+    path = tmp_path / "c.mat"
+    M.savemat73(str(path), dict(x=np.arange(3.0), sample_log_likelihoods_dla=M.LazyArray(
+        (Q, S), np.float64, src=full, chunk_rows=8)))
+    np.save(tmp_path / "full.npy", full)
+    code = ("import h5py,json,sys,numpy as np; f=h5py.File(sys.argv[1],'r'); d=f['sample_log_likelihoods_dla']; "
+            "a=np.load(sys.argv[2]); print(json.dumps([list(d.shape), list(d.chunks), "
+            "bool(np.array_equal(d[...], a.T)), bool(np.array_equal(d[:, 1234], a[1234])), "
+            "bool(np.array_equal(d[:, 2000:], a[2000:].T))]))")
+    res = subprocess.run([H5PY_PY, "-B", "-c", code, str(path), str(tmp_path / "full.npy")], capture_output=True,
+                         text=True, check=True)
+    assert json.loads(res.stdout.strip().splitlines()[-1]) == [[S, Q], [S, 8], True, True, True]
+
+
 def test_deferred_region_written_in_row_blocks(tmp_path):
     """process.run_process_qsos with world > 1: rank 0 lays out a deferred Q x S region, then every
     rank pwrites its own spectra (rows) of it with write_transposed; uneven blocks, S not a multiple
@@ -167,19 +215,26 @@ def test_h5py_sees_matlab_shapes(tmp_path):
 
 @needs_h5py
 @pytest.mark.skipif(not os.path.isdir(REF_CDDF), reason="reference not present (GPU box)")
-def test_reference_consumer_reads_our_file(tmp_path):
+@pytest.mark.parametrize("layout", ["contiguous", "chunked"])
+def test_reference_consumer_reads_our_file(tmp_path, layout):
     """calc_cddf.py's DLACatalogue loads processed_qsos + dla_samples written here and recovers
     p_dla, z ranges, test_ind and the normalised sample likelihoods (with its own
-    0.95 < sum < 1.05 assert, calc_cddf.py:246)."""
+    0.95 < sum < 1.05 assert, calc_cddf.py:246).  Both layouts of the sample array: contiguous
+    and chunked in blocks of whole rows (what large and sharded saves write), here 4 rows a chunk
+    so the 6 spectra span two chunks, the second one partial."""
     out, samples = _processed_out()
+    sll = out["sample_log_likelihoods_dla"]
+    saved = dict(out)
+    if layout == "chunked":
+        saved["sample_log_likelihoods_dla"] = M.LazyArray(sll.shape, np.float64, src=sll, chunk_rows=4)
     proc = tmp_path / "processed_qsos_dr12q.mat"
     samp = tmp_path / "dla_samples.mat"
     snrs = tmp_path / "snrs_qsos_dr12q.mat"
-    PR.save_processed_qsos(str(proc), out)
+    PR.save_processed_qsos(str(proc), saved)
     PR.save_dla_samples(str(samp), samples)
     Q = out["p_dlas"].size
     M.savemat73(str(snrs), dict(snrs=np.full(Q, 5.0)))
-    res = subprocess.run([H5PY_PY, str(Path(__file__).parent / "cddf_consumer.py"), REF_CDDF, str(proc),
+    res = subprocess.run([H5PY_PY, "-B", str(Path(__file__).parent / "cddf_consumer.py"), REF_CDDF, str(proc),
                           str(samp), str(snrs)], capture_output=True, text=True)
     assert res.returncode == 0, res.stderr[-2000:]
     got = json.loads(res.stdout.strip().splitlines()[-1])

@@ -49,14 +49,14 @@ def warning_compute(model, samples, packed, params, device):
     return out
 
 
-def _worker(rank, world, port, base, q, compute=oracle_compute):
+def _worker(rank, world, port, base, q, compute=oracle_compute, chunk_rows=None):
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        out = PR.run_process_qsos(base, *ARGS, rank=rank, world=world, compute=compute)
+        out = PR.run_process_qsos(base, *ARGS, rank=rank, world=world, compute=compute, chunk_rows=chunk_rows)
         q.put((rank, sorted(out), out.get("numeric_warning")))
     finally:
         dist.barrier()
@@ -70,19 +70,25 @@ def _free_port():
 
 
 @pytest.mark.timeout(600)
-def test_world2_file_equals_single_process(tmp_path):
+@pytest.mark.parametrize("world,chunk_rows", [(2, None), (2, 2), (3, 1)])
+def test_world2_file_equals_single_process(tmp_path, world, chunk_rows):
+    """world ranks (gloo) each decode, evaluate and write their own whole-chunk blocks of the
+    sample array (chunk-block LPT shards: with 2-row chunks the 9 test spectra are 5 blocks, so a
+    rank's blocks need not be adjacent); the file reads back equal to the single-process file."""
     from test_matv73 import write_reference_tree
     single, multi = tmp_path / "single", tmp_path / "multi"
+    Q = 5 if chunk_rows is None else 9
     for d in (single, multi):
-        write_reference_tree(d, Q=5, S=24, k=8)
+        write_reference_tree(d, Q=Q, S=24, k=8)
     PR.run_process_qsos(str(single), *ARGS, compute=oracle_compute)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, str(multi), q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, str(multi), q, oracle_compute, chunk_rows))
+             for r in range(world)]
     for pr in procs:
         pr.start()
-    got = {r: keys for r, keys, _ in (q.get(timeout=500) for _ in range(2))}
+    got = {r: keys for r, keys, _ in (q.get(timeout=500) for _ in range(world))}
     for pr in procs:
         pr.join(timeout=60)
         assert pr.exitcode == 0

@@ -11,7 +11,8 @@ import pytest
 import torch.multiprocessing as mp
 
 from gp_dla_detection_amd import synthetic as syn
-from gp_dla_detection_amd.shard import contiguous_shards, lpt_shards, merge_shards, process_sharded, subset_packed
+from gp_dla_detection_amd.shard import (block_lpt_shards, contiguous_shards, expected_pixels, lpt_shards, merge_shards,
+                                        process_sharded, subset_packed)
 
 
 def _compute(p):
@@ -35,6 +36,38 @@ def test_partitions_cover_exactly_once():
     assert np.array_equal(np.sort(np.concatenate(parts)), np.arange(100))
     loads = [costs[p].sum() for p in parts]
     assert max(loads) - min(loads) <= costs.max()
+
+
+def test_block_lpt_shards_whole_blocks_balanced():
+    """Chunk-aligned shards (run_process_qsos, world > 1): every rank holds whole blocks of
+    consecutive spectra, together exactly once; with DR12Q's count and ~4 MB chunks (56 rows at
+    S = 10^4) the expected-pixel load is balanced to within one block (< 0.3%)."""
+    rng = np.random.default_rng(3)
+    for Q, block, W in ((10, 3, 3), (7, 2, 8), (162861, 56, 8)):
+        costs = expected_pixels(rng.uniform(2.15, 6.0, Q))
+        shards = block_lpt_shards(costs, block, W)
+        allidx = np.sort(np.concatenate(shards))
+        assert np.array_equal(allidx, np.arange(Q))
+        for sh in shards:
+            assert np.all(np.diff(sh) > 0)
+            for b in np.unique(sh // block):    # whole blocks only
+                assert np.array_equal(sh[sh // block == b], np.arange(b * block, min(Q, (b + 1) * block)))
+        if Q > 1000:
+            loads = [costs[sh].sum() for sh in shards]
+            assert max(loads) / np.mean(loads) < 1.003     # LPT: within about one block of the mean
+    assert all(sh.size == 0 for sh in block_lpt_shards(np.zeros(0), 4, 3))
+
+
+def test_expected_pixels_matches_synthetic_spectra():
+    """The sweep-cost proxy against the in-range pixel count of DR12Q-shaped synthetic spectra
+    (BOSS 3600 A blue edge): within 2 pixels."""
+    model = syn.make_model(k=4, seed=1)
+    sp = syn.make_dr12q_like_spectra(model, 40, seed=5, mask_fraction=0.0)
+    from gp_dla_detection_amd import parameters as P
+    n = [int(np.sum((s["wavelengths"] / (1 + s["z_qso"]) >= P.MIN_LAMBDA)
+                    & (s["wavelengths"] / (1 + s["z_qso"]) <= P.MAX_LAMBDA))) for s in sp]
+    est = expected_pixels([s["z_qso"] for s in sp])
+    assert np.max(np.abs(est - np.array(n))) <= 2
 
 
 def test_subset_and_merge_roundtrip():
