@@ -81,6 +81,7 @@ SIGNATURES = {
     "gpdla_engine_synchronize": (C.c_int, [C.c_void_p]),
     "gpdla_engine_set_stream": (C.c_int, [C.c_void_p, C.c_void_p]),
     "gpdla_engine_get_stats": (C.c_int, [C.c_void_p, C.POINTER(Stats)]),
+    "gpdla_engine_get_stats_n": (C.c_int, [C.c_void_p, C.POINTER(Stats), C.c_int64]),
     "gpdla_engine_reset_stats": (C.c_int, [C.c_void_p]),
     "gpdla_engine_destroy": (None, [C.c_void_p]),
     "gpdla_voigt_f64": (C.c_int, [dp, C.c_int64, C.c_double, C.c_double, C.c_int32, dp]),

@@ -208,7 +208,7 @@ int upload(void* dst, const void* src, size_t bytes, hipStream_t s) {
 
 extern "C" {
 
-int32_t gpdla_version(void) { return 1; }
+int32_t gpdla_version(void) { return GPDLA_ABI_VERSION; }
 
 int32_t gpdla_device_count(void) {
   int c = 0;
@@ -457,11 +457,10 @@ int gpdla_engine_process(gpdla_engine* e, const gpdla_spectra* sp, const gpdla_r
   // full + a 1,697-sample tail that fills a sixth of the GPU), 47.4 with 7 equal chunks, 48.5 with
   // 2 and 49.1 with one (profiles/r2l); again after the round-2 GEMM work: 53.5 (6 equal chunks),
   // 58.8 (4), 61.7 (2), 63.1 (one; profiles/r2/c5_ab): smaller chunks keep the A digits in the
-  // Infinity Cache (GEMM -10%) but cost more in the weights and LDL^T launches.  The workspaces (A
-  // digits 8 B, Gram 8 k(k+1)/2 B per sample and slot / entry) stay a few GB in 288 GB of HBM.
+  // Infinity Cache (GEMM -10%) but cost more in the weights and LDL^T launches.  The chunk is also
+  // capped per batch by a workspace budget (panel_chunk below): per sample, the A digits (8 B per
+  // slot) or the fp64 weights (16 B per slot), plus the Gram and u (8 (k(k+1)/2 + k) B).
   constexpr int64_t kMaxChunk = 131072;
-  const int64_t nchunk = (e->S + 1 + kMaxChunk - 1) / kMaxChunk;
-  const int64_t sc_max = (e->S + 1 + nchunk - 1) / nchunk;
   const int64_t blocks_x = (e->S + 1 + kSamplesPerBlock - 1) / kSamplesPerBlock;
 
   // pinned metadata for every batch of this call: per batch (QB+1) + 4*QB int64
@@ -506,6 +505,25 @@ int gpdla_engine_process(gpdla_engine* e, const gpdla_spectra* sp, const gpdla_r
     }
     h_off[nq] = sp->offsets[q1] - sp->offsets[q0];
     const int64_t npix = h_off[nq];
+    // int8 contraction for this batch: its int32 level sums are exact only up to kI8MaxSlots
+    // slots, so a batch holding a longer spectrum runs the fp64 kernels (fused or dgemm) instead
+    const bool i8_exact = lpix_max <= kI8MaxSlots;
+    const bool batch_i8 = e->i8 && !e->gemm && i8_exact;
+    const bool batch_gemm_i8 = e->i8 && e->gemm && i8_exact;
+    // panel-GEMM sample chunk of this batch: equal chunks of at most kMaxChunk samples whose
+    // workspaces fit the budget (a quarter of the free device memory, at most 16 GiB)
+    int64_t sc_max = 0;
+    if (e->gemm) {
+      size_t free_b = 0, total_b = 0;
+      HIP_TRY(hipMemGetInfo(&free_b, &total_b));
+      const int64_t budget = (int64_t)std::min<size_t>(free_b / 4, (size_t)16 << 30);
+      const int64_t per_sample = (batch_gemm_i8 ? 8 * i8_gemm_kstride(cap_max) : 16 * cap_max) +
+                                 8 * (E + e->K + 2 * kWeightParts);
+      const int64_t fit = std::max<int64_t>(128, budget / std::max<int64_t>(per_sample, 1) / 128 * 128);
+      const int64_t cmax = std::min<int64_t>(kMaxChunk, fit);
+      const int64_t nchunk = (e->S + 1 + cmax - 1) / cmax;
+      sc_max = (e->S + 1 + nchunk - 1) / nchunk;
+    }
 
     int rc;
     if ((rc = grow(&e->d_meta, &e->cap_meta, per_batch))) return rc;
@@ -517,18 +535,17 @@ int gpdla_engine_process(gpdla_engine* e, const gpdla_spectra* sp, const gpdla_r
     if (e->gemm) {
       if ((rc = grow(&e->d_pm, &e->cap_pm, (size_t)slots * e->K))) return rc;
       if ((rc = grow(&e->d_srow, &e->cap_srow, (size_t)slots * 8))) return rc;
-      if ((rc = grow(&e->d_wg, &e->cap_wg, (size_t)(cap_max * sc_max)))) return rc;
-      if ((rc = grow(&e->d_wu, &e->cap_wu, (size_t)(cap_max * sc_max)))) return rc;
-      if ((rc = grow(&e->d_G, &e->cap_G, (size_t)(E * sc_max)))) return rc;
-      if ((rc = grow(&e->d_U, &e->cap_U, (size_t)(e->K * sc_max)))) return rc;
+      if (!batch_gemm_i8) {  // the fp64 weights: only the dgemm path reads them
+        if ((rc = grow(&e->d_wg, &e->cap_wg, (size_t)(cap_max * sc_max)))) return rc;
+        if ((rc = grow(&e->d_wu, &e->cap_wu, (size_t)(cap_max * sc_max)))) return rc;
+      }
+      // + 8 elements of slack: ldl_mfma_kernel's straight-line tile loads may address one element
+      // past the last sample's Gram when k is a multiple of 4 (the value is discarded)
+      if ((rc = grow(&e->d_G, &e->cap_G, (size_t)(E * sc_max + 8)))) return rc;
+      if ((rc = grow(&e->d_U, &e->cap_U, (size_t)(e->K * sc_max + 8)))) return rc;
       if ((rc = grow(&e->d_q1p, &e->cap_q1p, (size_t)(kWeightParts * sc_max)))) return rc;
       if ((rc = grow(&e->d_ldp, &e->cap_ldp, (size_t)(kWeightParts * sc_max)))) return rc;
     }
-    // int8 contraction for this batch: its int32 level sums are exact only up to kI8MaxSlots
-    // slots, so a batch holding a longer spectrum runs the fp64 kernels (fused or dgemm) instead
-    const bool i8_exact = lpix_max <= kI8MaxSlots;
-    const bool batch_i8 = e->i8 && !e->gemm && i8_exact;
-    const bool batch_gemm_i8 = e->i8 && e->gemm && i8_exact;
     if (batch_gemm_i8) {
       if ((rc = grow(&e->d_pi8, &e->cap_pi8, (size_t)chunks))) return rc;
       if ((rc = grow(&e->d_pent, &e->cap_pent, (size_t)nq * 2 * i8_gemm_entries(e->K)))) return rc;
@@ -708,14 +725,18 @@ int gpdla_engine_synchronize(gpdla_engine* e) {
   return GPDLA_OK;
 }
 
-int gpdla_engine_get_stats(gpdla_engine* e, gpdla_stats* s) {
-  if (!e || !s) return set_error(GPDLA_EINVAL, "null argument");
+int gpdla_engine_get_stats_n(gpdla_engine* e, gpdla_stats* s, int64_t stats_bytes) {
+  if (!e || !s || stats_bytes < 0) return set_error(GPDLA_EINVAL, "null argument");
   HIP_TRY(hipSetDevice(e->device));
   HIP_TRY(hipStreamSynchronize(e->stream));
   int rc = resolve_events(e);
   if (rc) return rc;
-  *s = e->stats;
+  std::memcpy(s, &e->stats, std::min<size_t>((size_t)stats_bytes, sizeof(gpdla_stats)));
   return GPDLA_OK;
+}
+
+int gpdla_engine_get_stats(gpdla_engine* e, gpdla_stats* s) {
+  return gpdla_engine_get_stats_n(e, s, (int64_t)sizeof(gpdla_stats));
 }
 
 int gpdla_engine_reset_stats(gpdla_engine* e) {

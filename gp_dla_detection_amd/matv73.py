@@ -1126,6 +1126,11 @@ def update_variable(path: str, name: str, value) -> bool:
         n = math.prod(dims) if dims else 1
         if addr == UNDEF or val.size != n or size != n * dt.itemsize:
             return False
+        # the MATLAB shape must match the stored one (a 1-D value is a Q x 1 column, like savemat73's
+        # vectors): a same-size value of another shape would land in the wrong column-major order
+        mshape = val.shape if val.ndim >= 2 else ((val.size, 1) if val.ndim == 1 else (1, 1))
+        if tuple(int(d) for d in reversed(mshape)) != tuple(int(d) for d in dims):
+            return False
         conv = val.astype(dt.newbyteorder("="))
         if not np.array_equal(conv, val):         # would not survive the class conversion
             return False

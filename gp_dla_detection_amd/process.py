@@ -15,6 +15,8 @@ the GPU (libgpdla.so); priors and posteriors are O(Q) host bookkeeping (process_
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 
 from . import parameters as P
@@ -315,6 +317,11 @@ def run_process_qsos(base_directory: str, training_release: str, training_set_na
     samples = load_dla_samples(f"{tdir}/dla_samples.mat")
     params = params or set_parameters(k=np.asarray(model["M"]).shape[1])
     catalog = loadmat(f"{rdir}/catalog.mat")
+    side = f"{rdir}/catalog_filter_flags.mat"
+    if os.path.exists(side):
+        # preload_qsos's filter_flags when catalog.mat could not take them in place (ingest.py:
+        # a catalog holding MATLAB objects is never rewritten): the sidecar supersedes the stale copy
+        catalog["filter_flags"] = loadmat(side)["filter_flags"]
     tind = evaluate_index(test_ind, catalog=catalog).astype(bool).ravel()
     tidx = np.flatnonzero(tind)
     z_all = np.asarray(catalog["z_qsos"], dtype=np.float64).ravel()[tidx]

@@ -41,6 +41,11 @@ extern "C" {
 #define GPDLA_ENOMEM (-3)
 #define GPDLA_EUNSUPPORTED (-4)
 
+/* ABI version (gpdla_version()).  2: gpdla_stats gained contraction_ms / contraction_launches
+ * (its size changed: a caller compiled against a version-1 header must use gpdla_engine_get_stats_n
+ * with its own sizeof(gpdla_stats), or be rebuilt). */
+#define GPDLA_ABI_VERSION 2
+
 #define GPDLA_MEM_HOST 0
 #define GPDLA_MEM_DEVICE 1
 
@@ -49,19 +54,20 @@ extern "C" {
 #define GPDLA_ABSORPTION_UNMASKED 1  /* pair every unmasked pixel with its own profile value */
 /* Likelihood path.  AUTO = the fused single-kernel sweep for ranks 1..24 (compiled for 4 8 10 12 16
  * 20 24; a rank in between runs on the next compiled one with M padded by zero columns, which is
- * exact: pivots 1, zero updates), otherwise the panel-GEMM path (weights kernel + dgemm + batched
- * LDL^T), which takes any rank 1..64 (BASELINE configs[4]: k = 50). */
+ * exact: pivots 1, zero updates), otherwise the panel-GEMM path (weights kernel + fp64 Gram/u GEMM +
+ * batched LDL^T), which takes any rank 1..64 (BASELINE configs[4]: k = 50). */
 #define GPDLA_PATH_AUTO 0
 #define GPDLA_PATH_FUSED 1
 #define GPDLA_PATH_PANEL_GEMM 2
-/* Fused sweep with the Gram/u contraction on the int8 matrix cores (Ozaki digit slicing, exact
- * integer accumulation, fp64 everywhere else); k <= 20 (compiled for 20, lower ranks zero-padded) with
- * num_lines = 3.  Spectra with more than
- * 30,000 pixels fall back to the fp64 fused kernel.  Agrees with the fp64 path to ~1e-10 relative. */
+/* Fused sweep with the Gram/u contraction on the int8 matrix cores (Ozaki digit slicing: 32-bit
+ * quantised operands, exact integer accumulation, fp64 everywhere else); k <= 20 (compiled for 20,
+ * lower ranks zero-padded) with num_lines = 3.  Spectra with more than 30,000 pixels fall back to the
+ * fp64 fused kernel.  Agrees with the fp64 path to <= 4e-9 relative on the log-likelihoods (measured
+ * 3.8e-9 at BASELINE configs[1]; tests assert 1e-8). */
 #define GPDLA_PATH_FUSED_I8 3
 /* Panel-GEMM path with the Gram/u GEMMs on the int8 matrix cores (same Ozaki scheme as
  * GPDLA_PATH_FUSED_I8), any rank 1..64 with num_lines = 3; for BASELINE configs[4] (k = 50, quoted in
- * fp32) it agrees with fp64 to ~1e-9 relative, far inside fp32's ~5e-6. */
+ * fp32) it agrees with fp64 to <= 4e-9 relative (tests assert 1e-8), far inside fp32's ~5e-6. */
 #define GPDLA_PATH_PANEL_GEMM_I8 4
 /* GPDLA_PATH_PANEL_GEMM_I8 with a 24-bit Gram contraction: 3 digit planes per operand and the 6 digit
  * pairs of level <= 2 for the k(k+1)/2 Gram entries (instead of 4 planes and 10 pairs: 40% fewer
@@ -151,6 +157,8 @@ int gpdla_engine_synchronize(gpdla_engine* engine);
  * is ordered on that stream. */
 int gpdla_engine_set_stream(gpdla_engine* engine, void* hip_stream);
 int gpdla_engine_get_stats(gpdla_engine* engine, gpdla_stats* stats);
+/* The same, writing at most stats_bytes bytes (a caller's sizeof(gpdla_stats) from an older header). */
+int gpdla_engine_get_stats_n(gpdla_engine* engine, gpdla_stats* stats, int64_t stats_bytes);
 int gpdla_engine_reset_stats(gpdla_engine* engine);
 void gpdla_engine_destroy(gpdla_engine* engine);
 

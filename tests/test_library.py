@@ -26,7 +26,7 @@ def test_library_exports_every_declared_symbol():
     for name in names:
         assert hasattr(lib, name), name
         assert name in L.SIGNATURES, f"{name} missing from the ctypes binding"
-    assert lib.gpdla_version() >= 1
+    assert lib.gpdla_version() == 2      # GPDLA_ABI_VERSION: gpdla_stats grew in version 2
 
 
 def test_faddeeva_host_matches_scipy():

@@ -326,3 +326,33 @@ def test_reference_tree_loaders(tmp_path):
     assert len(sp) == len(spectra)
     for a, b in zip(sp, spectra):
         assert np.array_equal(a["flux"], b["flux"]) and np.array_equal(a["pixel_mask"], b["pixel_mask"])
+
+
+def test_update_variable_requires_matching_shape(tmp_path):
+    """save(..., '-append') in place only for the stored MATLAB shape: a same-size value of another
+    shape would be written in the wrong column-major order, so it is refused (file untouched)."""
+    path = str(tmp_path / "u.mat")
+    M.savemat73(path, dict(flags=np.zeros(6, np.uint8), grid=np.zeros((2, 3))))
+    before = Path(path).read_bytes()
+    assert not M.update_variable(path, "grid", np.ones((3, 2)))
+    assert not M.update_variable(path, "flags", np.ones((2, 3), np.uint8))
+    assert Path(path).read_bytes() == before
+    assert M.update_variable(path, "grid", np.arange(6.0).reshape(2, 3))
+    assert M.update_variable(path, "flags", np.arange(6, dtype=np.uint8))        # Q and Q x 1 alike
+    r = M.loadmat73(path)
+    assert np.array_equal(r["grid"], np.arange(6.0).reshape(2, 3))
+    assert np.array_equal(r["flags"][:, 0], np.arange(6))
+
+
+def test_run_process_qsos_reads_sidecar_filter_flags(tmp_path):
+    """When preload_qsos's filter_flags could not go into catalog.mat (ingest.py sidecar), the
+    driver's test_ind '(catalog.filter_flags == 0)' uses the sidecar's flags, not the stale ones."""
+    from test_process_sharded import ARGS, oracle_compute
+    write_reference_tree(tmp_path, Q=4, S=8, k=8)
+    d = tmp_path / "dr12q" / "processed"
+    flags = np.ravel(M.loadmat73(str(d / "catalog.mat"))["filter_flags"]).copy()
+    flags[1] = 16                                       # preload_qsos.m:47: too few pixels
+    M.savemat73(str(d / "catalog_filter_flags.mat"), {"filter_flags": flags.reshape(-1, 1)})
+    out = PR.run_process_qsos(str(tmp_path), *ARGS, compute=oracle_compute, save=False)
+    assert out["test_ind"].sum() == 3 and not out["test_ind"][1]
+    assert out["log_likelihoods_dla"].size == 3
