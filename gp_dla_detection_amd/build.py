@@ -33,5 +33,31 @@ def build(verbose: bool = False, force: bool = False, out: Path | None = None,
     return OUT_
 
 
+MEX_API = PKG.parent / "tests" / "support" / "mex_api"
+
+
+def build_mex_mocks(verbose: bool = False) -> list[Path]:
+    """Test support: each MATLAB gateway in matlab/ linked with the in-process MEX runtime of
+    tests/support/mex_api/mex_mock.c into tests/support/mex_api/lib<gateway>_mock.so, so the tests
+    drive the gateways' own code against libgpdla (no MATLAB here).  Host C only (gcc)."""
+    import shutil
+    cc = shutil.which("gcc") or shutil.which("cc")
+    outs = []
+    if not cc or not (PKG.parent / "matlab").is_dir():
+        return outs
+    for src in sorted((PKG.parent / "matlab").glob("*.c")):
+        out = MEX_API / f"lib{src.stem}_mock.so"
+        deps = [src, MEX_API / "mex_mock.c", MEX_API / "mex.h", PKG.parent / "include" / "gpdla.h"]
+        if not (out.exists() and all(out.stat().st_mtime >= d.stat().st_mtime for d in deps)):
+            cmd = [cc, "-std=c99", "-O1", "-Wall", "-fPIC", "-shared", f"-I{MEX_API}", f"-I{PKG.parent / 'include'}",
+                   str(src), str(MEX_API / "mex_mock.c"), f"-L{PKG}", "-lgpdla",
+                   "-Wl,-rpath,$ORIGIN/../../../gp_dla_detection_amd", "-o", str(out)]
+            if verbose:
+                print(" ".join(cmd), file=sys.stderr)
+            subprocess.run(cmd, check=True)
+        outs.append(out)
+    return outs
+
+
 if __name__ == "__main__":
     print(build(verbose=True, force="--force" in sys.argv))
