@@ -8,7 +8,8 @@ from pathlib import Path
 
 PKG = Path(__file__).resolve().parent
 CSRC = PKG / "csrc"
-SOURCES = ["kernels.hip", "kernels_i8.hip", "gemm_path.hip", "gemm_i8.hip", "engine.hip", "objective.hip", "faddeeva_host.cpp"]
+SOURCES = ["kernels.hip", "kernels_i8.hip", "gemm_path.hip", "gemm_i8.hip", "gemm_f64.hip", "engine.hip", "objective.hip",
+           "faddeeva_host.cpp"]
 OUT = PKG / "libgpdla.so"
 
 
@@ -23,7 +24,7 @@ def build(verbose: bool = False, force: bool = False, out: Path | None = None,
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     cmd = [hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
            "-Wno-unused-result", "-o", str(OUT_)] + [f"-D{k}={v}" for k, v in (defines or {}).items()] \
-        + [str(s) for s in srcs] + ["-lrocblas"]
+        + [str(s) for s in srcs]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     tmp = OUT_.with_suffix(".so.tmp")

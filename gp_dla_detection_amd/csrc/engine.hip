@@ -1,7 +1,6 @@
 // C-ABI of libgpdla.so (include/gpdla.h): engine lifecycle, device workspaces, batching,
 // kernel-time accounting and the standalone voigt / log_mvnpdf_low_rank entry points.
 #include <hip/hip_runtime.h>
-#include <rocblas/rocblas.h>
 
 #include <algorithm>
 #include <cmath>
@@ -102,10 +101,9 @@ struct gpdla_engine {
   int device = 0;
   int K = 0;
   int64_t S = 0;
-  bool gemm = false;                 // panel-GEMM path (gemm_path.hip + rocBLAS) instead of fused
+  bool gemm = false;                 // panel-GEMM path (gemm_path.hip + gemm_f64 / gemm_i8) instead of fused
   bool i8 = false;                   // fused path with the int8 Ozaki contraction (kernels_i8.hip)
   int i8_nd = 4;                     // int8 panel-GEMM digit planes: 4 (levels <= 3) or 3 (_I8_24)
-  rocblas_handle blas = nullptr;
   gpdla_params params{};
   hipStream_t own_stream = nullptr;
   hipStream_t stream = nullptr;
@@ -240,7 +238,6 @@ void gpdla_engine_destroy(gpdla_engine* e) {
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (e->h_meta) (void)hipHostFree(e->h_meta);
-  if (e->blas) (void)rocblas_destroy_handle(e->blas);
   if (e->meta_done) (void)hipEventDestroy(e->meta_done);
 
   if (e->own_stream) (void)hipStreamDestroy(e->own_stream);
@@ -299,8 +296,6 @@ int gpdla_engine_create(int32_t device, const gpdla_model* model, const gpdla_sa
   e->stream = e->own_stream;
   if (hipEventCreateWithFlags(&e->meta_done, hipEventDisableTiming) != hipSuccess)
     return fail(set_error(GPDLA_EDEVICE, "hipEventCreate failed"));
-  if (e->gemm && rocblas_create_handle(&e->blas) != rocblas_status_success)
-    return fail(set_error(GPDLA_EDEVICE, "rocblas_create_handle failed"));
 
 
   const size_t G = model->num_rest, K = e->K, k_model = model->k;
@@ -356,8 +351,9 @@ int gpdla_engine_set_stream(gpdla_engine* e, void* hip_stream) {
   return GPDLA_OK;
 }
 
-// Panel-GEMM path for one batch: per spectrum and chunk of samples, weights -> GEMM (int8 digits
-// on the matrix cores, or two rocBLAS dgemm) -> batched LDL^T (gemm_path.hip), in stream order.
+// Panel-GEMM path for one batch: per spectrum and chunk of samples, weights -> GEMM on the matrix
+// cores (int8 digits, gemm_i8.hip, or fp64, gemm_f64.hip) -> batched LDL^T (gemm_path.hip), in
+// stream order.
 // (Second streams measured no gain and were removed: the LDL^T beside the next chunk's weights and
 // GEMM +5% with round 1's VALU LDL^T, 0% with the matrix-core one (profiles/r2f); the weights kernel
 // beside the previous chunk's GEMM and LDL^T, double-buffered, +0.5% (round 2, profiles/r2c).)
@@ -366,9 +362,6 @@ static int run_panel_gemm(gpdla_engine* e, bool i8, int64_t nq, const int64_t* h
                           int64_t ld, double* o_null, hipStream_t st) {
   const int K = e->K;
   const int64_t E = (int64_t)K * (K + 1) / 2;
-  if (rocblas_set_stream(e->blas, st) != rocblas_status_success)
-    return set_error(GPDLA_EDEVICE, "rocblas_set_stream failed");
-  const double one = 1.0, zero = 0.0;
   double *G = e->d_G, *U = e->d_U, *q1p = e->d_q1p, *ldp = e->d_ldp;
   const int64_t rows = (sc_max + 127) / 128 * 128;
   for (int64_t q = 0; q < nq; ++q) {
@@ -404,17 +397,19 @@ static int run_panel_gemm(gpdla_engine* e, bool i8, int64_t nq, const int64_t* h
         wa.num_lines = e->params.num_lines; wa.lines = make_line_args(e->d_lines);
         wa.wg = e->d_wg; wa.wu = e->d_wu; wa.q1p = q1p; wa.ldp = ldp;
         HIP_TRY(launch_weights(wa, st));
-        // Gram (E x sc) = PG (E x cap, the slot-major Khatri-Rao rows) * Wg^T (Wg stored [cap][sc])
-        rocblas_status bs = rocblas_dgemm(e->blas, rocblas_operation_none, rocblas_operation_transpose,
-                                          (rocblas_int)E, sc, (rocblas_int)h_cap[q], &one,
-                                          e->d_panel + h_sb[q] * E, (rocblas_int)E, e->d_wg, sc, &zero,
-                                          G, (rocblas_int)E);
-        if (bs == rocblas_status_success)
-          bs = rocblas_dgemm(e->blas, rocblas_operation_none, rocblas_operation_transpose, K, sc,
-                             (rocblas_int)h_cap[q], &one, e->d_pm + h_sb[q] * K, K, e->d_wu, sc, &zero,
-                             U, K);
-        if (bs != rocblas_status_success)
-          return set_error(GPDLA_EDEVICE, "rocblas_dgemm failed: %s", rocblas_status_to_string(bs));
+        // Gram[s][e] = sum_t Wg[t][s] PG[t][e] (the slot-major Khatri-Rao rows), u[s][i] likewise
+        // over the M rows, on the f64 matrix cores (gemm_f64.hip)
+        GemmF64Args ga{};
+        ga.W = e->d_wg; ga.P = e->d_panel + h_sb[q] * E; ga.ldp = E; ga.nent = (int32_t)E;
+        ga.cap = h_cap[q]; ga.cap16 = gemm_f64_cap16(h_cap[q]); ga.sc = sc; ga.C = G;
+        TimedLaunch tg{};
+        int rc;
+        if ((rc = record_start(e, &tg, 3))) return rc;
+        HIP_TRY(launch_gemm_f64(ga, st));
+        ga.W = e->d_wu; ga.P = e->d_pm + h_sb[q] * K; ga.ldp = K; ga.nent = K; ga.C = U;
+        HIP_TRY(launch_gemm_f64(ga, st));
+        HIP_TRY(hipEventRecord(tg.stop, st));
+        e->pending.push_back(tg);
       }
       LdlArgs da{};
       da.info = e->d_info; da.q = (int32_t)q; da.k = K;
@@ -517,7 +512,7 @@ int gpdla_engine_process(gpdla_engine* e, const gpdla_spectra* sp, const gpdla_r
       size_t free_b = 0, total_b = 0;
       HIP_TRY(hipMemGetInfo(&free_b, &total_b));
       const int64_t budget = (int64_t)std::min<size_t>(free_b / 4, (size_t)16 << 30);
-      const int64_t per_sample = (batch_gemm_i8 ? 8 * i8_gemm_kstride(cap_max) : 16 * cap_max) +
+      const int64_t per_sample = (batch_gemm_i8 ? 8 * i8_gemm_kstride(cap_max) : 16 * gemm_f64_cap16(cap_max)) +
                                  8 * (E + e->K + 2 * kWeightParts);
       const int64_t fit = std::max<int64_t>(128, budget / std::max<int64_t>(per_sample, 1) / 128 * 128);
       const int64_t cmax = std::min<int64_t>(kMaxChunk, fit);
@@ -535,9 +530,10 @@ int gpdla_engine_process(gpdla_engine* e, const gpdla_spectra* sp, const gpdla_r
     if (e->gemm) {
       if ((rc = grow(&e->d_pm, &e->cap_pm, (size_t)slots * e->K))) return rc;
       if ((rc = grow(&e->d_srow, &e->cap_srow, (size_t)slots * 8))) return rc;
-      if (!batch_gemm_i8) {  // the fp64 weights: only the dgemm path reads them
-        if ((rc = grow(&e->d_wg, &e->cap_wg, (size_t)(cap_max * sc_max)))) return rc;
-        if ((rc = grow(&e->d_wu, &e->cap_wu, (size_t)(cap_max * sc_max)))) return rc;
+      if (!batch_gemm_i8) {  // the fp64 weight tiles: only the fp64 GEMM reads them
+        const size_t wbytes = (size_t)(gemm_f64_cap16(cap_max) * gemm_f64_rows(sc_max));
+        if ((rc = grow(&e->d_wg, &e->cap_wg, wbytes))) return rc;
+        if ((rc = grow(&e->d_wu, &e->cap_wu, wbytes))) return rc;
       }
       // + 8 elements of slack: ldl_mfma_kernel's straight-line tile loads may address one element
       // past the last sample's Gram when k is a multiple of 4 (the value is discarded)
@@ -807,13 +803,17 @@ static int lines_on_device(double** d_lines) {
   return GPDLA_OK;
 }
 
-// Device buffers of the standalone entry points, cached per device and grown on demand: the MEX
-// drop-ins are called once per sample from a MATLAB loop, so allocating and
-// freeing device memory per call would dominate them.  Calls are serialised per device.
+// Device and pinned host buffers of the standalone entry points, cached per device and grown on
+// demand, plus a non-blocking stream: the MEX drop-ins are called once per
+// sample from a MATLAB loop, so a call is one memcpy into pinned memory, one H2D copy, the kernel,
+// one D2H copy and a stream synchronisation -- no allocation, no pageable copies, no memset.
+// Calls are serialised per device.
 struct StandaloneBufs {
   std::mutex mu;
-  char* buf = nullptr;
-  size_t cap = 0;
+  char* buf = nullptr;    // device
+  char* host = nullptr;   // pinned host staging
+  size_t cap = 0, hcap = 0;
+  hipStream_t stream = nullptr;
 };
 
 static StandaloneBufs& standalone_bufs(int dev) {
@@ -825,13 +825,23 @@ static StandaloneBufs& standalone_bufs(int dev) {
   return *per_dev[dev];
 }
 
-static hipError_t standalone_reserve(StandaloneBufs& b, size_t bytes) {
-  if (bytes <= b.cap && b.buf) return hipSuccess;
-  if (b.buf) (void)hipFree(b.buf);
-  b.buf = nullptr;
-  b.cap = 0;
-  hipError_t e = hipMalloc((void**)&b.buf, bytes);
-  if (e == hipSuccess) b.cap = bytes;
+static hipError_t standalone_reserve(StandaloneBufs& b, size_t bytes, size_t host_bytes) {
+  hipError_t e = hipSuccess;
+  if (!b.stream) e = hipStreamCreateWithFlags(&b.stream, hipStreamNonBlocking);
+  if (e == hipSuccess && (bytes > b.cap || !b.buf)) {
+    if (b.buf) (void)hipFree(b.buf);
+    b.buf = nullptr;
+    b.cap = 0;
+    e = hipMalloc((void**)&b.buf, bytes);
+    if (e == hipSuccess) b.cap = bytes;
+  }
+  if (e == hipSuccess && (host_bytes > b.hcap || !b.host)) {
+    if (b.host) (void)hipHostFree(b.host);
+    b.host = nullptr;
+    b.hcap = 0;
+    e = hipHostMalloc((void**)&b.host, host_bytes);
+    if (e == hipSuccess) b.hcap = host_bytes;
+  }
   return e;
 }
 
@@ -850,18 +860,24 @@ int gpdla_voigt_batch_f64(const double* lambdas, int64_t n_padded, const double*
   StandaloneBufs& sb = standalone_bufs(dev);
   std::lock_guard<std::mutex> lock(sb.mu);
   const int64_t n_out = n_padded - 2 * kWidth;
-  const size_t bytes = (size_t)(n_padded + 2 * count + count * n_out) * 8;
-  hipError_t err = standalone_reserve(sb, bytes);
+  const size_t n_in = (size_t)(n_padded + 2 * count);          // [lambdas | z | N]
+  const size_t bytes = (n_in + (size_t)count * n_out) * 8;
+  hipError_t err = standalone_reserve(sb, bytes, bytes);
+  if (err != hipSuccess) return set_error(GPDLA_EDEVICE, "voigt: %s", hipGetErrorString(err));
+  double* h = (double*)sb.host;
+  std::memcpy(h, lambdas, n_padded * 8);
+  std::memcpy(h + n_padded, z, count * 8);
+  std::memcpy(h + n_padded + count, N, count * 8);
   double* d_lam = (double*)sb.buf;
   double* d_z = d_lam + n_padded;
   double* d_N = d_z + count;
   double* d_out = d_N + count;
-  if (err == hipSuccess) err = hipMemcpy(d_lam, lambdas, n_padded * 8, hipMemcpyHostToDevice);
-  if (err == hipSuccess) err = hipMemcpy(d_z, z, count * 8, hipMemcpyHostToDevice);
-  if (err == hipSuccess) err = hipMemcpy(d_N, N, count * 8, hipMemcpyHostToDevice);
-  if (err == hipSuccess) err = launch_voigt_batch(d_lam, n_padded, d_z, d_N, count, num_lines, make_line_args(d_lines), d_out, nullptr);
-  if (err == hipSuccess) err = hipMemcpy(out, d_out, count * n_out * 8, hipMemcpyDeviceToHost);
+  err = hipMemcpyAsync(d_lam, h, n_in * 8, hipMemcpyHostToDevice, sb.stream);
+  if (err == hipSuccess) err = launch_voigt_batch(d_lam, n_padded, d_z, d_N, count, num_lines, make_line_args(d_lines), d_out, sb.stream);
+  if (err == hipSuccess) err = hipMemcpyAsync(h + n_in, d_out, count * n_out * 8, hipMemcpyDeviceToHost, sb.stream);
+  if (err == hipSuccess) err = hipStreamSynchronize(sb.stream);
   if (err != hipSuccess) return set_error(GPDLA_EDEVICE, "voigt: %s", hipGetErrorString(err));
+  std::memcpy(out, h + n_in, count * n_out * 8);
   return GPDLA_OK;
 }
 
@@ -882,28 +898,28 @@ int gpdla_log_mvnpdf_low_rank_f64(const double* y, const double* mu, const doubl
   StandaloneBufs& sb = standalone_bufs(dev);
   std::lock_guard<std::mutex> lock(sb.mu);
   // one staging copy: [y | mu | d | M | out | status]
-  const size_t nd = (size_t)n * (3 + k) + 2;
-  hipError_t err = standalone_reserve(sb, nd * 8);
+  const size_t nin = (size_t)n * (3 + k);
+  hipError_t err = standalone_reserve(sb, (nin + 2) * 8, (nin + 2) * 8);
+  if (err != hipSuccess) return set_error(GPDLA_EDEVICE, "log_mvnpdf_low_rank: %s", hipGetErrorString(err));
+  double* h = (double*)sb.host;
+  std::memcpy(h, y, n * 8);
+  std::memcpy(h + n, mu, n * 8);
+  std::memcpy(h + 2 * n, d, n * 8);
+  std::memcpy(h + 3 * n, M, (size_t)n * k * 8);
   double* dy = (double*)sb.buf;
   double* dmu = dy + n;
   double* dd = dmu + n;
   double* dM = dd + n;
-  double* dout = dM + (size_t)n * k;
+  double* dout = dy + nin;
   int32_t* dst = (int32_t*)(dout + 1);
-  std::vector<double> host(nd - 2);
-  std::memcpy(host.data(), y, n * 8);
-  std::memcpy(host.data() + n, mu, n * 8);
-  std::memcpy(host.data() + 2 * n, d, n * 8);
-  std::memcpy(host.data() + 3 * n, M, (size_t)n * k * 8);
-  if (err == hipSuccess) err = hipMemcpy(dy, host.data(), (nd - 2) * 8, hipMemcpyHostToDevice);
-  if (err == hipSuccess) err = hipMemset(dst, 0, 4);
-  if (err == hipSuccess) err = launch_mvn_single(dy, dmu, dM, dd, n, k, dout, dst, nullptr);
-  double res[2] = {0, 0};
-  if (err == hipSuccess) err = hipMemcpy(res, dout, 16, hipMemcpyDeviceToHost);
+  err = hipMemcpyAsync(dy, h, nin * 8, hipMemcpyHostToDevice, sb.stream);
+  if (err == hipSuccess) err = launch_mvn_single(dy, dmu, dM, dd, n, k, dout, dst, sb.stream);
+  if (err == hipSuccess) err = hipMemcpyAsync(h + nin, dout, 16, hipMemcpyDeviceToHost, sb.stream);
+  if (err == hipSuccess) err = hipStreamSynchronize(sb.stream);
   if (err != hipSuccess) return set_error(GPDLA_EDEVICE, "log_mvnpdf_low_rank: %s", hipGetErrorString(err));
-  *out = res[0];
+  *out = h[nin];
   int32_t status = 0;
-  std::memcpy(&status, &res[1], 4);
+  std::memcpy(&status, h + nin + 1, 4);
   if (status) return set_error(GPDLA_ENUMERIC, "B = I + M'D^-1M is not positive definite");
   return GPDLA_OK;
 }

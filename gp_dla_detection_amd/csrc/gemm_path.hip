@@ -2,8 +2,9 @@
 // "MFMA for the n x k panel contraction" branch.  Per (spectrum, chunk of samples):
 //   weights_kernel    Voigt absorption x pixel terms (process_qsos.m:186-197) ->
 //                     Wg[slot][s] = a^2/d, Wu[slot][s] = a r/d, per-segment sum r^2/d, sum log d
-//   rocBLAS dgemm x2  Gram[s] = PG^T Wg[:, s] (Khatri-Rao panel, k(k+1)/2 columns) and
-//                     u[s] = M^T Wu[:, s]  (engine.hip)  -- log_mvnpdf_low_rank.m:13-23
+//   gemm_f64_kernel   Gram[s] = PG^T Wg[:, s] (Khatri-Rao panel, k(k+1)/2 columns) and
+//                     u[s] = M^T Wu[:, s] on the f64 matrix cores (gemm_f64.hip), or the int8
+//                     digit GEMM of gemm_i8.hip  -- log_mvnpdf_low_rank.m:13-23
 //   ldl_mfma_kernel   augmented LDL^T of [[I + Gram, u], [u', sum r^2/d]] per sample -> logdet and
 //                     r'K^-1 r (log_mvnpdf_low_rank.m:24-32), 4 samples per wave on the f64
 //                     matrix cores.
@@ -23,9 +24,10 @@ namespace {
 // One wave per (segment g, quarter h) of the slot sweep (4 per block, blockIdx.y = h), lanes over
 // 64 consecutive samples of the chunk; the wave walks its Ls/4 slots with the same register
 // sliding window as the fused kernel (warmed up at its first slot).  Splitting each segment in
-// four gives 16 waves per CU for a 16,384-sample chunk (4 with whole segments).  Writes are
-// coalesced (sample-contiguous rows), slot scalars are wave-uniform loads; sum r^2/d and
-// sum log d are left as kWeightParts partials per sample.
+// four gives 16 waves per CU for a 16,384-sample chunk (4 with whole segments).  The weights go
+// to gemm_f64's tile layout (a 32-sample tile's 32 values of a slot are one 256-B run), for
+// every sample of the padded chunk (lanes past sc: the null model's N = 0, finite); slot scalars
+// are wave-uniform loads; sum r^2/d and sum log d are left as kWeightParts partials per sample.
 template <int NL>
 __global__ __launch_bounds__(256) void weights_kernel(WeightsArgs a) {
   constexpr int kWingLds = 4 * ((3 * kWingStride + 3) / 4);
@@ -70,7 +72,10 @@ __global__ __launch_bounds__(256) void weights_kernel(WeightsArgs a) {
   double w3 = raw(lamp[3]), w4 = raw(lamp[4]), w5 = raw(lamp[5]);
   double q1 = 0.0, pm = 1.0;
   int pe = 0;
-  const int64_t ldw = a.sc;
+  const int64_t cap16 = gemm_f64_cap16(a.cap);
+  const int sloc = sl & 31;
+  double* wg_t = a.wg + (int64_t)(sl >> 5) * cap16 * 32 + 8 * (sloc & 3) + (sloc >> 2);
+  double* wu_t = a.wu + (wg_t - a.wg);
   for (int t = t0; t < t0 + Lq; ++t) {
     const int64_t slot = (int64_t)g * Ls + t;
     const double* sr = a.srow + slot * 8;
@@ -96,18 +101,14 @@ __global__ __launch_bounds__(256) void weights_kernel(WeightsArgs a) {
       pm = frexp(pm, &ex);
       pe += ex;
     }
-    if (active) {
-      a.wg[slot * ldw + sl] = a2 * dinv;
-      a.wu[slot * ldw + sl] = ab * rd;
-    }
+    wg_t[slot * 32] = a2 * dinv;
+    wu_t[slot * 32] = ab * rd;
   }
-  // slots past the 4 segments (capacity slack) are neutral rows of the panel: weight 0
+  // slots past the 4 segments (capacity slack, and the GEMM's padding to 16) are neutral: weight 0
   if (h == 0) {
-    for (int64_t slot = 4 * (int64_t)Ls + g; slot < a.cap; slot += 4) {
-      if (active) {
-        a.wg[slot * ldw + sl] = 0.0;
-        a.wu[slot * ldw + sl] = 0.0;
-      }
+    for (int64_t slot = 4 * (int64_t)Ls + g; slot < cap16; slot += 4) {
+      wg_t[slot * 32] = 0.0;
+      wu_t[slot * 32] = 0.0;
     }
   }
   if (active) {
@@ -291,7 +292,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT <= 13 ? 
 }  // namespace
 
 hipError_t launch_weights(const WeightsArgs& a, hipStream_t s) {
-  const dim3 grid((unsigned)((a.sc + 63) / 64), kWeightQuarters);
+  // every sample of the GEMM's padded 128-sample tiles gets finite weights
+  const dim3 grid((unsigned)(gemm_f64_rows(a.sc) / 64), kWeightQuarters);
   if (a.num_lines == 3)
     hipLaunchKernelGGL(weights_kernel<3>, grid, dim3(256), 0, s, a);
   else

@@ -129,7 +129,7 @@ struct LineArgs {
   const double* buf;   // device line buffer (layout above)
 };
 
-// ---- panel-GEMM path (any rank 1..kGemmMaxK; gemm_path.hip + rocBLAS dgemm in engine.hip)
+// ---- panel-GEMM path (any rank 1..kGemmMaxK; gemm_path.hip + gemm_f64.hip or gemm_i8.hip)
 constexpr int kGemmMaxK = 64;
 constexpr int kWeightQuarters = 4;                 // weights_kernel: waves per segment
 constexpr int kWeightParts = 4 * kWeightQuarters;  // per-sample partial sums (segment x quarter)
@@ -146,8 +146,8 @@ struct WeightsArgs {
   int32_t sc;
   int32_t num_lines;
   LineArgs lines;
-  double* wg;                    // [cap][sc] a^2 / d
-  double* wu;                    // [cap][sc] a r / d
+  double* wg;                    // a^2 / d, weight tiles of gemm_f64 (GemmF64Args)
+  double* wu;                    // a r / d, likewise
   double* q1p;                   // [sc][kWeightParts] partial sum r^2 / d
   double* ldp;                   // [sc][kWeightParts] partial sum log d
 };
@@ -171,6 +171,23 @@ struct LdlArgs {
 
 hipError_t launch_weights(const WeightsArgs& a, hipStream_t s);
 hipError_t launch_ldl_batch(const LdlArgs& a, hipStream_t s);
+
+// fp64 Gram / u GEMM of the panel path (gemm_f64.hip).  The weights are stored per 32-sample tile
+// as [tile][slot (cap16)][32], sample 4 g + i of the tile at position 8 i + g (weights_kernel), for
+// whole 128-sample blocks (sc rounded up to kGemmF64TileS)
+constexpr int kGemmF64TileS = 128;
+__host__ __device__ inline int64_t gemm_f64_cap16(int64_t cap) { return (cap + 15) / 16 * 16; }
+__host__ __device__ inline int64_t gemm_f64_rows(int64_t sc) { return (sc + kGemmF64TileS - 1) / kGemmF64TileS * kGemmF64TileS; }
+struct GemmF64Args {
+  const double* W;               // weight tiles (layout above)
+  const double* P;               // [slot][ldp] this spectrum's panel rows
+  int64_t ldp;                   // doubles per panel row
+  int32_t nent;                  // output entries per sample (k(k+1)/2 Gram, or k u)
+  int64_t cap, cap16;            // slots, and slots padded to 16 (the weights' tile rows)
+  int32_t sc;                    // samples of the chunk
+  double* C;                     // [sc][nent]
+};
+hipError_t launch_gemm_f64(const GemmF64Args& a, hipStream_t s);
 
 struct LikelihoodArgs {
   int32_t q_count;

@@ -626,74 +626,119 @@ __global__ __launch_bounds__(256) void voigt_batch_kernel(const double* __restri
 }
 
 // ---------------------------------------------------------------------------------------------
-// standalone log_mvnpdf_low_rank: one block; Gram + u + scalars by block reduction, then a
-// Cholesky by one lane (not the hot path: the engine fuses this into likelihood_kernel)
+// standalone log_mvnpdf_low_rank (the MEX drop-in; the engine fuses this into its sweeps): one
+// block of 256 threads.
+//   * Gram and u: the pixels go through LDS in chunks of 64 rows of M, staged column by column
+//     (coalesced reads of the column-major n x k M) as M and D^-1 M; thread t owns Gram / u entries
+//     t, t + 256, ... and sums them over the chunk in pixel order (log_mvnpdf_low_rank.m:13-23).
+//   * The augmented (k+1) x (k+1) matrix [[I + Gram, u], [u', r'D^-1 r]] is factored R'R in LDS
+//     by one wave (lane = column, right-looking): its last column is t = R^-T u and its last pivot
+//     before the square root is r'D^-1 r - t't, so log det B = 2 sum_p log R_pp and the quadratic
+//     form come out of the same elimination (log_mvnpdf_low_rank.m:24-32).
 // ---------------------------------------------------------------------------------------------
 constexpr int kMvnMaxK = 64;
+constexpr int kMvnChunk = 64;
+constexpr int kMvnSlots = (kMvnMaxK * (kMvnMaxK + 1) / 2 + kMvnMaxK + 255) / 256;  // entries per thread
 __global__ __launch_bounds__(256) void mvn_single_kernel(const double* __restrict__ y,
                                                          const double* __restrict__ mu,
                                                          const double* __restrict__ M,
                                                          const double* __restrict__ d, int64_t n,
                                                          int32_t k, double* out, int32_t* status) {
-  __shared__ double B[kMvnMaxK * kMvnMaxK];
-  __shared__ double u[kMvnMaxK];
+  __shared__ double Ms[kMvnChunk][kMvnMaxK + 1];    // chunk rows of M (+1: bank spread)
+  __shared__ double Mw[kMvnChunk][kMvnMaxK + 2];    // the same rows scaled by 1/d; column k: r/d
+  __shared__ double A[kMvnMaxK + 1][kMvnMaxK + 2];  // augmented matrix, upper triangle
   __shared__ double s_d4[4];
-  const int nent = k * (k + 1) / 2;
-  for (int e = threadIdx.x; e < nent + k; e += 256) {
-    double acc = 0.0;
+  const int tid = threadIdx.x;
+  const int nent = k * (k + 1) / 2, ntot = nent + k;
+  int er[kMvnSlots], ec[kMvnSlots];                 // entry t + 256 j -> (row, column); column k = u
+#pragma unroll
+  for (int j = 0; j < kMvnSlots; ++j) {
+    const int e = tid + 256 * j;
     if (e < nent) {
       int r = 0, start = 0;
       while (e >= start + (k - r)) { start += k - r; ++r; }
-      const int c = r + (e - start);
-      for (int64_t i = 0; i < n; ++i) acc += M[i + r * n] * (M[i + c * n] / d[i]);
-      B[r * k + c] = acc + (r == c ? 1.0 : 0.0);
-      B[c * k + r] = B[r * k + c];
+      er[j] = r; ec[j] = r + (e - start);
     } else {
-      const int r = e - nent;
-      for (int64_t i = 0; i < n; ++i) acc += M[i + r * n] * ((y[i] - mu[i]) / d[i]);
-      u[r] = acc;
+      er[j] = e - nent; ec[j] = k;
     }
   }
+  double acc[kMvnSlots];
+#pragma unroll
+  for (int j = 0; j < kMvnSlots; ++j) acc[j] = 0.0;
   double q1 = 0.0, ld = 0.0;
-  for (int64_t i = threadIdx.x; i < n; i += 256) {
-    const double r = y[i] - mu[i];
-    q1 += r * (r / d[i]);
-    ld += log(d[i]);
+  for (int64_t p0 = 0; p0 < n; p0 += kMvnChunk) {
+    const int np = (int)min<int64_t>(kMvnChunk, n - p0);
+    __syncthreads();
+    if (tid < kMvnChunk) {
+      double wi = 0.0, rwi = 0.0;
+      if (tid < np) {
+        const double di = d[p0 + tid], r = y[p0 + tid] - mu[p0 + tid];
+        wi = 1.0 / di;
+        rwi = r * wi;
+        q1 += r * rwi;
+        ld += log(di);
+      }
+      Mw[tid][kMvnMaxK + 1] = wi;
+      Mw[tid][k] = rwi;
+    }
+    __syncthreads();
+    for (int idx = tid; idx < kMvnChunk * k; idx += 256) {
+      const int c = idx / kMvnChunk, pr = idx % kMvnChunk;
+      const double v = pr < np ? M[(p0 + pr) + (int64_t)c * n] : 0.0;
+      Ms[pr][c] = v;
+      Mw[pr][c] = v * Mw[pr][kMvnMaxK + 1];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kMvnSlots; ++j) {
+      if (tid + 256 * j < ntot) {
+        const int r = er[j], c = ec[j];
+        double a = acc[j];
+        for (int pr = 0; pr < np; ++pr) a = fma(Ms[pr][r], Mw[pr][c], a);
+        acc[j] = a;
+      }
+    }
   }
   q1 = block_reduce_sum(q1, s_d4);
   ld = block_reduce_sum(ld, s_d4);
+#pragma unroll
+  for (int j = 0; j < kMvnSlots; ++j)
+    if (tid + 256 * j < ntot) A[er[j]][ec[j]] = acc[j] + (er[j] == ec[j] ? 1.0 : 0.0);
+  if (tid == 0) A[k][k] = q1;
   __syncthreads();
-  if (threadIdx.x == 0) {
-    // upper Cholesky R'R = B in place (row-major upper triangle)
-    bool bad = false;
-    double logdet = 0.0;
-    for (int p = 0; p < k; ++p) {
-      double v = B[p * k + p];
-      for (int t = 0; t < p; ++t) v -= B[t * k + p] * B[t * k + p];
-      if (!(v > 0.0)) bad = true;
-      const double rpp = sqrt(v);
-      B[p * k + p] = rpp;
-      logdet += log(rpp);
-      for (int c = p + 1; c < k; ++c) {
-        double w = B[p * k + c];
-        for (int t = 0; t < p; ++t) w -= B[t * k + p] * B[t * k + c];
-        B[p * k + c] = w / rpp;
-      }
+  if (tid >= 64) return;
+  // augmented upper Cholesky by wave 0: lane -> column c = p + 1 + lane of step p
+  const int lane = tid;
+  bool bad = false;
+  double logdet = 0.0;
+  for (int p = 0; p < k; ++p) {
+    const double v = A[p][p];
+    bad |= !(v > 0.0);
+    const double rpp = sqrt(v), irpp = 1.0 / rpp;
+    logdet += log(rpp);
+    const int c = p + 1 + lane;
+    double rpc = 0.0;
+    if (c <= k) {
+      rpc = A[p][c] * irpp;
+      A[p][c] = rpc;
     }
-    // t = R^-T u, quad = q1 - t't
-    double tt = 0.0;
-    for (int p = 0; p < k; ++p) {
-      double v = u[p];
-      for (int t = 0; t < p; ++t) v -= B[t * k + p] * u[t];
-      u[p] = v / B[p * k + p];
-      tt += u[p] * u[p];
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    if (c <= k)
+      for (int r = p + 1; r <= c; ++r) A[r][c] = fma(-A[p][r], rpc, A[r][c]);
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  }
+  if (lane == 0) {
+    const double quad = A[k][k];                    // r'D^-1 r - t't
+    double res = -0.5 * (quad + (ld + 2 * logdet) + n * kLog2Pi);
+    int st = 0;
+    if (bad || !(fabs(res) < INFINITY)) {
+      res = NAN;
+      st = 1;
     }
-    double r = -0.5 * ((q1 - tt) + (ld + 2 * logdet) + n * kLog2Pi);
-    if (bad || !(fabs(r) < INFINITY)) {
-      r = NAN;
-      *status = 1;
-    }
-    *out = r;
+    *out = res;
+    *status = st;
   }
 }
 

@@ -10,8 +10,8 @@ rules and keeps the 910-1217 A rest range plus one unmasked pixel on either side
 The FITS reader is a numpy implementation of the binary-table subset these files use (no
 astropy on the GPU box).  MATLAB's fitsread returns a 'E' column as single precision, and
 read_spec/preload_qsos keep computing in single (10.^loglam, 1./ivar, the normalisation); that
-is reproduced here (float32 arithmetic, then widened to float64 for the engine) so the
-preloaded cells hold the values the reference's cells hold.
+is reproduced here (float32 arithmetic, float32 cells, widened to float64 only when packed for
+the engine) so the preloaded cells hold the values and the class the reference's cells hold.
 """
 from __future__ import annotations
 
@@ -149,13 +149,30 @@ def read_spec(filename: str):
     return wavelengths, flux, noise_variance, pixel_mask
 
 
+def nanmedian(v: np.ndarray):
+    """MATLAB's nanmedian (preload_qsos.m:33) in the array's own class: NaNs dropped, the middle
+    element, or for an even count median.m's meanof(a, b) = a + (b - a) / 2 when a and b are finite
+    with the same sign, else (a + b) / 2 -- numpy's (a + b) / 2 can differ from it in the last bit."""
+    v = np.sort(v[~np.isnan(v)])
+    n = v.size
+    if n == 0:
+        return v.dtype.type(np.nan)
+    if n % 2:
+        return v[n // 2]
+    a, b = v[n // 2 - 1], v[n // 2]
+    two = v.dtype.type(2)
+    if np.isfinite(a) and np.isfinite(b) and np.sign(a) == np.sign(b):
+        return a + (b - a) / two
+    return (a + b) / two
+
+
 def spec_filename(spectra_directory: str, plate: int, mjd: int, fiber_id: int) -> str:
     """The DR12Q layout file_loader reads: <spectra>/<plate>/spec-<plate>-<mjd>-<fiber>.fits."""
     return f"{spectra_directory}/{int(plate)}/spec-{int(plate)}-{int(mjd)}-{int(fiber_id):04d}.fits"
 
 
 def preload_qsos(z_qsos, plates, mjds, fiber_ids, filter_flags, file_loader, log=None) -> dict:
-    """preload_qsos.m:13-75.  ``file_loader(plate, mjd, fiber_id)`` returns read_spec's tuple.
+    """preload_qsos.m:10-71.  ``file_loader(plate, mjd, fiber_id)`` returns read_spec's tuple.
     Returns the saved variables (cells as lists, filter_flags updated with bits 3 and 4)."""
     z_qsos = np.asarray(z_qsos, dtype=np.float64).ravel()
     filter_flags = np.array(filter_flags, dtype=np.uint8).ravel().copy()
@@ -163,36 +180,36 @@ def preload_qsos(z_qsos, plates, mjds, fiber_ids, filter_flags, file_loader, log
     all_w, all_f, all_n, all_m = ([np.zeros(0) for _ in range(Q)] for _ in range(4))
     all_normalizers = np.zeros(Q)
     for i in range(Q):
-        if filter_flags[i] > 0:                                                           # :25-27
+        if filter_flags[i] > 0:                                                           # :19-21
             continue
-        w, fl, nv, pm = file_loader(plates[i], mjds[i], fiber_ids[i])                     # :29-30
-        # emitted_wavelengths (:32); single-precision cells stay single as in MATLAB
+        w, fl, nv, pm = file_loader(plates[i], mjds[i], fiber_ids[i])                     # :23-24
+        # emitted_wavelengths (:26); single-precision cells stay single as in MATLAB
         rest = w / (np.float32(1 + z_qsos[i]) if w.dtype == np.float32 else 1 + z_qsos[i])
-        ind = (rest >= P.NORMALIZATION_MIN_LAMBDA) & (rest <= P.NORMALIZATION_MAX_LAMBDA) & ~pm  # :35-37
-        vals = fl[ind]
-        vals = vals[~np.isnan(vals)]
-        med = np.median(vals) if vals.size else np.nan                                   # :38 nanmedian
-        if np.isnan(med):                                                                 # :41-44
+        ind = (rest >= P.NORMALIZATION_MIN_LAMBDA) & (rest <= P.NORMALIZATION_MAX_LAMBDA) & ~pm  # :29-31
+        med = nanmedian(fl[ind])                                                          # :33
+        if np.isnan(med):                                                                 # :36-39
             filter_flags[i] |= 1 << 2
             continue
-        ind = (rest >= P.MIN_LAMBDA) & (rest <= P.MAX_LAMBDA) & ~pm                       # :46-48
-        if np.count_nonzero(ind) < P.MIN_NUM_PIXELS:                                       # :51-54
+        ind = (rest >= P.MIN_LAMBDA) & (rest <= P.MAX_LAMBDA) & ~pm                       # :41-43
+        if np.count_nonzero(ind) < P.MIN_NUM_PIXELS:                                       # :46-49
             filter_flags[i] |= 1 << 3
             continue
-        all_normalizers[i] = med                                                          # :56
-        fl = fl / med                                                                     # :58
-        nv = nv / (med * med)                                                             # :59
-        ind = (rest >= P.LOADING_MIN_LAMBDA) & (rest <= P.LOADING_MAX_LAMBDA)             # :61-62
-        avail = np.flatnonzero(~ind & ~pm)                                                # :65
+        all_normalizers[i] = med                                                          # :51
+        fl = fl / med                                                                     # :53
+        nv = nv / (med * med)                                                             # :54
+        ind = (rest >= P.LOADING_MIN_LAMBDA) & (rest <= P.LOADING_MAX_LAMBDA)             # :56-57
+        avail = np.flatnonzero(~ind & ~pm)                                                # :60
         if ind.any():
             first, last = np.flatnonzero(ind)[0], np.flatnonzero(ind)[-1]
             after, before = avail[avail > last], avail[avail < first]
             if after.size:
-                ind[after.min()] = True                                                  # :66
+                ind[after.min()] = True                                                  # :61
             if before.size:
-                ind[before.max()] = True                                                 # :67
-        all_w[i], all_f[i] = w[ind].astype(np.float64), fl[ind].astype(np.float64)        # :69-72
-        all_n[i], all_m[i] = nv[ind].astype(np.float64), pm[ind].astype(bool)
+                ind[before.max()] = True                                                 # :62
+        # the cells keep fitsread's single class, as the reference's preloaded_qsos.mat holds them;
+        # pack_spectra widens them (exactly) to the engine's fp64
+        all_w[i], all_f[i] = w[ind], fl[ind]                                               # :64-67
+        all_n[i], all_m[i] = nv[ind], pm[ind].astype(bool)
         if log:
             log(f"loaded quasar {i + 1} of {Q} ({plates[i]}/{mjds[i]}/{int(fiber_ids[i]):04d})")
     return dict(loading_min_lambda=P.LOADING_MIN_LAMBDA, loading_max_lambda=P.LOADING_MAX_LAMBDA,

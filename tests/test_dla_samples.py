@@ -111,3 +111,18 @@ def test_run_generate_dla_samples_files(tmp_path, prior):
     assert float(r["alpha"][0, 0]) == 0.9
     s = PR.load_dla_samples(str(d / "dla_samples.mat"))
     np.testing.assert_array_equal(s["nhi_samples"], out["nhi_samples"])
+
+
+def test_matches_the_oracle_restatement(prior):
+    """Product vs oracle/dla_samples_oracle.py, the step-by-step MATLAB-order restatement of
+    generate_dla_samples.m (digit-by-digit RR2 Halton, ksdensity loop, QR polyfit, quadrature
+    integral for Z and the CDF, bracket + Brent fzero): offsets bit for bit, log N_HI to 1e-11
+    (the oracle's quadrature and root tolerances; the product integrates in closed form)."""
+    from oracle import dla_samples_oracle as DO
+    _, log_nhis = prior
+    cells = list(np.array_split(log_nhis, 40)) + [np.zeros(0)]
+    got = D.generate_dla_samples(cells, num_dla_samples=300)
+    want = DO.generate_dla_samples(cells, 300)
+    np.testing.assert_array_equal(got["offset_samples"], want["offset_samples"])
+    np.testing.assert_allclose(got["log_nhi_samples"], want["log_nhi_samples"], rtol=0, atol=1e-11)
+    np.testing.assert_allclose(got["nhi_samples"], want["nhi_samples"], rtol=1e-10)

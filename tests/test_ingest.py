@@ -155,3 +155,97 @@ def test_own_fits_writer_roundtrip(tmp_path):
     got = I.read_bintable(str(tmp_path / "s.fits"), 1)
     for a, b in zip(got, (f, ll, iv, am)):
         assert np.array_equal(a, b)
+
+
+H5PY_PY = "/opt/conda/bin/python3.9"
+
+
+def _has_astropy():
+    import os
+    import subprocess
+    if not os.path.exists(H5PY_PY):
+        return False
+    return subprocess.run([H5PY_PY, "-c", "import astropy.io.fits"], capture_output=True).returncode == 0
+
+
+@pytest.mark.skipif(not _has_astropy(), reason="no interpreter with astropy (GPU box)")
+def test_preload_matches_the_oracle_restatement(tmp_path):
+    """Product read_spec + preload_qsos against oracle/ingest_oracle.py, the line-by-line
+    restatement of read_spec.m and preload_qsos.m that reads the FITS files with astropy (run with
+    the interpreter that has it).  Cases: plain spectra (odd and even counts in the normalisation
+    window), a pre-filtered entry, a masked normalisation window (bit 3), too few pixels (bit 4),
+    NaN fluxes in the window, BRIGHTSKY-masked pixels, loading-range edges with and without an
+    unmasked neighbour.  Every saved variable must agree bit for bit (cells widened to double)."""
+    import subprocess
+    from fits_writer import write_speclite
+    rng = np.random.default_rng(17)
+    spectra = tmp_path / "spectra"
+    cases = [  # (z, lo, hi, prefilter, mask window, nan in window, first-pixel masked)
+        (2.5, 3400, 5600, 0, False, False, False), (2.7, 3560, 5900, 0, False, True, False),
+        (3.1, 3600, 6200, 0, False, False, True), (2.4, 3300, 5200, 1, False, False, False),
+        (2.6, 3500, 5700, 0, True, False, False), (3.3, 5100, 6000, 0, False, False, False),
+        (2.2, 2860, 4300, 0, False, False, False), (2.9, 3700, 6100, 0, False, True, True)]
+    z, plates, mjds, fibers, flags = [], [], [], [], []
+    for q, (zq, lo, hi, pre, mwin, nanw, mfirst) in enumerate(cases):
+        ll = np.arange(np.log10(lo), np.log10(hi), 1e-4).astype(np.float32)
+        w = np.float32(10) ** ll
+        rest = w / np.float32(1 + zq)
+        f = rng.normal(3.0, 0.4, ll.size).astype(np.float32)
+        iv = rng.uniform(20, 80, ll.size).astype(np.float32)
+        iv[rng.uniform(size=ll.size) < 0.05] = 0
+        am = np.where(rng.uniform(size=ll.size) < 0.05, 1 << 23, 0).astype(np.int32)   # BRIGHTSKY
+        am |= np.where(rng.uniform(size=ll.size) < 0.1, 1 << 5, 0).astype(np.int32)    # an ignored bit
+        win = (rest >= 1310) & (rest <= 1325)
+        if mwin:
+            iv[win] = 0
+        if nanw:
+            f[np.flatnonzero(win)[::7]] = np.nan
+        if mfirst:   # the pixel just below the loading range is masked: the next unmasked one is taken
+            below = np.flatnonzero(rest < 910)
+            if below.size:
+                iv[below[-1]] = 0
+        p, m, fi = 5000 + q, 56000 + q, 10 + q
+        d = spectra / str(p)
+        d.mkdir(parents=True, exist_ok=True)
+        write_speclite(str(d / f"spec-{p}-{m}-{fi:04d}.fits"), f, ll, iv, am)
+        z.append(zq); plates.append(p); mjds.append(m); fibers.append(fi); flags.append(pre)
+    got = I.preload_qsos(z, plates, mjds, fibers, np.array(flags, np.uint8),
+                         lambda p, m, f: I.read_spec(I.spec_filename(str(spectra), p, m, f)))
+    job = tmp_path / "job.npz"
+    np.savez(job, z_qsos=np.array(z), plates=np.array(plates), mjds=np.array(mjds), fiber_ids=np.array(fibers),
+             filter_flags=np.array(flags, np.uint8), spectra_dir=str(spectra))
+    oracle = Path(__file__).resolve().parents[1] / "oracle" / "ingest_oracle.py"
+    res = subprocess.run([H5PY_PY, "-B", str(oracle), str(job), str(tmp_path / "out.npz")], capture_output=True,
+                         text=True)
+    assert res.returncode == 0, res.stderr[-2000:]
+    want = np.load(tmp_path / "out.npz")
+    assert got["filter_flags"].tolist() == want["filter_flags"].tolist()
+    assert sorted(set(got["filter_flags"].tolist())) == [0, 1, 4, 8]          # every branch exercised
+    np.testing.assert_array_equal(got["all_normalizers"], want["all_normalizers"])
+    for key in ("all_wavelengths", "all_flux", "all_noise_variance", "all_pixel_mask"):
+        for q in range(len(cases)):
+            name = f"{key}__{q}"
+            if name in want.files:
+                np.testing.assert_array_equal(got[key][q], want[name].astype(got[key][q].dtype), err_msg=name)
+            else:
+                assert got[key][q].size == 0, name
+
+
+def test_nanmedian_is_matlabs():
+    """median.m's meanof for an even count (a + (b - a) / 2 for finite same-sign a, b), NaNs dropped,
+    in single: cases where numpy's (a + b) / 2 rounds differently."""
+    f = np.float32
+    a, b = f(1.0000001), f(3.9999998)
+    v = np.array([b, np.nan, a], dtype=np.float32)
+    assert I.nanmedian(v) == a + (b - a) / f(2)
+    rng = np.random.default_rng(3)
+    seen = 0
+    for _ in range(2000):
+        x = (rng.lognormal(0, 3, 2 * rng.integers(1, 8)) * rng.choice([-1, 1])).astype(np.float32)
+        s = np.sort(x)
+        lo, hi = s[x.size // 2 - 1], s[x.size // 2]
+        want = lo + (hi - lo) / f(2) if np.sign(lo) == np.sign(hi) else (lo + hi) / f(2)
+        assert I.nanmedian(x) == want and I.nanmedian(x).dtype == np.float32
+        seen += want != np.median(x)
+    assert seen > 0                                   # numpy's median differs on some of these
+    assert np.isnan(I.nanmedian(np.array([np.nan], np.float32)))
