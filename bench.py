@@ -71,6 +71,25 @@ def i8_roofline(st: dict, n: float, k: int, Q: int, S: int, steps: int, path: st
                     "the 24-bit path counted as one); the batch adds the weights and LDL^T kernels"}
 
 
+def f64_gemm_roofline(st: dict, n: float, k: int, Q: int, S: int, steps: int) -> dict:
+    """Roofline of the fp64 panel path's dominant kernel, the Gram/u GEMM on the f64 matrix cores
+    (gemm_f64.hip): 2 n (k(k+1)/2 + k) algorithmic flops per evaluation (the Gram and u part of
+    SURVEY.md 8d's F_eval) over its average launch time (HIP events around the Gram + u launches of
+    each spectrum and sample chunk, gpdla_stats.contraction_ms), against the FP64 matrix peak."""
+    flops = 2 * n * (k * (k + 1) / 2 + k)
+    if st["contraction_launches"] == 0:      # a library build without GEMM timing (A/B variants)
+        return {"note": "no GEMM launch timing in this library build"}
+    nl = st["contraction_launches"]
+    gemm_ms = st["contraction_ms"] / nl
+    evals_per_gemm = Q * (S + 1) * steps / nl
+    achieved = flops * evals_per_gemm / (gemm_ms * 1e-3) / 1e12
+    return {"bound": "mfma", "mfma_dtype": "f64", "unit": "TFLOP/s", "peak": FP64_PEAK_TFLOPS, "achieved": achieved,
+            "frac": achieved / FP64_PEAK_TFLOPS, "avg_launch_ms": gemm_ms, "evals_per_launch": evals_per_gemm,
+            "gemm_flops_per_eval": flops,
+            "note": "gemm_f64 launches only (Gram + u per spectrum and sample chunk, counted as one); the batch "
+                    "adds the weights and LDL^T kernels"}
+
+
 def effective_bytes_per_eval(n: int, k: int, w: int = 8) -> float:
     """SURVEY.md 8d streamed-panel accounting (north-star 'effective HBM')."""
     return w * (n * (k + 5) + 8) + w
@@ -482,8 +501,6 @@ def main():
     eff_gbs = effective_bytes_per_eval(n_mean, args.k) * evals_per_launch / (avg_ms * 1e-3) / 1e9
 
     traffic, traffic_src = profiled_traffic(Q, S, args.k, path)
-    # batched LDL^T kernel of the panel paths (gemm_path.hip launch_ldl_batch)
-    ldl_name = f"ldl_mfma_kernel<{(args.k + 4) // 4}>"
     result = {
         "metric": "(spectrum x DLA-sample) log-evidence evals/sec",
         "value": value,
@@ -510,14 +527,15 @@ def main():
                      "kernel": {"fused": f"likelihood_kernel<{args.k}>",
                                 "fused-int8": f"likelihood_i8_kernel<{args.k}>",
                                 "panel-GEMM-int8": "gemm_i8_kernel<4>",
-                                "panel-GEMM-int8-24": "gemm_i8_kernel<3> (Gram) + gemm_i8_kernel<4> (u)"}.get(
-                                    path, f"weights_kernel + rocBLAS dgemm + {ldl_name} (per batch)"),
+                                "panel-GEMM-int8-24": "gemm_i8_kernel<3> (Gram) + gemm_i8_kernel<4> (u)",
+                                "panel-GEMM": "gemm_f64_kernel (Gram + u)"}.get(path, path),
                      "avg_launch_ms": avg_ms,
                      "flops_per_eval": algorithmic_flops_per_eval(n_mean, args.k),
                      "evals_per_launch": evals_per_launch,
                      # int8 panel paths: the int8 GEMM kernel's own roofline (overrides the fields above)
-                     **({} if not path.startswith("panel-GEMM-int8") else i8_roofline(st, n_mean, args.k, Q, S,
-                                                                                      args.steps, path))},
+                     **(i8_roofline(st, n_mean, args.k, Q, S, args.steps, path) if path.startswith("panel-GEMM-int8")
+                        else f64_gemm_roofline(st, n_mean, args.k, Q, S, args.steps) if path == "panel-GEMM"
+                        else {})},
         "hbm_effective": {"achieved": eff_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                           "frac": eff_gbs / HBM_PEAK_GBS,
                           "bytes_per_eval": effective_bytes_per_eval(n_mean, args.k),

@@ -535,10 +535,12 @@ int gpdla_engine_process(gpdla_engine* e, const gpdla_spectra* sp, const gpdla_r
         if ((rc = grow(&e->d_wg, &e->cap_wg, wbytes))) return rc;
         if ((rc = grow(&e->d_wu, &e->cap_wu, wbytes))) return rc;
       }
-      // + 8 elements of slack: ldl_mfma_kernel's straight-line tile loads may address one element
-      // past the last sample's Gram when k is a multiple of 4 (the value is discarded)
-      if ((rc = grow(&e->d_G, &e->cap_G, (size_t)(E * sc_max + 8)))) return rc;
-      if ((rc = grow(&e->d_U, &e->cap_U, (size_t)(e->K * sc_max + 8)))) return rc;
+      // the GEMMs store whole 128-sample tiles (quad_index layout, internal.h); + 64 elements of
+      // slack: ldl_mfma_kernel's straight-line tile loads may address one entry past the last
+      // sample's Gram when k is a multiple of 4 (the value is discarded)
+      const int64_t grows = gemm_f64_rows(sc_max);
+      if ((rc = grow(&e->d_G, &e->cap_G, (size_t)(E * grows + 64)))) return rc;
+      if ((rc = grow(&e->d_U, &e->cap_U, (size_t)(e->K * grows + 64)))) return rc;
       if ((rc = grow(&e->d_q1p, &e->cap_q1p, (size_t)(kWeightParts * sc_max)))) return rc;
       if ((rc = grow(&e->d_ldp, &e->cap_ldp, (size_t)(kWeightParts * sc_max)))) return rc;
     }
@@ -862,7 +864,7 @@ int gpdla_voigt_batch_f64(const double* lambdas, int64_t n_padded, const double*
   const int64_t n_out = n_padded - 2 * kWidth;
   const size_t n_in = (size_t)(n_padded + 2 * count);          // [lambdas | z | N]
   const size_t bytes = (n_in + (size_t)count * n_out) * 8;
-  hipError_t err = standalone_reserve(sb, bytes, bytes);
+  hipError_t err = standalone_reserve(sb, bytes, n_in * 8);
   if (err != hipSuccess) return set_error(GPDLA_EDEVICE, "voigt: %s", hipGetErrorString(err));
   double* h = (double*)sb.host;
   std::memcpy(h, lambdas, n_padded * 8);
@@ -874,10 +876,11 @@ int gpdla_voigt_batch_f64(const double* lambdas, int64_t n_padded, const double*
   double* d_out = d_N + count;
   err = hipMemcpyAsync(d_lam, h, n_in * 8, hipMemcpyHostToDevice, sb.stream);
   if (err == hipSuccess) err = launch_voigt_batch(d_lam, n_padded, d_z, d_N, count, num_lines, make_line_args(d_lines), d_out, sb.stream);
-  if (err == hipSuccess) err = hipMemcpyAsync(h + n_in, d_out, count * n_out * 8, hipMemcpyDeviceToHost, sb.stream);
+  // the profiles straight into the caller's buffer (the pinned staging is write-combined: reading
+  // it back on the host is slow)
+  if (err == hipSuccess) err = hipMemcpyAsync(out, d_out, count * n_out * 8, hipMemcpyDeviceToHost, sb.stream);
   if (err == hipSuccess) err = hipStreamSynchronize(sb.stream);
   if (err != hipSuccess) return set_error(GPDLA_EDEVICE, "voigt: %s", hipGetErrorString(err));
-  std::memcpy(out, h + n_in, count * n_out * 8);
   return GPDLA_OK;
 }
 

@@ -125,17 +125,17 @@ __global__ __launch_bounds__(256, 2) void gemm_f64_kernel(GemmF64Args a) {
     if (more) store_b(buf ^ 1, bst);
     __syncthreads();
   }
-  // D: lane 16 i + 4 b + j holds sample 4 g + (lane >> 4), entry 16 eg + (lane & 15)
+  // D: lane 16 i + 4 b + j holds sample 4 g + (lane >> 4), entry 16 eg + (lane & 15); in the
+  // quad_index layout a wave's store of (g, eg) is 64 consecutive doubles (every sample of the
+  // padded tile is stored; those past sc are never read)
   const int s_wave = st * kFS + wave * 32;
 #pragma unroll
   for (int g = 0; g < 8; ++g) {
-    const int s = s_wave + 4 * g + kk;
-    if (s >= a.sc) continue;
-    double* crow = a.C + (int64_t)s * a.nent;
+    double* cg = a.C + quad_index(s_wave + 4 * g, 0, a.nent) + kk;
 #pragma unroll
     for (int eg = 0; eg < 8; ++eg) {
       const int e = e_base + 16 * eg + j16;
-      if (e < a.nent) crow[e] = acc[g][eg];
+      if (e < a.nent) cg[4 * e] = acc[g][eg];
     }
   }
 }

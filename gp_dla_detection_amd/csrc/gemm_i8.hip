@@ -345,18 +345,29 @@ __global__ __launch_bounds__(256, ND == 3 ? 3 : 2) void gemm_i8_kernel(GemmI8Arg
       const double sc = a.ent[e], off0 = a.ent[NE + e];
 #pragma unroll
       for (int rt = 0; rt < 2; ++rt) {
+        // the lane's 4 consecutive samples of entry col: one vector store in the quad_index layout
+        // (every sample of the rows is stored; those past sc are never read)
+        const int s4 = s_tile + 32 * wave + 16 * rt + 4 * (lane >> 4);
+        double v[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int sl = s_tile + 32 * wave + 16 * rt + 4 * (lane >> 4) + r;
-          if (sl >= a.sc) continue;
           // sum_l 2^(48 - 8 l) C_l, least significant level first
           double val = (double)acc[ND - 1][rt][ct][r] * __builtin_ldexp(1.0, 48 - 8 * (ND - 1));
 #pragma unroll
           for (int l = ND - 2; l >= 0; --l) val = fma((double)acc[l][rt][ct][r], __builtin_ldexp(1.0, 48 - 8 * l), val);
-          val = (val + off0) * sc;
-          if (u_tile) a.U[(int64_t)sl * K + col] = val;
-          else if (a.G32) a.G32[(int64_t)sl * E + col] = (float)val;
-          else a.G[(int64_t)sl * E + col] = val;
+          v[r] = (val + off0) * sc;
+        }
+        if (u_tile) {
+          double2* d = reinterpret_cast<double2*>(a.U + quad_index(s4, col, K));
+          d[0] = make_double2(v[0], v[1]);
+          d[1] = make_double2(v[2], v[3]);
+        } else if (a.G32) {
+          *reinterpret_cast<float4*>(a.G32 + quad_index(s4, col, E)) =
+              make_float4((float)v[0], (float)v[1], (float)v[2], (float)v[3]);
+        } else {
+          double2* d = reinterpret_cast<double2*>(a.G + quad_index(s4, col, E));
+          d[0] = make_double2(v[0], v[1]);
+          d[1] = make_double2(v[2], v[3]);
         }
       }
     }

@@ -117,14 +117,6 @@ __global__ __launch_bounds__(256) void weights_kernel(WeightsArgs a) {
   }
 }
 
-// the kWeightParts per-sample partials of sum r^2/d or sum log d, in slot order
-__device__ inline double sum_parts(const double* p) {
-  double acc = 0.0;
-#pragma unroll
-  for (int i = 0; i < kWeightParts; ++i) acc += p[i];
-  return acc;
-}
-
 __device__ inline void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -172,10 +164,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT <= 13 ? 
   }
   const int64_t E = (int64_t)K * (K + 1) / 2;
   const int slc = live ? sl : 0;  // idle samples of the last wave compute on sample 0, discarded
-  const GT* Gs = gram_of<GT>(a) + (int64_t)slc * E;  // fp64, or fp32 on the 24-bit int8 path
-  const double* Us = a.U + (int64_t)slc * K;
-  const double q1 = sum_parts(a.q1p + (int64_t)slc * kWeightParts);
-  const double logdet_d = sum_parts(a.ldp + (int64_t)slc * kWeightParts);
+  // quad_index layout (internal.h): entry e of this lane's sample at 4 e; the wave's 4 samples x 16
+  // tile positions are 64 consecutive values per load
+  const GT* Gs = gram_of<GT>(a) + quad_index(slc, 0, E);  // fp64, or fp32 on the 24-bit int8 path
+  const double* Us = a.U + quad_index(slc, 0, K);
+  // sum r^2/d and sum log d: the sample's 16 lanes load one partial each and add them up
+  double q1 = a.q1p[(int64_t)slc * kWeightParts + 4 * ti + tj];
+  double logdet_d = a.ldp[(int64_t)slc * kWeightParts + 4 * ti + tj];
+#pragma unroll
+  for (int m = 1; m <= 32; m <<= 1) {
+    if (m == 4 || m == 8) continue;          // lane bits 2-3 are the sample
+    q1 += __shfl_xor(q1, m);
+    logdet_d += __shfl_xor(logdet_d, m);
+  }
   // Load the tiles: straight-line code (unconditional loads from valid addresses, then selects), so
   // the NT (NT + 1) / 2 loads go out back to back.  Since 4 (NT - 1) <= k, only the last tile
   // column (I = NT - 1) holds the u column (c = k), r'D^-1 r (r = c = k) and identity padding
@@ -194,20 +195,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT <= 13 ? 
       double v;
       if (I < NT - 1) {
         const int tb = 10 * L + 16 * (L * (NT - 2) - L * (L - 1) / 2) + (I == L ? 0 : 10 + 16 * (I - L - 1));
-        v = I == L ? (double)Gs[tb + ldiag] + done : (double)Gs[tb + loff];   // B = I + Gram
+        v = I == L ? (double)Gs[4 * (tb + ldiag)] + done : (double)Gs[4 * (tb + loff)];   // B = I + Gram
       } else if (L < NT - 1) {
         // rows 4L + ti < k, column c = 4 (NT - 1) + tj: Gram if tj < w, u if tj == w, padding after
         const int r = 4 * L + ti;
-        const double g = (double)Gs[base2 + L * 4 * w + ti * w + min(tj, max(w - 1, 0))], u = Us[r];
+        const double g = (double)Gs[4 * (base2 + L * 4 * w + ti * w + min(tj, max(w - 1, 0)))], u = Us[4 * r];
         v = tj < w ? g : (tj == w ? u : 0.0);
       } else {
         // corner tile: Gram (di <= dj < w), then u (dj == w, di < w), r'D^-1 r (di == dj == w),
         // identity padding
         const int r = 4 * L + di;
         const int cw = max(w, 1);
-        const double g = (double)Gs[base2 + L * 4 * w + min(di, cw - 1) * w - min(di, cw - 1) * (min(di, cw - 1) - 1) / 2 +
-                                    (min(dj, cw - 1) - min(di, cw - 1))];
-        const double u = Us[min(r, K - 1)];
+        const double g = (double)Gs[4 * (base2 + L * 4 * w + min(di, cw - 1) * w - min(di, cw - 1) * (min(di, cw - 1) - 1) / 2 +
+                                         (min(dj, cw - 1) - min(di, cw - 1)))];
+        const double u = Us[4 * min(r, K - 1)];
         v = dj < w ? g + done : (dj == w ? (di < w ? u : q1) : done);
       }
       T[L * NT - L * (L - 1) / 2 + (I - L)] = v;

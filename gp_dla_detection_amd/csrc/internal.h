@@ -156,9 +156,9 @@ struct LdlArgs {
   const SpecInfo* info;
   int32_t q;
   int32_t k;
-  const double* G;               // [sc][k(k+1)/2] Gram per sample, entries in gram_tile_index order
+  const double* G;               // Gram, quad_index(s, e, k(k+1)/2), entries in gram_tile_index order
   const float* G32;              // the same in fp32 (panel_gemm_i8_24), or nullptr: then G is read
-  const double* U;               // [sc][k]
+  const double* U;               // u, quad_index(s, i, k)
   const double* q1p;
   const double* ldp;
   int64_t S, s0;
@@ -171,6 +171,15 @@ struct LdlArgs {
 
 hipError_t launch_weights(const WeightsArgs& a, hipStream_t s);
 hipError_t launch_ldl_batch(const LdlArgs& a, hipStream_t s);
+
+// Gram / u hand-off between the panel GEMMs (gemm_f64.hip, gemm_i8.hip) and ldl_mfma_kernel:
+// samples in groups of 4, entry e of sample s at (s >> 2) 4 n + 4 e + (s & 3) (n = entries per
+// sample).  A GEMM lane's 4 consecutive samples of one entry are one 16-B (fp32) or 32-B store, and
+// the LDL^T wave (4 samples x the 16 positions of a tile) reads 64 consecutive values.  Buffers
+// cover whole GEMM sample tiles (gemm_f64_rows), so the GEMMs store without a sample bound.
+__host__ __device__ inline int64_t quad_index(int64_t s, int64_t e, int64_t n) {
+  return (s >> 2) * 4 * n + 4 * e + (s & 3);
+}
 
 // fp64 Gram / u GEMM of the panel path (gemm_f64.hip).  The weights are stored per 32-sample tile
 // as [tile][slot (cap16)][32], sample 4 g + i of the tile at position 8 i + g (weights_kernel), for
@@ -185,7 +194,7 @@ struct GemmF64Args {
   int32_t nent;                  // output entries per sample (k(k+1)/2 Gram, or k u)
   int64_t cap, cap16;            // slots, and slots padded to 16 (the weights' tile rows)
   int32_t sc;                    // samples of the chunk
-  double* C;                     // [sc][nent]
+  double* C;                     // quad_index(s, e, nent), for every sample of the padded tiles
 };
 hipError_t launch_gemm_f64(const GemmF64Args& a, hipStream_t s);
 
@@ -337,9 +346,9 @@ struct GemmI8Args {
   const uint8_t* adig;
   const uint8_t* bdig;           // this spectrum's B planes
   const double* ent;             // this spectrum's [2][entries]
-  double* G;                     // [sc][E]
+  double* G;                     // quad_index(s, e, E), every sample of the rows
   float* G32;                    // if set, the Gram goes here in fp32 instead (24-bit path)
-  double* U;                     // [sc][k]
+  double* U;                     // quad_index(s, i, k)
 };
 
 hipError_t launch_convert_gemm_i8(const ConvertGemmI8Args& a, int32_t q_count, hipStream_t s);
