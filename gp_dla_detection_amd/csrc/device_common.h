@@ -36,6 +36,18 @@ __device__ inline double rcp_sweep(double d) {
   return fma(r, fma(-d, r, 1.0), r);
 }
 
+// global -> LDS DMA of one 1 KiB piece (64 lanes x 16 B, per-lane global byte offsets from a
+// wave-uniform base), issued from inline asm so the compiler's waitcnt pass does not drain it before
+// unrelated LDS reads; the consumer waits with an explicit s_waitcnt vmcnt + barrier.  s_nop 4: a
+// fresh SGPR base read by a global_* op; s_nop 0: between the M0 write and the LDS-DMA reading it.
+__device__ inline void dma_piece(const void* sbase, uint32_t voffset, uint32_t lds_dst) {
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+  asm volatile("s_nop 4\n\ts_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2"
+               :: "s"(lds_dst), "v"(voffset), "s"(sbase) : "memory", "m0");
+#pragma clang diagnostic pop
+}
+
 // ---- int8 Ozaki contraction helpers (kernels_i8.hip, gemm_i8.hip)
 typedef int v4i __attribute__((ext_vector_type(4)));
 

@@ -400,13 +400,13 @@ static int run_panel_gemm(gpdla_engine* e, bool i8, int64_t nq, const int64_t* h
         // Gram[s][e] = sum_t Wg[t][s] PG[t][e] (the slot-major Khatri-Rao rows), u[s][i] likewise
         // over the M rows, on the f64 matrix cores (gemm_f64.hip)
         GemmF64Args ga{};
-        ga.W = e->d_wg; ga.P = e->d_panel + h_sb[q] * E; ga.ldp = E; ga.nent = (int32_t)E;
-        ga.cap = h_cap[q]; ga.cap16 = gemm_f64_cap16(h_cap[q]); ga.sc = sc; ga.C = G;
+        ga.seg[0] = GemmF64Seg{e->d_wg, e->d_panel + h_sb[q] * gemm_ldp(K), gemm_ldp(K), (int32_t)E, G};
+        ga.seg[1] = GemmF64Seg{e->d_wu, e->d_pm + h_sb[q] * gemm_ldm(K), gemm_ldm(K), K, U};
+        ga.nseg = 2;
+        ga.cap = h_cap[q]; ga.cap16 = gemm_f64_cap16(h_cap[q]); ga.sc = sc;
         TimedLaunch tg{};
         int rc;
         if ((rc = record_start(e, &tg, 3))) return rc;
-        HIP_TRY(launch_gemm_f64(ga, st));
-        ga.W = e->d_wu; ga.P = e->d_pm + h_sb[q] * K; ga.ldp = K; ga.nent = K; ga.C = U;
         HIP_TRY(launch_gemm_f64(ga, st));
         HIP_TRY(hipEventRecord(tg.stop, st));
         e->pending.push_back(tg);
@@ -445,7 +445,7 @@ int gpdla_engine_process(gpdla_engine* e, const gpdla_spectra* sp, const gpdla_r
   const int64_t QB = e->params.max_batch_spectra > 0 ? e->params.max_batch_spectra : (e->gemm ? 64 : 1024);
   // panel doubles per slot: fused layout row, or the Khatri-Rao row of the panel-GEMM layout
   const int64_t E = (int64_t)e->K * (e->K + 1) / 2;
-  const int64_t row = e->gemm ? E : panel_row_doubles(e->K);
+  const int64_t row = e->gemm ? gemm_ldp(e->K) : panel_row_doubles(e->K);
   const int es = e->gemm ? 0 : scratch_doubles(e->K);
   // panel-GEMM sample chunks: the S + 1 samples (null model included) in equal chunks of at most
   // kMaxChunk.  configs[4] (S + 1 = 100,001) measured 46.2 Mevals/s with 16,384-sample chunks (6
@@ -525,10 +525,14 @@ int gpdla_engine_process(gpdla_engine* e, const gpdla_spectra* sp, const gpdla_r
     if ((rc = grow(&e->d_info, &e->cap_q, (size_t)QB))) return rc;
     // + one LDS row of slack: the staging DMA reads whole 1 KiB pieces (kernels.hip stage_chunk)
     if ((rc = grow(&e->d_panel, &e->cap_slots,
-                   (size_t)(slots * row + (e->gemm ? 0 : panel_lds_row_doubles(e->K)))))) return rc;
+                   (size_t)(slots * row + (e->gemm ? gemm_panel_slack(row) : panel_lds_row_doubles(e->K)))))) return rc;
     if ((rc = grow(&e->d_lam, &e->cap_lam, (size_t)lams))) return rc;
     if (e->gemm) {
-      if ((rc = grow(&e->d_pm, &e->cap_pm, (size_t)slots * e->K))) return rc;
+      const int64_t ldm = gemm_ldm(e->K);
+      if ((rc = grow(&e->d_pm, &e->cap_pm, (size_t)(slots * ldm + gemm_panel_slack(ldm))))) return rc;
+      // the rows gemm_f64 reads past the batch's last slot: zero (finite, against zero weights)
+      HIP_TRY(hipMemsetAsync(e->d_panel + slots * row, 0, gemm_panel_slack(row) * 8, st));
+      HIP_TRY(hipMemsetAsync(e->d_pm + slots * ldm, 0, gemm_panel_slack(ldm) * 8, st));
       if ((rc = grow(&e->d_srow, &e->cap_srow, (size_t)slots * 8))) return rc;
       if (!batch_gemm_i8) {  // the fp64 weight tiles: only the fp64 GEMM reads them
         const size_t wbytes = (size_t)(gemm_f64_cap16(cap_max) * gemm_f64_rows(sc_max));

@@ -13,13 +13,25 @@
 // on 8 A and 8 B registers (0.125 LDS bytes per flop).  Operand maps (probed, tools/probe_layout.hip):
 // A[i][k] at lane 16k + 4b + i, B[k][j] at 16k + 4b + j, D[i][j] at 16i + 4b + j.
 //
-// Block: 4 waves = 128 samples x 128 entries.  B (the panel, shared by the 4 waves) is staged
-// through a double-buffered LDS tile, 16 slots per stage, with the entries permuted so a lane reads
-// its 8 B operands of a K step as 4 ds_read_b128; A (the weights, private to a wave) comes from
-// global memory, one K step ahead, in the tile layout weights_kernel writes: per 32-sample tile,
-// [slot][32], sample 4g + i at position 8i + g, so a lane's 8 A operands are 64 contiguous bytes.
-// Blocks map to (sample tile, entry tile) in XCD-contiguous runs, entry tile fastest: a sample tile's
-// weights are fetched into one XCD's L2 and reused by all its entry tiles.
+// Block: 4 waves = 128 samples x 128 Gram entries (or 64 u entries); K in stages of 16 slots.  Both operands reach LDS by
+// LDS-DMA (global_load_lds_dwordx4, 1 KiB per wave instruction, no VGPRs, no VALU), double-buffered:
+// the next stage's pieces fly while this one's MFMAs run, and the stage ends with a vmcnt(0) wait and
+// one barrier.
+//   * B, the panel (shared by the 4 waves): each slot's 128 entries are one contiguous 1 KiB row of
+//     the panel (rows 16-B aligned: gemm_ldp pads the row length to even) -> one piece per slot, LDS
+//     rows padded by 64 B so the 4 slots of a K step sit on different banks.  MFMA column (eg, lane
+//     j16) is entry 8 j16 + eg of the tile, so a lane's 8 B operands are 64 contiguous bytes.
+//   * A, the weights (private to a wave): the tile layout weights_kernel writes (per 32-sample tile,
+//     [slot][32], sample 4g + i at position 8i + g), so a wave's 16 slots are 4 KiB contiguous = 4
+//     pieces, and a lane's 8 A operands of a K step are again 64 contiguous bytes.
+// Per K step a lane reads 4 + 4 ds_read_b128 and issues 64 MFMAs; the address arithmetic is
+// per-stage scalar work.  Rows past the spectrum's slots read the next rows (finite panel values; a
+// zeroed tail past the last spectrum, engine.hip) against exactly-zero weights.
+// One launch computes both products (GemmF64Args::seg): a sample tile's entry tiles are the Gram's
+// followed by u's, which read Wu and the M panel instead (uniform per block).  Blocks map to (sample
+// tile, entry tile) in XCD-contiguous runs, entry tile fastest: a sample tile's weights are fetched
+// into one XCD's L2 and reused by all its entry tiles.
+
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -32,122 +44,131 @@ namespace gpdla {
 namespace {
 
 constexpr int kFS = kGemmF64TileS;   // samples per block (4 waves x 32)
-constexpr int kFE = 128;             // entries per block
-constexpr int kFKC = 16;             // slots per LDS stage (4 K steps)
-constexpr int kFRow = kFE + 2;       // LDS row stride (doubles): rows of a K step on different banks
+constexpr int kFKC = 16;             // slots per stage (4 K steps)
+constexpr int kBRow = 128 + 8;       // LDS B row stride (doubles): one 1 KiB piece + 64 B
+constexpr int kBStage = kFKC * kBRow;
+constexpr int kAStage = kGemmF64Waves * kFKC * 32;
+constexpr int kStage = kBStage + kAStage;
+// entry tile widths: 16 kEG entries, kEG = 8 for the Gram (128 entries, one whole piece), 4 for u
+// (64: k = 50 fills 78 % of it, against 39 % of a 128-entry tile)
+constexpr int kEG0 = 8, kEG1 = 4;
+__host__ __device__ constexpr int f64_tiles(int nent, int eg) { return (nent + 16 * eg - 1) / (16 * eg); }
 
-__global__ __launch_bounds__(256, 2) void gemm_f64_kernel(GemmF64Args a) {
-  __shared__ __attribute__((aligned(16))) double Bs[2][kFKC][kFRow];
-  const int n_et = (a.nent + kFE - 1) / kFE;
+template <int kEG>
+__device__ __forceinline__ void gemm_f64_tile(const GemmF64Seg& g_, int64_t cap16, int st, int et, double* lds) {
+  constexpr int kFE = 16 * kEG;
+  const double* __restrict__ gW = g_.W;
+  const int64_t ldp = g_.ldp;
+  const int nent = g_.nent;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int kk = lane >> 4, i4 = lane & 3, j16 = lane & 15;
+  const int e_base = et * kFE;
+  const int nchunk = (int)(cap16 / kFKC);
+  const uint32_t lds_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)lds;
+  const uint32_t voff = (uint32_t)lane * 16;
+  const double* Pt = g_.P + e_base;                                        // + slot * ldp
+  const double* Wt = gW + (int64_t)(st * kGemmF64Waves + wave) * cap16 * 32;
+  constexpr int kBRowsPerWave = kFKC / kGemmF64Waves;
+
+  // a stage: 16 panel rows (one 1 KiB piece each from the tile's first entry; a 64-entry tile uses
+  // the first half) and the wave's 16 x 32 weights (4 pieces)
+  auto stage = [&](int c, int buf) {
+    const uint32_t sb = lds_base + (uint32_t)(buf * kStage * 8);
+#pragma unroll
+    for (int r = 0; r < kBRowsPerWave; ++r) {
+      const int row = wave * kBRowsPerWave + r;
+      dma_piece(Pt + ((int64_t)c * kFKC + row) * ldp, voff, sb + (uint32_t)(row * kBRow * 8));
+    }
+    const double* wsrc = Wt + (int64_t)c * kFKC * 32;
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+      dma_piece(wsrc + p * 128, voff, sb + (uint32_t)((kBStage + wave * kFKC * 32 + p * 128) * 8));
+  };
+
+  double acc[8][kEG];
+#pragma unroll
+  for (int g = 0; g < 8; ++g)
+#pragma unroll
+    for (int eg = 0; eg < kEG; ++eg) acc[g][eg] = 0.0;
+
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int c = 0; c < nchunk; ++c) {
+    const int buf = c & 1;
+    if (c + 1 < nchunk) stage(c + 1, buf ^ 1);
+    const double* Bb = lds + buf * kStage;
+    const double* Ab = Bb + kBStage + wave * kFKC * 32;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const double2* ap = reinterpret_cast<const double2*>(Ab + (4 * ks + kk) * 32 + 8 * i4);
+      const double2* bp = reinterpret_cast<const double2*>(Bb + (4 * ks + kk) * kBRow + kEG * j16);
+      double Av[8], Bv[kEG];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const double2 va = ap[q];
+        Av[2 * q] = va.x;
+        Av[2 * q + 1] = va.y;
+      }
+#pragma unroll
+      for (int q = 0; q < kEG / 2; ++q) {
+        const double2 vb = bp[q];
+        Bv[2 * q] = vb.x;
+        Bv[2 * q + 1] = vb.y;
+      }
+#pragma unroll
+      for (int g = 0; g < 8; ++g)
+#pragma unroll
+        for (int eg = 0; eg < kEG; ++eg) acc[g][eg] = __builtin_amdgcn_mfma_f64_4x4x4f64(Av[g], Bv[eg], acc[g][eg], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's pieces of the next stage
+    __syncthreads();                                     // ... and everyone's; this buffer is free
+  }
+  // D: lane 16 i + 4 b + j holds sample 4 g + (lane >> 4) and MFMA column (eg, j16), i.e. entry
+  // e_base + kEG j16 + eg, stored in the quad_index layout (every sample of the padded tile; those
+  // past sc are never read)
+  const int s_wave = st * kFS + wave * 32;
+#pragma unroll
+  for (int g = 0; g < 8; ++g) {
+    double* cg = g_.C + quad_index(s_wave + 4 * g, 0, nent) + kk;
+#pragma unroll
+    for (int eg = 0; eg < kEG; ++eg) {
+      const int e = e_base + kEG * j16 + eg;
+      if (e < nent) cg[4 * e] = acc[g][eg];
+    }
+  }
+}
+
+__global__ __launch_bounds__(64 * kGemmF64Waves, 8 / kGemmF64Waves) void gemm_f64_kernel(GemmF64Args a) {
+  __shared__ __attribute__((aligned(16))) double lds[2 * kStage];
+  const int n_et0 = f64_tiles(a.seg[0].nent, kEG0);
+  const int n_et = n_et0 + (a.nseg > 1 ? f64_tiles(a.seg[1].nent, kEG1) : 0);
   const int n_st = (a.sc + kFS - 1) / kFS;
   // XCD-contiguous runs: the dispatcher deals block b to XCD b % 8
   const int per = gridDim.x / 8;
   const int lin = (blockIdx.x % 8) * per + blockIdx.x / 8;
   if (lin >= n_st * n_et) return;
   const int st = lin / n_et, et = lin - st * n_et;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int kk = lane >> 4, i4 = lane & 3, j16 = lane & 15;
-  const int e_base = et * kFE;
-  const int64_t cap = a.cap, cap16 = a.cap16;
-  const int nchunk = (int)(cap16 / kFKC);
-
-  // A: this wave's 32-sample weight tile; lane (kk, i4) reads slot t0 + kk, positions 8 i4 .. 8 i4 + 7
-  const double* Wt = a.W + ((int64_t)(st * 4 + wave) * cap16) * 32 + kk * 32 + i4 * 8;
-  auto load_a = [&](int64_t t0, double (&r)[8]) {
-    const double2* p = reinterpret_cast<const double2*>(Wt + t0 * 32);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const double2 v = p[q];
-      r[2 * q] = v.x;
-      r[2 * q + 1] = v.y;
-    }
-  };
-  // B staging: thread -> (slot tid / 16, entries 8 (tid % 16) .. + 7) of the stage
-  const int bs_slot = tid >> 4, bs_e = (tid & 15) * 8;
-  auto load_b = [&](int c, double (&r)[8]) {
-    const int64_t t = (int64_t)c * kFKC + bs_slot;
-    const int e = e_base + bs_e;
-    const double* src = a.P + t * a.ldp + e;
-    if (t < cap && e + 8 <= a.nent) {
-#pragma unroll
-      for (int q = 0; q < 8; ++q) r[q] = src[q];
-    } else {
-#pragma unroll
-      for (int q = 0; q < 8; ++q) r[q] = (t < cap && e + q < a.nent) ? src[q] : 0.0;
-    }
-  };
-  // entry e_local lives at column 8 (e_local & 15) + (e_local >> 4): a lane's 8 entries j16 + 16 eg
-  // are 8 consecutive doubles
-  auto store_b = [&](int buf, const double (&r)[8]) {
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const int el = bs_e + q;
-      Bs[buf][bs_slot][8 * (el & 15) + (el >> 4)] = r[q];
-    }
-  };
-
-  double acc[8][8];
-#pragma unroll
-  for (int g = 0; g < 8; ++g)
-#pragma unroll
-    for (int eg = 0; eg < 8; ++eg) acc[g][eg] = 0.0;
-
-  double bst[8];
-  load_b(0, bst);
-  store_b(0, bst);
-  double A0[8], A1[8];
-  load_a(0, A0);
-  __syncthreads();
-  for (int c = 0; c < nchunk; ++c) {
-    const int buf = c & 1;
-    const bool more = c + 1 < nchunk;
-    if (more) load_b(c + 1, bst);                  // next stage, in flight during this one's MFMAs
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      double (&Ac)[8] = (ks & 1) ? A1 : A0;
-      double (&An)[8] = (ks & 1) ? A0 : A1;
-      const int64_t tn = (int64_t)c * kFKC + 4 * (ks + 1);
-      if (tn < cap16) load_a(tn, An);              // next K step's weights
-      const double2* bp = reinterpret_cast<const double2*>(&Bs[buf][4 * ks + kk][8 * j16]);
-      double Bv[8];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const double2 v = bp[q];
-        Bv[2 * q] = v.x;
-        Bv[2 * q + 1] = v.y;
-      }
-#pragma unroll
-      for (int g = 0; g < 8; ++g)
-#pragma unroll
-        for (int eg = 0; eg < 8; ++eg) acc[g][eg] = __builtin_amdgcn_mfma_f64_4x4x4f64(Ac[g], Bv[eg], acc[g][eg], 0, 0, 0);
-    }
-    if (more) store_b(buf ^ 1, bst);
-    __syncthreads();
-  }
-  // D: lane 16 i + 4 b + j holds sample 4 g + (lane >> 4), entry 16 eg + (lane & 15); in the
-  // quad_index layout a wave's store of (g, eg) is 64 consecutive doubles (every sample of the
-  // padded tile is stored; those past sc are never read)
-  const int s_wave = st * kFS + wave * 32;
-#pragma unroll
-  for (int g = 0; g < 8; ++g) {
-    double* cg = a.C + quad_index(s_wave + 4 * g, 0, a.nent) + kk;
-#pragma unroll
-    for (int eg = 0; eg < 8; ++eg) {
-      const int e = e_base + 16 * eg + j16;
-      if (e < a.nent) cg[4 * e] = acc[g][eg];
-    }
-  }
+  if (et < n_et0)
+    gemm_f64_tile<kEG0>(a.seg[0], a.cap16, st, et, lds);
+  else
+    gemm_f64_tile<kEG1>(a.seg[1], a.cap16, st, et - n_et0, lds);
 }
 
 }  // namespace
 
 hipError_t launch_gemm_f64(const GemmF64Args& a, hipStream_t s) {
-  if (a.nent < 1 || a.sc < 1 || a.cap16 % kFKC != 0 || a.cap16 < a.cap) return hipErrorInvalidValue;
-  const int64_t n_et = (a.nent + kFE - 1) / kFE, n_st = (a.sc + kFS - 1) / kFS;
+  if (a.nseg < 1 || a.nseg > 2 || a.sc < 1 || a.cap16 % kFKC != 0 || a.cap16 < a.cap) return hipErrorInvalidValue;
+  int64_t n_et = 0;
+  for (int i = 0; i < a.nseg; ++i) {
+    if (a.seg[i].nent < 1) return hipErrorInvalidValue;
+    n_et += f64_tiles(a.seg[i].nent, i == 0 ? kEG0 : kEG1);
+  }
+  const int64_t n_st = (a.sc + kFS - 1) / kFS;
   const int64_t nb = (n_et * n_st + 7) / 8 * 8;     // a multiple of 8 for the XCD runs
   if (nb > INT32_MAX) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(gemm_f64_kernel, dim3((unsigned)nb), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(gemm_f64_kernel, dim3((unsigned)nb), dim3(64 * kGemmF64Waves), 0, s, a);
   return hipGetLastError();
 }
 

@@ -52,7 +52,8 @@ __global__ __launch_bounds__(256) void convert_gemm_i8_kernel(ConvertGemmI8Args 
     const int64_t row = sb + (int64_t)g * Ls + t;
     const double* sr = a.srow + row * 8;
     const double y = sr[1], noise = sr[2], mu = sr[3], om2 = sr[4];
-    return is_u ? a.panel_m[row * K + col] * u_bound(y, mu, noise) : a.panel[row * E + col] / (om2 + noise);
+    return is_u ? a.panel_m[row * gemm_ldm(K) + col] * u_bound(y, mu, noise)
+                : a.panel[row * gemm_ldp(K) + col] / (om2 + noise);
   };
   double mx = 0.0;
   for (int t = 0; t < L; ++t) mx = fmax(mx, fabs(value(t)));
@@ -207,15 +208,6 @@ __global__ __launch_bounds__(256) void weights_i8_kernel(WeightsI8Args a) {
     a.q1p[(int64_t)sl * kWeightParts + g * kWeightQuarters + h] = q1;
     a.ldp[(int64_t)sl * kWeightParts + g * kWeightQuarters + h] = log(pm) + pe * kLn2;
   }
-}
-
-// global -> LDS DMA of one 1 KiB piece (64 lanes x 16 B, per-lane global byte offsets)
-__device__ inline void dma_piece(const uint8_t* sbase, uint32_t voffset, uint32_t lds_dst) {
-#pragma clang diagnostic push
-#pragma clang diagnostic ignored "-Winline-asm"
-  asm volatile("s_nop 4\n\ts_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2"
-               :: "s"(lds_dst), "v"(voffset), "s"(sbase) : "memory", "m0");
-#pragma clang diagnostic pop
 }
 
 constexpr int kGTileS = 128, kGTileE = 64;

@@ -184,17 +184,32 @@ __host__ __device__ inline int64_t quad_index(int64_t s, int64_t e, int64_t n) {
 // fp64 Gram / u GEMM of the panel path (gemm_f64.hip).  The weights are stored per 32-sample tile
 // as [tile][slot (cap16)][32], sample 4 g + i of the tile at position 8 i + g (weights_kernel), for
 // whole 128-sample blocks (sc rounded up to kGemmF64TileS)
-constexpr int kGemmF64TileS = 128;
+#ifndef GPDLA_F64_WAVES
+#define GPDLA_F64_WAVES 4
+#endif
+constexpr int kGemmF64Waves = GPDLA_F64_WAVES;     // waves per block, 32 samples each
+constexpr int kGemmF64TileS = 32 * kGemmF64Waves;
 __host__ __device__ inline int64_t gemm_f64_cap16(int64_t cap) { return (cap + 15) / 16 * 16; }
+// row strides (doubles) of the panel-GEMM layout's Khatri-Rao rows (k(k+1)/2 entries) and M rows
+// (k): rounded up to even so every row starts 16-B aligned for gemm_f64's LDS-DMA pieces
+__host__ __device__ inline int64_t gemm_ldp(int k) { return ((int64_t)k * (k + 1) / 2 + 1) / 2 * 2; }
+__host__ __device__ inline int64_t gemm_ldm(int k) { return ((int64_t)k + 1) / 2 * 2; }
+// doubles read past the last panel / M row by gemm_f64 (the pad rows up to cap16 and a 128-entry
+// piece starting in the last row); the engine keeps them zeroed
+__host__ __device__ inline int64_t gemm_panel_slack(int64_t ld) { return 16 * ld + 128; }
 __host__ __device__ inline int64_t gemm_f64_rows(int64_t sc) { return (sc + kGemmF64TileS - 1) / kGemmF64TileS * kGemmF64TileS; }
-struct GemmF64Args {
+struct GemmF64Seg {              // one product C = W' P of a launch
   const double* W;               // weight tiles (layout above)
   const double* P;               // [slot][ldp] this spectrum's panel rows
   int64_t ldp;                   // doubles per panel row
   int32_t nent;                  // output entries per sample (k(k+1)/2 Gram, or k u)
+  double* C;                     // quad_index(s, e, nent), for every sample of the padded tiles
+};
+struct GemmF64Args {
+  GemmF64Seg seg[2];             // Gram and u, one launch (the u entry tiles after the Gram ones)
+  int32_t nseg;
   int64_t cap, cap16;            // slots, and slots padded to 16 (the weights' tile rows)
   int32_t sc;                    // samples of the chunk
-  double* C;                     // quad_index(s, e, nent), for every sample of the padded tiles
 };
 hipError_t launch_gemm_f64(const GemmF64Args& a, hipStream_t s);
 

@@ -259,8 +259,8 @@ __global__ __launch_bounds__(256) void prep_kernel(PrepArgs a) {
       // panel-GEMM layout: Khatri-Rao row (entry (r, c) at gram_tile_index(r, c), internal.h) and M
       // row (the 8 slot scalars come from pass 3a); all zero for masked and padding slots
       const int64_t E = (int64_t)KK * (KK + 1) / 2;
-      double* pg = a.panel + (sb + j) * E;
-      double* pm = a.panel_m + (sb + j) * KK;
+      double* pg = a.panel + (sb + j) * gemm_ldp(KK);
+      double* pm = a.panel_m + (sb + j) * gemm_ldm(KK);
       for (int64_t e = lane; e < E; e += 64) {
         const int rc = s_rc[e];
         pg[e] = pix >= 0 ? Mi(rc & 255) * Mi(rc >> 8) : 0.0;
@@ -627,33 +627,41 @@ __global__ __launch_bounds__(256) void voigt_batch_kernel(const double* __restri
 
 // ---------------------------------------------------------------------------------------------
 // standalone log_mvnpdf_low_rank (the MEX drop-in; the engine fuses this into its sweeps): one
-// block of 256 threads.
+// block of 1,024 threads.
 //   * Gram and u: the pixels go through LDS in chunks of 64 rows of M, staged column by column
-//     (coalesced reads of the column-major n x k M) as M and D^-1 M; thread t owns Gram / u entries
-//     t, t + 256, ... and sums them over the chunk in pixel order (log_mvnpdf_low_rank.m:13-23).
-//   * The augmented (k+1) x (k+1) matrix [[I + Gram, u], [u', r'D^-1 r]] is factored R'R in LDS
-//     by one wave (lane = column, right-looking): its last column is t = R^-T u and its last pivot
-//     before the square root is r'D^-1 r - t't, so log det B = 2 sum_p log R_pp and the quadratic
-//     form come out of the same elimination (log_mvnpdf_low_rank.m:24-32).
+//     (coalesced reads of the column-major n x k M) as M and D^-1 M, the next chunk's values
+//     already in registers while this one is summed.  Thread t owns Gram / u entries t % 256,
+//     t % 256 + 256, ... and sums them over the chunk's pixels p = t / 256 (mod 4); the four
+//     partial sums of an entry are added at the end (log_mvnpdf_low_rank.m:13-23).
+//   * The augmented (k+1) x (k+1) matrix [[I + Gram, u], [u', r'D^-1 r]] is factored R'R in LDS,
+//     right-looking, every step's trailing update spread over the block: its last column is
+//     t = R^-T u and its last pivot before the square root is r'D^-1 r - t't, so log det B =
+//     2 sum_p log R_pp and the quadratic form come out of the same elimination
+//     (log_mvnpdf_low_rank.m:24-32).
 // ---------------------------------------------------------------------------------------------
 constexpr int kMvnMaxK = 64;
 constexpr int kMvnChunk = 64;
+constexpr int kMvnThreads = 1024;
+constexpr int kMvnPhases = kMvnThreads / 256;
 constexpr int kMvnSlots = (kMvnMaxK * (kMvnMaxK + 1) / 2 + kMvnMaxK + 255) / 256;  // entries per thread
-__global__ __launch_bounds__(256) void mvn_single_kernel(const double* __restrict__ y,
-                                                         const double* __restrict__ mu,
-                                                         const double* __restrict__ M,
-                                                         const double* __restrict__ d, int64_t n,
-                                                         int32_t k, double* out, int32_t* status) {
-  __shared__ double Ms[kMvnChunk][kMvnMaxK + 1];    // chunk rows of M (+1: bank spread)
-  __shared__ double Mw[kMvnChunk][kMvnMaxK + 2];    // the same rows scaled by 1/d; column k: r/d
-  __shared__ double A[kMvnMaxK + 1][kMvnMaxK + 2];  // augmented matrix, upper triangle
-  __shared__ double s_d4[4];
-  const int tid = threadIdx.x;
+constexpr int kMvnMPer = (kMvnChunk * kMvnMaxK + kMvnThreads - 1) / kMvnThreads;   // M values per thread
+__global__ __launch_bounds__(kMvnThreads) void mvn_single_kernel(const double* __restrict__ y,
+                                                                 const double* __restrict__ mu,
+                                                                 const double* __restrict__ M,
+                                                                 const double* __restrict__ d, int64_t n,
+                                                                 int32_t k, double* out, int32_t* status) {
+  constexpr int kMs = kMvnChunk * (kMvnMaxK + 1), kMw = kMvnChunk * (kMvnMaxK + 2);
+  __shared__ double sm[kMs + kMw];                   // chunk rows of M and of D^-1 M; column k of
+  __shared__ double A[kMvnMaxK + 1][kMvnMaxK + 2];   // the latter r/d, column k+1 1/d
+  __shared__ double s_d4[16];
+  double (*Ms)[kMvnMaxK + 1] = reinterpret_cast<double (*)[kMvnMaxK + 1]>(sm);
+  double (*Mw)[kMvnMaxK + 2] = reinterpret_cast<double (*)[kMvnMaxK + 2]>(sm + kMs);
+  const int tid = threadIdx.x, et = tid & 255, phase = tid >> 8;
   const int nent = k * (k + 1) / 2, ntot = nent + k;
-  int er[kMvnSlots], ec[kMvnSlots];                 // entry t + 256 j -> (row, column); column k = u
+  int er[kMvnSlots], ec[kMvnSlots];                 // entry et + 256 j -> (row, column); column k = u
 #pragma unroll
   for (int j = 0; j < kMvnSlots; ++j) {
-    const int e = tid + 256 * j;
+    const int e = et + 256 * j;
     if (e < nent) {
       int r = 0, start = 0;
       while (e >= start + (k - r)) { start += k - r; ++r; }
@@ -666,71 +674,108 @@ __global__ __launch_bounds__(256) void mvn_single_kernel(const double* __restric
 #pragma unroll
   for (int j = 0; j < kMvnSlots; ++j) acc[j] = 0.0;
   double q1 = 0.0, ld = 0.0;
+  // registers holding a chunk in flight: M values idx = tid + 1024 i (column idx / 64, row idx % 64)
+  // and, for the first 64 threads, the pixel's y - mu and d
+  double mreg[kMvnMPer], rreg = 0.0, dreg = 1.0;
+  auto fetch = [&](int64_t p0) {
+    const int np = (int)min<int64_t>(kMvnChunk, n - p0);
+#pragma unroll
+    for (int i = 0; i < kMvnMPer; ++i) {
+      const int idx = tid + kMvnThreads * i, c = idx / kMvnChunk, pr = idx % kMvnChunk;
+      mreg[i] = (c < k && pr < np) ? M[(p0 + pr) + (int64_t)c * n] : 0.0;
+    }
+    if (tid < kMvnChunk && tid < np) {
+      rreg = y[p0 + tid] - mu[p0 + tid];
+      dreg = d[p0 + tid];
+    }
+  };
+  if (n > 0) fetch(0);
   for (int64_t p0 = 0; p0 < n; p0 += kMvnChunk) {
     const int np = (int)min<int64_t>(kMvnChunk, n - p0);
-    __syncthreads();
+    __syncthreads();                                   // the previous chunk's sums are done
     if (tid < kMvnChunk) {
       double wi = 0.0, rwi = 0.0;
       if (tid < np) {
-        const double di = d[p0 + tid], r = y[p0 + tid] - mu[p0 + tid];
-        wi = 1.0 / di;
-        rwi = r * wi;
-        q1 += r * rwi;
-        ld += log(di);
+        wi = 1.0 / dreg;
+        rwi = rreg * wi;
+        q1 += rreg * rwi;
+        ld += log(dreg);
       }
       Mw[tid][kMvnMaxK + 1] = wi;
       Mw[tid][k] = rwi;
     }
     __syncthreads();
-    for (int idx = tid; idx < kMvnChunk * k; idx += 256) {
-      const int c = idx / kMvnChunk, pr = idx % kMvnChunk;
-      const double v = pr < np ? M[(p0 + pr) + (int64_t)c * n] : 0.0;
-      Ms[pr][c] = v;
-      Mw[pr][c] = v * Mw[pr][kMvnMaxK + 1];
+#pragma unroll
+    for (int i = 0; i < kMvnMPer; ++i) {
+      const int idx = tid + kMvnThreads * i, c = idx / kMvnChunk, pr = idx % kMvnChunk;
+      if (c < k) {
+        Ms[pr][c] = mreg[i];
+        Mw[pr][c] = mreg[i] * Mw[pr][kMvnMaxK + 1];
+      }
     }
     __syncthreads();
+    if (p0 + kMvnChunk < n) fetch(p0 + kMvnChunk);     // next chunk's loads fly during the sums
 #pragma unroll
     for (int j = 0; j < kMvnSlots; ++j) {
-      if (tid + 256 * j < ntot) {
+      if (et + 256 * j < ntot) {
         const int r = er[j], c = ec[j];
         double a = acc[j];
-        for (int pr = 0; pr < np; ++pr) a = fma(Ms[pr][r], Mw[pr][c], a);
+        for (int pr = phase; pr < np; pr += kMvnPhases) a = fma(Ms[pr][r], Mw[pr][c], a);
         acc[j] = a;
       }
     }
   }
-  q1 = block_reduce_sum(q1, s_d4);
-  ld = block_reduce_sum(ld, s_d4);
+  // q1 and sum log d live in threads 0..63 (wave 0); the 4 phases' partial entry sums meet in LDS
+  if (tid < 64) {
 #pragma unroll
-  for (int j = 0; j < kMvnSlots; ++j)
-    if (tid + 256 * j < ntot) A[er[j]][ec[j]] = acc[j] + (er[j] == ec[j] ? 1.0 : 0.0);
+    for (int off = 32; off > 0; off >>= 1) {
+      q1 += __shfl_xor(q1, off);
+      ld += __shfl_xor(ld, off);
+    }
+  }
+  __syncthreads();
+  double* red = sm;                                    // [2][kMvnSlots * 256]
+  constexpr int kRed = kMvnSlots * 256;
+  for (int half = kMvnPhases / 2; half >= 1; half >>= 1) {
+    if (phase >= half && phase < 2 * half) {
+#pragma unroll
+      for (int j = 0; j < kMvnSlots; ++j) red[(phase - half) * kRed + et + 256 * j] = acc[j];
+    }
+    __syncthreads();
+    if (phase < half) {
+#pragma unroll
+      for (int j = 0; j < kMvnSlots; ++j) acc[j] += red[phase * kRed + et + 256 * j];
+    }
+    __syncthreads();
+  }
+  if (phase == 0) {
+#pragma unroll
+    for (int j = 0; j < kMvnSlots; ++j)
+      if (et + 256 * j < ntot) A[er[j]][ec[j]] = acc[j] + (er[j] == ec[j] ? 1.0 : 0.0);
+  }
   if (tid == 0) A[k][k] = q1;
   __syncthreads();
-  if (tid >= 64) return;
-  // augmented upper Cholesky by wave 0: lane -> column c = p + 1 + lane of step p
-  const int lane = tid;
+  // augmented upper Cholesky, right-looking: row p scaled by 1/R_pp, then the trailing upper
+  // triangle (rows and columns p+1 .. k) updated by the whole block
   bool bad = false;
   double logdet = 0.0;
   for (int p = 0; p < k; ++p) {
     const double v = A[p][p];
     bad |= !(v > 0.0);
-    const double rpp = sqrt(v), irpp = 1.0 / rpp;
+    const double rpp = sqrt(v);
     logdet += log(rpp);
-    const int c = p + 1 + lane;
-    double rpc = 0.0;
-    if (c <= k) {
-      rpc = A[p][c] * irpp;
-      A[p][c] = rpc;
+    const int m = k - p;                               // columns p+1 .. k
+    __syncthreads();                                   // everyone has read A[p][p]
+    if (tid < m) A[p][p + 1 + tid] /= rpp;
+    __syncthreads();
+    for (int idx = tid; idx < m * m; idx += kMvnThreads) {
+      const int r = p + 1 + idx / m, c = p + 1 + idx % m;
+      if (r <= c) A[r][c] = fma(-A[p][r], A[p][c], A[r][c]);
     }
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-    if (c <= k)
-      for (int r = p + 1; r <= c; ++r) A[r][c] = fma(-A[p][r], rpc, A[r][c]);
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __syncthreads();
   }
-  if (lane == 0) {
-    const double quad = A[k][k];                    // r'D^-1 r - t't
+  if (tid == 0) {
+    const double quad = A[k][k];                       // r'D^-1 r - t't
     double res = -0.5 * (quad + (ld + 2 * logdet) + n * kLog2Pi);
     int st = 0;
     if (bad || !(fabs(res) < INFINITY)) {
@@ -840,7 +885,7 @@ hipError_t launch_mvn_single(const double* y, const double* mu, const double* M_
                              const double* d, int64_t n, int32_t k, double* out, int32_t* status,
                              hipStream_t s) {
   if (k > kMvnMaxK) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(mvn_single_kernel, dim3(1), dim3(256), 0, s, y, mu, M_colmajor, d, n, k,
+  hipLaunchKernelGGL(mvn_single_kernel, dim3(1), dim3(kMvnThreads), 0, s, y, mu, M_colmajor, d, n, k,
                      out, status);
   return hipGetLastError();
 }

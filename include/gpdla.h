@@ -138,7 +138,7 @@ typedef struct gpdla_stats {
   double prep_ms, likelihood_ms, reduce_ms;
   int64_t prep_launches, likelihood_launches, reduce_launches;
   int64_t spectra, sample_evals;       /* sample_evals = sum over spectra of S (null evals excluded) */
-  double contraction_ms;               /* int8 panel-GEMM path: the gemm_i8 launches (part of likelihood_ms) */
+  double contraction_ms;               /* panel-GEMM paths: the Gram/u GEMM launches (part of likelihood_ms) */
   int64_t contraction_launches;
 } gpdla_stats;
 
