@@ -271,6 +271,26 @@ __device__ inline double raw_profile3(double lam, const double (&afac)[3], doubl
   return exp_tab64(N * total, exp_lds);
 }
 
+// The fix-up lanes of the batched sweeps (some |x_j| < kOuterX): the nearest line j, |x_j| and T_j,
+// and its kWingStride block.  At most one line can be that close: the Lyman lines are >= 5% apart
+// in wavelength (>= 16,000 km/s) and kOuterX is 32 Doppler units (411 km/s), so the other two
+// lines' outer-wing values stand.
+__device__ inline void nearest_line(double lam, const double (&afac)[3], double T0, double T1, double T2,
+                                    const double* __restrict__ wing_lds, double& ax, double& T,
+                                    const double*& wl, int& j) {
+  const double a0 = fabs(fma(lam, afac[0], -kC2)), a1 = fabs(fma(lam, afac[1], -kC2)),
+               a2 = fabs(fma(lam, afac[2], -kC2));
+  const bool p1 = a1 < a0;
+  ax = p1 ? a1 : a0;
+  T = p1 ? T1 : T0;
+  j = p1 ? 1 : 0;
+  const bool p2 = a2 < ax;
+  ax = p2 ? a2 : ax;
+  T = p2 ? T2 : T;
+  j = p2 ? 2 : j;
+  wl = wing_lds + j * kWingStride;
+}
+
 // raw_profile3 with the three damping-wing T_j = 1/x_j^2 from ONE v_rcp_f64 (wing_T3) instead of
 // three (+ their Newton steps) and the outer wing polynomial; lanes with |x_j| < kOuterX take the
 // inner wing, lanes with |x_j| < kCoreX the core polynomial (their T_j may be inf/NaN and are

@@ -402,8 +402,8 @@ __global__ __launch_bounds__(256, (K <= 20 ? 2 : 1)) void likelihood_kernel(Like
     if (c + 1 < nchunks)
       stage_chunk<K>(panel, Ls, c + 1, lds_base + (uint32_t)(((c + 1) & 1) * kBuf * 8), wave_s, voff);
     // raw profiles of the chunk's 4 steps first: branch-free outer damping wings (one basic block,
-    // so the 4 chains interleave), a rare fix-up for lanes with |x| < kOuterX (core or inner wing,
-    // raw_profile3's evaluation), then the 4 table exps
+    // so the 4 chains interleave), a rare fix-up for lanes with |x| < kOuterX (the nearest line's
+    // inner wing or core, nearest_line), then the 4 table exps
     double rwv[kChunkSteps];
     if constexpr (NL == 3) {
       double tot[kChunkSteps], lamc[kChunkSteps];
@@ -437,18 +437,23 @@ __global__ __launch_bounds__(256, (K <= 20 ? 2 : 1)) void likelihood_kernel(Like
 #pragma unroll
         for (int tt = 0; tt < kChunkSteps; ++tt) {
           if (cm & (1u << tt)) {
-            double t = 0.0;
+            double ax, T;
+            const double* wl;
+            int j;
+            nearest_line(lamc[tt], afac, Tj[0][tt], Tj[1][tt], Tj[2][tt], wing_lds, ax, T, wl, j);
+            if (ax >= kCoreX) {
+              // inner wing: the line's outer value swapped for its wing polynomial (both finite and
+              // of the same size here, so the swap costs no precision)
+              tot[tt] += outer_poly(wl, T) - wing_poly(wl, T);
+            } else {
+              // core: this line's outer value is meaningless (T_j up to 2^1000), so the sum is
+              // rebuilt from the other two lines' outer wings and this line's core polynomial
+              const double cf = core_eval(core_lds + j * kCoreTable, ax);
+              double t = 0.0;
 #pragma unroll
-            for (int j = 0; j < 3; ++j) {
-              const double x = fma(lamc[tt], afac[j], -kC2);
-              const double ax = fabs(x);
-              // inner wing from the shared T_j (exact enough for |x| >= kCoreX; huge in the core,
-              // where the select below discards it): +0.9% against its own rcp (profiles/r3g)
-              double f = wing_poly(wing_lds + j * kWingStride, Tj[j][tt]);
-              if (ax < kCoreX) f = core_eval(core_lds + j * kCoreTable, ax);
-              t -= f;
+              for (int jj = 0; jj < 3; ++jj) t -= jj == j ? cf : outer_poly(wing_lds + jj * kWingStride, Tj[jj][tt]);
+              tot[tt] = t;
             }
-            tot[tt] = t;
           }
         }
       }
