@@ -317,6 +317,56 @@ __device__ inline double raw_profile3_t3(double lam, const double (&afac)[3], do
   return exp_tab64(N * total, exp_lds);
 }
 
+// Raw profiles of NB pixels at once, the batched sweeps' scheme: branch-free outer damping wings for
+// every lane and line (one basic block, so the NB chains interleave), ONE wave-level fix-up branch for
+// lanes with some |x_j| < kOuterX (the nearest line only, nearest_line), then the NB table exps.
+// Same arithmetic as the fused kernel's chunk (kernels.hip likelihood_kernel).
+template <int NB>
+__device__ inline void raw_profile3_batch(const double (&lam)[NB], const double (&afac)[3], double N,
+                                          const double* __restrict__ core_lds,
+                                          const double* __restrict__ wing_lds,
+                                          const double* __restrict__ exp_lds, double (&out)[NB]) {
+  double tot[NB], Tj[3][NB];
+  uint32_t cm = 0;
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    const double x0 = fma(lam[b], afac[0], -kC2), x1 = fma(lam[b], afac[1], -kC2), x2 = fma(lam[b], afac[2], -kC2);
+    cm |= (((fabs(x0) < kOuterX) | (fabs(x1) < kOuterX) | (fabs(x2) < kOuterX)) ? 1u : 0u) << b;
+    wing_T3(x0, x1, x2, Tj[0][b], Tj[1][b], Tj[2][b]);
+    tot[b] = 0.0;
+  }
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    int zoff;
+    asm volatile("s_mov_b32 %0, 0" : "=s"(zoff));  // one line's coefficients live at a time
+    const double* wl = wing_lds + zoff + j * kWingStride;
+#pragma unroll
+    for (int b = 0; b < NB; ++b) tot[b] -= outer_poly(wl, Tj[j][b]);
+  }
+  if (cm) {
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      if (cm & (1u << b)) {
+        double ax, T;
+        const double* wl;
+        int j;
+        nearest_line(lam[b], afac, Tj[0][b], Tj[1][b], Tj[2][b], wing_lds, ax, T, wl, j);
+        if (ax >= kCoreX) {
+          tot[b] += outer_poly(wl, T) - wing_poly(wl, T);
+        } else {
+          const double cf = core_eval(core_lds + j * kCoreTable, ax);
+          double t = 0.0;
+#pragma unroll
+          for (int jj = 0; jj < 3; ++jj) t -= jj == j ? cf : outer_poly(wing_lds + jj * kWingStride, Tj[jj][b]);
+          tot[b] = t;
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int b = 0; b < NB; ++b) out[b] = exp_tab64(N * tot[b], exp_lds);
+}
+
 // ---------------------------------------------------------------------------------------------
 // Per-sample augmented LDL^T in registers, one quad of lanes per sample.
 //   Lane jq of the quad owns Gram columns c = 4jj + jq (rows 0..4jj+3, A[jj][i]) and u rows

@@ -155,40 +155,49 @@ __global__ __launch_bounds__(256) void weights_i8_kernel(WeightsI8Args a) {
   // byte offset of 16-slot group G (= K index / 16), plane i
   auto goff = [&](int G, int i) { return ((int64_t)((G >> 2) * 4 + i) * 4 + (G & 3)) * 2048; };
   for (int tg = t0; tg < t1; tg += 16) {
-    // per slot as the fp64 weights kernel (its core branch is coherent: a block's 64 samples are
-    // consecutive in z), 16 slots' quantised weights collected for the digit planes
+    // 16 slots' quantised weights collected for the digit planes, the raw profiles 4 slots at a time
+    // (raw_profile3_batch: one fix-up branch per 4 slots; a block's 64 samples are consecutive in z)
     uint32_t xg[16], xu[16];
 #pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      const int t = tg + e;
+    for (int qb = 0; qb < 16 / kWB; ++qb) {
       // neutral past the segment (quantisation scales as prep_kernel computes them for y = mu = om2 = 0,
       // noise = 1: u_bound = 1)
-      double lam, y = 0.0, noise = 1.0, mu = 0.0, om2 = 0.0, su = kI8ScaleU, sg = kI8ScaleG;
-      if (t < L) {
-        const double* sr = a.srow + ((int64_t)g * Ls + t) * 8;
-        lam = sr[0]; y = sr[1]; noise = sr[2]; mu = sr[3]; om2 = sr[4]; su = sr[6]; sg = sr[7];
-      } else {
-        lam = a.lam_pad[(int64_t)g * L + t + 2 * kWidth];
+      double lam[kWB], w6v[kWB];
+#pragma unroll
+      for (int b = 0; b < kWB; ++b) {
+        const int t = tg + kWB * qb + b;
+        lam[b] = t < L ? a.srow[((int64_t)g * Ls + t) * 8] : a.lam_pad[(int64_t)g * L + t + 2 * kWidth];
       }
-      const double w6 = raw(lam);
-      double ab = w0 * kInstrumentProfile[0];  // voigt.c:297-299
-      ab = fma(w1, kInstrumentProfile[1], ab);
-      ab = fma(w2, kInstrumentProfile[2], ab);
-      ab = fma(w3, kInstrumentProfile[3], ab);
-      ab = fma(w4, kInstrumentProfile[4], ab);
-      ab = fma(w5, kInstrumentProfile[5], ab);
-      ab = fma(w6, kInstrumentProfile[6], ab);
-      w0 = w1; w1 = w2; w2 = w3; w3 = w4; w4 = w5; w5 = w6;
-      const double r = fma(-mu, ab, y);  // process_qsos.m:191-197, log_mvnpdf_low_rank.m:11-15
-      const double a2 = ab * ab;
-      const double d = fma(om2, a2, noise);
-      const double dinv = rcp_sweep(d);
-      const double rd = r * dinv;
-      q1 = fma(r, rd, q1);
-      pm *= d;
-      xg[e] = (uint32_t)__builtin_rint(a2 * dinv * sg) ^ 0x80808080u;
-      xu[e] = (uint32_t)__builtin_rint(fma(ab * rd, su, 0x1p31)) ^ 0x80808080u;
-      asm volatile("" : "+v"(xg[e]), "+v"(xu[e]), "+v"(q1), "+v"(pm));  // no sinking across slots
+      raw_profile3_batch<kWB>(lam, afac, N, core_lds, wing_lds, exp_lds, w6v);
+#pragma unroll
+      for (int b = 0; b < kWB; ++b) {
+        const int e = kWB * qb + b;
+        const int t = tg + e;
+        double y = 0.0, noise = 1.0, mu = 0.0, om2 = 0.0, su = kI8ScaleU, sg = kI8ScaleG;
+        if (t < L) {
+          const double* sr = a.srow + ((int64_t)g * Ls + t) * 8;
+          y = sr[1]; noise = sr[2]; mu = sr[3]; om2 = sr[4]; su = sr[6]; sg = sr[7];
+        }
+        const double w6 = w6v[b];
+        double ab = w0 * kInstrumentProfile[0];  // voigt.c:297-299
+        ab = fma(w1, kInstrumentProfile[1], ab);
+        ab = fma(w2, kInstrumentProfile[2], ab);
+        ab = fma(w3, kInstrumentProfile[3], ab);
+        ab = fma(w4, kInstrumentProfile[4], ab);
+        ab = fma(w5, kInstrumentProfile[5], ab);
+        ab = fma(w6, kInstrumentProfile[6], ab);
+        w0 = w1; w1 = w2; w2 = w3; w3 = w4; w4 = w5; w5 = w6;
+        const double r = fma(-mu, ab, y);  // process_qsos.m:191-197, log_mvnpdf_low_rank.m:11-15
+        const double a2 = ab * ab;
+        const double d = fma(om2, a2, noise);
+        const double dinv = rcp_sweep(d);
+        const double rd = r * dinv;
+        q1 = fma(r, rd, q1);
+        pm *= d;
+        xg[e] = (uint32_t)__builtin_rint(a2 * dinv * sg) ^ 0x80808080u;
+        xu[e] = (uint32_t)__builtin_rint(fma(ab * rd, su, 0x1p31)) ^ 0x80808080u;
+        asm volatile("" : "+v"(xg[e]), "+v"(xu[e]), "+v"(q1), "+v"(pm));  // no sinking across slots
+      }
     }
     {
       int ex;

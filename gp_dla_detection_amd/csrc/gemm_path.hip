@@ -76,33 +76,48 @@ __global__ __launch_bounds__(256) void weights_kernel(WeightsArgs a) {
   const int sloc = sl & 31;
   double* wg_t = a.wg + (int64_t)(sl >> 5) * cap16 * 32 + 8 * (sloc & 3) + (sloc >> 2);
   double* wu_t = a.wu + (wg_t - a.wg);
-  for (int t = t0; t < t0 + Lq; ++t) {
-    const int64_t slot = (int64_t)g * Ls + t;
-    const double* sr = a.srow + slot * 8;
-    const double lam = sr[0], y = sr[1], noise = sr[2], mu = sr[3], om2 = sr[4];
-    const double w6 = raw(lam);
-    double ab = w0 * kInstrumentProfile[0];  // voigt.c:297-299
-    ab = fma(w1, kInstrumentProfile[1], ab);
-    ab = fma(w2, kInstrumentProfile[2], ab);
-    ab = fma(w3, kInstrumentProfile[3], ab);
-    ab = fma(w4, kInstrumentProfile[4], ab);
-    ab = fma(w5, kInstrumentProfile[5], ab);
-    ab = fma(w6, kInstrumentProfile[6], ab);
-    w0 = w1; w1 = w2; w2 = w3; w3 = w4; w4 = w5; w5 = w6;
-    const double r = fma(-mu, ab, y);  // process_qsos.m:191-197, log_mvnpdf_low_rank.m:11-15
-    const double a2 = ab * ab;
-    const double d = fma(om2, a2, noise);
-    const double dinv = rcp_sweep(d);
-    const double rd = r * dinv;
-    q1 = fma(r, rd, q1);
-    pm *= d;
-    if (((t - t0) & 3) == 3) {
-      int ex;
-      pm = frexp(pm, &ex);
-      pe += ex;
+  // the raw profiles go kWB slots at a time for the 3-line set (raw_profile3_batch: one fix-up branch
+  // per batch); a batch past the quarter's last slot evaluates a valid wavelength and drops it
+  constexpr int kB = NL == 3 ? kWB : 1;
+  for (int t = t0; t < t0 + Lq; t += kB) {
+    double lamb[kB], w6v[kB];
+#pragma unroll
+    for (int b = 0; b < kB; ++b) lamb[b] = t + b < t0 + Lq ? a.srow[((int64_t)g * Ls + t + b) * 8] : lamp[0];
+    if constexpr (NL == 3) {
+      raw_profile3_batch<kB>(lamb, afac, N, core_lds, wing_lds, exp_lds, w6v);
+    } else {
+      w6v[0] = raw(lamb[0]);
     }
-    wg_t[slot * 32] = a2 * dinv;
-    wu_t[slot * 32] = ab * rd;
+#pragma unroll
+    for (int b = 0; b < kB; ++b) {
+      if (t + b >= t0 + Lq) break;
+      const int64_t slot = (int64_t)g * Ls + t + b;
+      const double* sr = a.srow + slot * 8;
+      const double y = sr[1], noise = sr[2], mu = sr[3], om2 = sr[4];
+      const double w6 = w6v[b];
+      double ab = w0 * kInstrumentProfile[0];  // voigt.c:297-299
+      ab = fma(w1, kInstrumentProfile[1], ab);
+      ab = fma(w2, kInstrumentProfile[2], ab);
+      ab = fma(w3, kInstrumentProfile[3], ab);
+      ab = fma(w4, kInstrumentProfile[4], ab);
+      ab = fma(w5, kInstrumentProfile[5], ab);
+      ab = fma(w6, kInstrumentProfile[6], ab);
+      w0 = w1; w1 = w2; w2 = w3; w3 = w4; w4 = w5; w5 = w6;
+      const double r = fma(-mu, ab, y);  // process_qsos.m:191-197, log_mvnpdf_low_rank.m:11-15
+      const double a2 = ab * ab;
+      const double d = fma(om2, a2, noise);
+      const double dinv = rcp_sweep(d);
+      const double rd = r * dinv;
+      q1 = fma(r, rd, q1);
+      pm *= d;
+      if (((t + b - t0) & 3) == 3) {
+        int ex;
+        pm = frexp(pm, &ex);
+        pe += ex;
+      }
+      wg_t[slot * 32] = a2 * dinv;
+      wu_t[slot * 32] = ab * rd;
+    }
   }
   // slots past the 4 segments (capacity slack, and the GEMM's padding to 16) are neutral: weight 0
   if (h == 0) {

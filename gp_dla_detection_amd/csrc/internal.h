@@ -132,6 +132,9 @@ struct LineArgs {
 // ---- panel-GEMM path (any rank 1..kGemmMaxK; gemm_path.hip + gemm_f64.hip or gemm_i8.hip)
 constexpr int kGemmMaxK = 64;
 constexpr int kWeightQuarters = 4;                 // weights_kernel: waves per segment
+// weights kernels: raw profiles per fix-up branch (raw_profile3_batch).  configs[4] A/B: 2 beats 1 and
+// 4 (4 needs more registers than 4 waves per SIMD allow; profiles/r4k)
+constexpr int kWB = 2;
 constexpr int kWeightParts = 4 * kWeightQuarters;  // per-sample partial sums (segment x quarter)
 
 struct WeightsArgs {
