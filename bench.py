@@ -258,9 +258,11 @@ def run_e2e(args, world: int, rank: int, local_rank: int, dist) -> None:
 
 
 # rocprofv3 summaries of the bench workloads (tools/profile.sh + tools/summarize_profile.py), committed
-PROFILE_SUMMARY = ROOT / "profiles" / "r3i_summary.json"        # configs[1], fused fp64
-PROFILE_SUMMARY_C5 = {"panel-GEMM-int8": ROOT / "profiles" / "r2a_c5_summary.json",      # configs[4], 32-bit
-                      "panel-GEMM-int8-24": ROOT / "profiles" / "r3i_c5_summary.json"}   # configs[4], 24-bit
+PROFILE_SUMMARY = ROOT / "profiles" / "r4z_c2_summary.json"     # configs[1], fused fp64
+# configs[4]: summary file and the roofline kernel's name
+PROFILE_SUMMARY_C5 = {"panel-GEMM-int8": (ROOT / "profiles" / "r2a_c5_summary.json", "gemm_i8_kernel"),      # 32-bit
+                      "panel-GEMM-int8-24": (ROOT / "profiles" / "r4z_c5_summary.json", "gemm_i8_kernel"),  # 24-bit
+                      "panel-GEMM": (ROOT / "profiles" / "r4z_c5f64_summary.json", "gemm_f64_kernel")}     # fp64
 
 
 def profiled_traffic(Q: int, S: int, k: int, path: str = "fused"):
@@ -269,12 +271,12 @@ def profiled_traffic(Q: int, S: int, k: int, path: str = "fused"):
     hits): the fused kernel for configs[1]; for configs[4] the int8 GEMM launches of one spectrum and
     sample chunk (the Gram and u launches of the 24-bit path together).  None for other workloads or
     if no summary is present."""
-    if (Q, S, k) == (128, 100000, 50) and path in PROFILE_SUMMARY_C5 and PROFILE_SUMMARY_C5[path].exists():
-        f = PROFILE_SUMMARY_C5[path]
+    if (Q, S, k) == (128, 100000, 50) and path in PROFILE_SUMMARY_C5 and PROFILE_SUMMARY_C5[path][0].exists():
+        f, kname = PROFILE_SUMMARY_C5[path]
         d = json.loads(f.read_text())
-        rows = [e for e in d["kernels"] if "gemm_i8_kernel" in e["kernel"] and "hbm_bytes_per_launch" in e]
+        rows = [e for e in d["kernels"] if kname in e["kernel"] and "hbm_bytes_per_launch" in e]
         if rows:
-            return sum(e["hbm_bytes_per_launch"] for e in rows), f"{f.relative_to(ROOT)} (rocprofv3 PMC, gemm_i8 launches)"
+            return sum(e["hbm_bytes_per_launch"] for e in rows), f"{f.relative_to(ROOT)} (rocprofv3 PMC, {kname} launches)"
         return None, None
     if (Q, S, k) != (1024, 10000, 20) or path != "fused" or not PROFILE_SUMMARY.exists():
         return None, None
