@@ -13,6 +13,7 @@
 
 #include <cmath>
 #include <cstdint>
+#include <type_traits>
 
 #include "device_common.h"
 #include "internal.h"
@@ -192,51 +193,94 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT <= 13 ? 
     q1 += __shfl_xor(q1, m);
     logdet_d += __shfl_xor(logdet_d, m);
   }
-  // Load the tiles: straight-line code (unconditional loads from valid addresses, then selects), so
-  // the NT (NT + 1) / 2 loads go out back to back.  Since 4 (NT - 1) <= k, only the last tile
-  // column (I = NT - 1) holds the u column (c = k), r'D^-1 r (r = c = k) and identity padding
-  // (c > k); every other tile is Gram only.  Gram offsets follow gram_tile_index (internal.h): a
-  // compile-time tile base plus a per-lane position inside the tile.
+  // Load the tiles: straight-line code (unconditional loads from valid addresses), all issued up
+  // front in row order; a row's values are formed only when its step comes (below), so the
+  // factorisation of row J runs while rows > J are still in flight (the compiler's vmcnt waits count
+  // only the loads before them).  Since 4 (NT - 1) <= k, only the last tile column (I = NT - 1) holds
+  // the u column (c = k), r'D^-1 r (r = c = k) and identity padding (c > k); every other tile is
+  // Gram only.  Gram offsets follow gram_tile_index (internal.h): a compile-time tile base plus a
+  // per-lane position inside the tile.
   const int di = min(ti, tj), dj = max(ti, tj);            // diagonal tiles: upper-triangle slot
   const int ldiag = di * 4 - di * (di - 1) / 2 + (dj - di), loff = 4 * ti + tj;
   const double done = ti == tj ? 1.0 : 0.0;
   const int w = K - 4 * (NT - 1);                           // Gram columns in the last tile column
   constexpr int base2 = 10 * (NT - 1) + 8 * (NT - 1) * (NT - 2);
-  double T[NTT];  // tile (L, I), L <= I, at L NT - L (L - 1) / 2 + (I - L)
+  // fp64 Gram: the last tile column's u entries come through the same register (a per-lane address
+  // select, so one load per tile); fp32 Gram: u is loaded beside it
+  constexpr bool kOneLoad = std::is_same<GT, double>::value;
+  GT graw[NTT];   // tile (L, I), L <= I, at L NT - L (L - 1) / 2 + (I - L)
+  double uraw[NT];
 #pragma unroll
   for (int L = 0; L < NT; ++L) {
 #pragma unroll
     for (int I = L; I < NT; ++I) {
-      double v;
+      GT g;
       if (I < NT - 1) {
         const int tb = 10 * L + 16 * (L * (NT - 2) - L * (L - 1) / 2) + (I == L ? 0 : 10 + 16 * (I - L - 1));
-        v = I == L ? (double)Gs[4 * (tb + ldiag)] + done : (double)Gs[4 * (tb + loff)];   // B = I + Gram
-      } else if (L < NT - 1) {
-        // rows 4L + ti < k, column c = 4 (NT - 1) + tj: Gram if tj < w, u if tj == w, padding after
-        const int r = 4 * L + ti;
-        const double g = (double)Gs[4 * (base2 + L * 4 * w + ti * w + min(tj, max(w - 1, 0)))], u = Us[4 * r];
-        v = tj < w ? g : (tj == w ? u : 0.0);
+        g = Gs[4 * (tb + (I == L ? ldiag : loff))];
       } else {
-        // corner tile: Gram (di <= dj < w), then u (dj == w, di < w), r'D^-1 r (di == dj == w),
-        // identity padding
-        const int r = 4 * L + di;
-        const int cw = max(w, 1);
-        const double g = (double)Gs[4 * (base2 + L * 4 * w + min(di, cw - 1) * w - min(di, cw - 1) * (min(di, cw - 1) - 1) / 2 +
-                                         (min(dj, cw - 1) - min(di, cw - 1)))];
-        const double u = Us[4 * min(r, K - 1)];
-        v = dj < w ? g + done : (dj == w ? (di < w ? u : q1) : done);
+        const GT* gp;
+        const double* up;
+        if (L < NT - 1) {
+          gp = Gs + 4 * (base2 + L * 4 * w + ti * w + min(tj, max(w - 1, 0)));
+          up = Us + 4 * (4 * L + ti);
+        } else {
+          const int cw = max(w, 1), dm = min(di, cw - 1);
+          gp = Gs + 4 * (base2 + L * 4 * w + dm * w - dm * (dm - 1) / 2 + (min(dj, cw - 1) - dm));
+          up = Us + 4 * min(4 * L + di, K - 1);
+        }
+        if constexpr (kOneLoad) {
+          const bool take_u = L < NT - 1 ? tj == w : (dj == w && di < w);
+          g = *(take_u ? reinterpret_cast<const GT*>(up) : gp);
+        } else {
+          g = *gp;
+          uraw[L] = *up;
+        }
       }
-      T[L * NT - L * (L - 1) / 2 + (I - L)] = v;
+      graw[L * NT - L * (L - 1) / 2 + (I - L)] = g;
     }
   }
+  // the augmented matrix's tile (L, I) from the loaded values: B = I + Gram, then the u column,
+  // r'D^-1 r and identity padding in the last tile column
+  auto tile_value = [&](int L, int I) -> double {
+    GT g = graw[L * NT - L * (L - 1) / 2 + (I - L)];
+    asm volatile("" : "+v"(g));        // formed here, at its row's step, not where it was loaded
+    if (I < NT - 1) return I == L ? (double)g + done : (double)g;
+    double u;
+    if constexpr (kOneLoad) {
+      u = (double)g;
+    } else {
+      u = uraw[L];
+      asm volatile("" : "+v"(u));
+    }
+    if (L < NT - 1) return tj < w ? (double)g : (tj == w ? u : 0.0);
+    return dj < w ? (double)g + done : (dj == w ? (di < w ? u : q1) : done);
+  };
+  double T[NTT];
+  double inv_p[NT];  // this lane's element of S_PP^-1 per finished block row P
   double pb = 1.0;  // prod_{p<k} D_p = pb 2^eb
   int eb = 0;
   double quad = 0.0;
   bool bad = false;
+  // Left-looking block elimination: row J gets the updates of every finished row P < J, in the order
+  // P = 0, 1, ... -- the same MFMAs, operands and accumulation order as the right-looking sweep, so
+  // the results are bitwise those of it -- then its diagonal tile is factored.
 #pragma unroll
   for (int J = 0; J < NT; ++J) {
-    // ---- diagonal tile -> LDS -> every lane of the sample
     const int jj = J * NT - J * (J - 1) / 2;
+#pragma unroll
+    for (int I = J; I < NT; ++I) T[jj + (I - J)] = tile_value(J, I);
+#pragma unroll
+    for (int P = 0; P < J; ++P) {
+      const int pp = P * NT - P * (P - 1) / 2;
+      const double x = -__builtin_amdgcn_mfma_f64_4x4x4f64(inv_p[P], T[pp + (J - P)], 0.0, 0, 0, 0);
+#pragma unroll
+      for (int I = J; I < NT; ++I) {
+        double& t = T[jj + (I - J)];
+        t = __builtin_amdgcn_mfma_f64_4x4x4f64(x, T[pp + (I - P)], t, 0, 0, 0);
+      }
+    }
+    // ---- diagonal tile -> LDS -> every lane of the sample
     double* diag = diag_all[wave][J & 1];
     diag[b * 16 + ti * 4 + tj] = T[jj];
     wave_sync();
@@ -283,18 +327,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT <= 13 ? 
                  y3 = fma(-l32, y2, fma(-l31, y1, fma(-l30, y0, e3)));
     const double x3 = y3 * i3, x2 = fma(-l32, x3, y2 * i2), x1 = fma(-l31, x3, fma(-l21, x2, y1 * i1)),
                  x0 = fma(-l30, x3, fma(-l20, x2, fma(-l10, x1, y0 * i0)));
-    const double inv = tj == 0 ? x0 : (tj == 1 ? x1 : (tj == 2 ? x2 : x3));
-    // ---- per block row L > J (the next diagonal tile's row first): X_L = S_JJ^-1 S(J, L), then
-    //      S(L, I) -= X_L' S(J, I) for I >= L; X_L lives only for its row
-#pragma unroll
-    for (int L = J + 1; L < NT; ++L) {
-      const double x = -__builtin_amdgcn_mfma_f64_4x4x4f64(inv, T[jj + (L - J)], 0.0, 0, 0, 0);
-#pragma unroll
-      for (int I = L; I < NT; ++I) {
-        double& t = T[L * NT - L * (L - 1) / 2 + (I - L)];
-        t = __builtin_amdgcn_mfma_f64_4x4x4f64(x, T[jj + (I - J)], t, 0, 0, 0);
-      }
-    }
+    inv_p[J] = tj == 0 ? x0 : (tj == 1 ? x1 : (tj == 2 ? x2 : x3));
   }
   const double logdet_b = log(pb) + eb * kLn2;
   double ll = -0.5 * (quad + (logdet_d + logdet_b) + inf.n * kLog2Pi);  // log_mvnpdf_low_rank.m:30-32
