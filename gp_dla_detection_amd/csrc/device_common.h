@@ -36,6 +36,40 @@ __device__ inline double rcp_sweep(double d) {
   return fma(r, fma(-d, r, 1.0), r);
 }
 
+// 1/q_0 .. 1/q_3 from ONE v_rcp_f64 (+ Newton step) of the product q_0 q_1 q_2 q_3 (Montgomery's
+// trick): the same instruction count as four rcp_sweep, three fewer quarter-rate reciprocals.  The
+// product must stay a normal double (callers bound their q_i).
+__device__ inline void batch_rcp4(const double (&q)[4], double (&iq)[4]) {
+  const double q01 = q[0] * q[1], q23 = q[2] * q[3];
+  const double P = q01 * q23;
+  double R = __builtin_amdgcn_rcp(P);
+  R = fma(R, fma(-P, R, 1.0), R);
+  const double R23 = R * q23, R01 = R * q01;
+  iq[0] = R23 * q[1];
+  iq[1] = R23 * q[0];
+  iq[2] = R01 * q[3];
+  iq[3] = R01 * q[2];
+}
+
+// batch_rcp4 for unbounded positive q_i (the per-pixel d = omega^2 a^2 + sigma^2): when the product
+// leaves [2^-1000, 2^1000] (a d outside ~[1e-75, 1e75]) the wave takes four rcp_sweep instead.
+__device__ inline void batch_rcp4_guarded(const double (&q)[4], double (&iq)[4]) {
+  const double q01 = q[0] * q[1], q23 = q[2] * q[3];
+  const double P = q01 * q23;
+  if (__builtin_expect(!(P > 0x1p-1000 && P < 0x1p1000), 0)) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) iq[i] = rcp_sweep(q[i]);
+    return;
+  }
+  double R = __builtin_amdgcn_rcp(P);
+  R = fma(R, fma(-P, R, 1.0), R);
+  const double R23 = R * q23, R01 = R * q01;
+  iq[0] = R23 * q[1];
+  iq[1] = R23 * q[0];
+  iq[2] = R01 * q[3];
+  iq[3] = R01 * q[2];
+}
+
 // global -> LDS DMA of one 1 KiB piece (64 lanes x 16 B, per-lane global byte offsets from a
 // wave-uniform base), issued from inline asm so the compiler's waitcnt pass does not drain it before
 // unrelated LDS reads; the consumer waits with an explicit s_waitcnt vmcnt + barrier.  s_nop 4: a
@@ -101,6 +135,27 @@ __device__ inline double exp_tab64(double v, const double* __restrict__ tab) {
   p = fma(p, r, 1.0);
   p = fma(p, r, 1.0);
   return __builtin_ldexp(p * tab[ki & 63], ki >> 6);
+}
+
+// exp_tab64 on a 128-entry table: v = (128 m + j) ln2/128 + r, |r| <= ln2/256, and e^r by a degree-4
+// minimax polynomial on that interval (relative error 7.6e-17, Remez fit: tools/fit_exp_poly.py), one
+// FMA fewer than exp_tab64.  No clamp of v: callers guarantee v >= -2^31 ln2/128 (k then fits an
+// int; below -745 the ldexp underflows to +0 like exp).  The fused fp64 sweep clamps only its
+// core-zone lanes, and every lane of a wave whose N_HI could take the wings alone past that bound.
+__device__ inline double exp_tab128_nc(double v, const double* __restrict__ tab) {
+  constexpr double kInvL = 184.6649652337873;              // 128 / ln 2
+  constexpr double kLhi = 0x1.62e42fefp-8;                 // ln2/128 to 33 bits (k*kLhi exact)
+  constexpr double kLlo = 5.812982117197185e-13;           // ln2/128 - kLhi
+  const double kd = fma(v, kInvL, 0x1.8p52);
+  const int ki = __double2loint(kd);
+  const double k = kd - 0x1.8p52;
+  double r = fma(-k, kLhi, v);
+  r = fma(-k, kLlo, r);
+  double p = fma(r, 0.04166665394028975, 0.16666674303258167);
+  p = fma(p, r, 0.5000000000001633);
+  p = fma(p, r, 0.99999999999986);
+  p = fma(p, r, 1.0);
+  return __builtin_ldexp(p * tab[ki & 127], ki >> 7);
 }
 
 // T_j = 1/x_j^2 of the three Lyman lines with ONE v_rcp_f64 (+ Newton step) on x0^2 x1^2 x2^2
@@ -255,6 +310,8 @@ __device__ inline double raw_profile(double lam, double zfac, double N, int num_
 // 3-line fast path (Lyman alpha, beta, gamma; set_parameters.m:63): the damping wing is
 // evaluated branch-free for every lane with its coefficients read from LDS by broadcast
 // (wing_lds), the core polynomial (LDS tables) only by the lanes with |x| < kCoreX.
+// TAB = the exp table in exp_lds: 64 entries (exp_tab64) or 128 (exp_tab128_nc, clamped here).
+template <int TAB = 64>
 __device__ inline double raw_profile3(double lam, const double (&afac)[3], double N,
                                       const double* __restrict__ core_lds,
                                       const double* __restrict__ wing_lds,
@@ -268,7 +325,8 @@ __device__ inline double raw_profile3(double lam, const double (&afac)[3], doubl
     if (ax < kCoreX) f = core_eval(core_lds + j * kCoreTable, ax);
     total -= f;
   }
-  return exp_tab64(N * total, exp_lds);
+  if constexpr (TAB == 128) return exp_tab128_nc(fmax(N * total, -1100.0), exp_lds);
+  else return exp_tab64(N * total, exp_lds);
 }
 
 // The fix-up lanes of the batched sweeps (some |x_j| < kOuterX): the nearest line j, |x_j| and T_j,

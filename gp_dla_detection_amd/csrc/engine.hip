@@ -68,6 +68,7 @@ const HostLineData& host_line_data() {
       d.buf[kLineBufFac + j] = (double)f;
     }
     for (int j = 0; j < 64; ++j) d.buf[kLineBufExp2 + j] = (double)std::exp2((long double)j / 64.0L);
+    for (int j = 0; j < 128; ++j) d.buf[kLineBufExp128 + j] = (double)std::exp2((long double)j / 128.0L);
   });
   return d;
 }

@@ -123,7 +123,8 @@ struct PrepArgs {
 constexpr size_t kLineBufWing = (size_t)kMaxLines * kCoreTable;
 constexpr size_t kLineBufFac = kLineBufWing + (size_t)kMaxLines * kWingStride;
 constexpr size_t kLineBufExp2 = kLineBufFac + kMaxLines;  // 2^(j/64), j = 0..63 (exp_tab64)
-constexpr size_t kLineBufDoubles = kLineBufExp2 + 64;
+constexpr size_t kLineBufExp128 = kLineBufExp2 + 64;      // 2^(j/128), j = 0..127 (exp_tab128_nc)
+constexpr size_t kLineBufDoubles = kLineBufExp128 + 128;
 
 struct LineArgs {
   const double* buf;   // device line buffer (layout above)

@@ -7,6 +7,7 @@
 
 #include <cmath>
 #include <cstdint>
+#include <type_traits>
 
 #include "device_common.h"
 #include "internal.h"
@@ -320,7 +321,8 @@ __global__ __launch_bounds__(256, (K <= 20 ? 2 : 1)) void likelihood_kernel(Like
   constexpr int kBuf = 4 * kChunkSteps * kRowS;
   static_assert(kWavesPerBlock == 4, "stage_chunk: one wave per segment");
   constexpr int kWingLds = 4 * ((3 * kWingStride + 3) / 4);
-  constexpr int kCoreLds = NL == 3 ? 3 * kCoreTable + kWingLds + 64 : 1;
+  constexpr int kExpLds = 128;
+  constexpr int kCoreLds = NL == 3 ? 3 * kCoreTable + kWingLds + kExpLds : 1;
   __shared__ __attribute__((aligned(16))) double lds[2 * kBuf + kCoreLds];
   double* core_lds = lds + 2 * kBuf;
   double* wing_lds = core_lds + 3 * kCoreTable;
@@ -358,7 +360,7 @@ __global__ __launch_bounds__(256, (K <= 20 ? 2 : 1)) void likelihood_kernel(Like
   stage_chunk<K>(panel, Ls, 0, lds_base, wave_s, voff);
   if constexpr (NL == 3) {
     for (int i = threadIdx.x; i < 3 * kCoreTable; i += 256) core_lds[i] = a.lines.buf[i];
-    if (threadIdx.x < 64) exp_lds[threadIdx.x] = a.lines.buf[kLineBufExp2 + threadIdx.x];
+    if (threadIdx.x < 128) exp_lds[threadIdx.x] = a.lines.buf[kLineBufExp128 + threadIdx.x];
     if (threadIdx.x < 3 * kWingStride) wing_lds[threadIdx.x] = a.lines.buf[kLineBufWing + threadIdx.x];
   }
 
@@ -381,14 +383,32 @@ __global__ __launch_bounds__(256, (K <= 20 ? 2 : 1)) void likelihood_kernel(Like
   for (int i = 0; i < 6; ++i) lw[i] = lamp[i];
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  // exp without its clamp (exp_tab128_nc): only a core-zone lane (|x| < kCoreX) can reach v = N tot
+  // below -2^31 ln2/128 (tau up to ~6e9 at a line centre); its fix-up clamps tot at -1100 / N.  Outside
+  // the core |tot| <= sum_j f_j(kCoreX) (the wings decrease with |x|), so a wave whose N_HI keep
+  // N sum_j f_j(kCoreX) <= 1e7 needs no clamp at all; any other wave (N_HI beyond ~1e27) clamps every
+  // lane (wave-uniform branch).
+  const double core_lim = -1100.0 / N;  // -inf for N = 0
+  bool wave_clamp = false;
+  if constexpr (NL == 3) {
+    double fmax9 = 0.0;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) fmax9 += fabs(wing_poly(wing_lds + j * kWingStride, 1.0 / (kCoreX * kCoreX)));
+    wave_clamp = __builtin_amdgcn_ballot_w64(!(N * fmax9 <= 1e7)) != 0;
+  }
 
   auto raw = [&](double lam, const double* wing) {
-    if constexpr (NL == 3) return raw_profile3(lam, afac, N, core_lds, wing, exp_lds);
+    if constexpr (NL == 3) return raw_profile3<kExpLds>(lam, afac, N, core_lds, wing, exp_lds);
     else return raw_profile(lam, zfac, N, a.num_lines, a.lines);
   };
-  // sliding window: raw profile at padded positions gL + 0..5
-  double w0 = raw(lw[0], wing_lds), w1 = raw(lw[1], wing_lds), w2 = raw(lw[2], wing_lds);
-  double w3 = raw(lw[3], wing_lds), w4 = raw(lw[4], wing_lds), w5 = raw(lw[5], wing_lds);
+  // sliding window over a ring of 10 registers: at the start of a chunk of phase P the window (raw
+  // profiles at the 6 padded positions ahead of the chunk's first pixel) is win[(4 P + i) % 10],
+  // i = 0..5, and the chunk's 4 new raw profiles go to win[(4 P + 6 + tt) % 10] (dead values).  The
+  // chunk loop is unrolled by 5 (4 * 5 = 0 mod 10), so every index is a compile-time register and
+  // the window never moves (one step at a time, each chunk ended in 6 register copies).
+  double win[10];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) win[i] = raw(lw[i], wing_lds);
 
   double acc[kTiles];
 #pragma unroll
@@ -397,7 +417,8 @@ __global__ __launch_bounds__(256, (K <= 20 ? 2 : 1)) void likelihood_kernel(Like
   double pm = 1.0;  // prod d = pm * 2^pe
   int pe = 0;
 
-  for (int c = 0; c < nchunks; ++c) {
+  auto chunk = [&](const int c, auto phase) __attribute__((always_inline)) {
+    constexpr int B = (4 * decltype(phase)::value) % 10;
     double* cur = lds + (c & 1) * kBuf;
     if (c + 1 < nchunks)
       stage_chunk<K>(panel, Ls, c + 1, lds_base + (uint32_t)(((c + 1) & 1) * kBuf * 8), wave_s, voff);
@@ -413,13 +434,30 @@ __global__ __launch_bounds__(256, (K <= 20 ? 2 : 1)) void likelihood_kernel(Like
         lamc[tt] = cur[(tt * 4 + g) * kRowS + Lay::kLam];
         tot[tt] = 0.0;
       }
+      // T_j = 1/x_j^2 of the 3 lines and 4 steps from ONE reciprocal (batch_rcp4 of the 4 steps'
+      // x_0^2 x_1^2 x_2^2; 3 fewer v_rcp_f64 per chunk than one per step).  x_j^2 + 2^-60 equals x_j^2
+      // for |x_j| >= 2^-30 and keeps each factor in [2^-60, ~2^37], so the 12-factor product stays a
+      // normal double; a lane on a line centre gets a huge but finite T_j that the core fix-up discards.
       double Tj[3][kChunkSteps];
+      {
+        double a0[kChunkSteps], a1[kChunkSteps], a2[kChunkSteps], p01[kChunkSteps], qq[kChunkSteps], iq[kChunkSteps];
 #pragma unroll
-      for (int tt = 0; tt < kChunkSteps; ++tt) {
-        const double x0 = fma(lamc[tt], afac[0], -kC2), x1 = fma(lamc[tt], afac[1], -kC2),
-                     x2 = fma(lamc[tt], afac[2], -kC2);
-        cm |= (((fabs(x0) < kOuterX) | (fabs(x1) < kOuterX) | (fabs(x2) < kOuterX)) ? 1u : 0u) << tt;
-        wing_T3(x0, x1, x2, Tj[0][tt], Tj[1][tt], Tj[2][tt]);
+        for (int tt = 0; tt < kChunkSteps; ++tt) {
+          const double x0 = fma(lamc[tt], afac[0], -kC2), x1 = fma(lamc[tt], afac[1], -kC2),
+                       x2 = fma(lamc[tt], afac[2], -kC2);
+          cm |= (((fabs(x0) < kOuterX) | (fabs(x1) < kOuterX) | (fabs(x2) < kOuterX)) ? 1u : 0u) << tt;
+          a0[tt] = fma(x0, x0, 0x1p-60); a1[tt] = fma(x1, x1, 0x1p-60); a2[tt] = fma(x2, x2, 0x1p-60);
+          p01[tt] = a0[tt] * a1[tt];
+          qq[tt] = p01[tt] * a2[tt];
+        }
+        batch_rcp4(qq, iq);
+#pragma unroll
+        for (int tt = 0; tt < kChunkSteps; ++tt) {
+          const double r01 = iq[tt] * a2[tt];
+          Tj[0][tt] = a1[tt] * r01;
+          Tj[1][tt] = a0[tt] * r01;
+          Tj[2][tt] = p01[tt] * iq[tt];
+        }
       }
       // line-outer order (same per-step summation order): one line's 9 coefficients live at a
       // time, re-read from LDS per line (opaque zero offset) rather than hoisted
@@ -452,20 +490,26 @@ __global__ __launch_bounds__(256, (K <= 20 ? 2 : 1)) void likelihood_kernel(Like
               double t = 0.0;
 #pragma unroll
               for (int jj = 0; jj < 3; ++jj) t -= jj == j ? cf : outer_poly(wing_lds + jj * kWingStride, Tj[jj][tt]);
-              tot[tt] = t;
+              tot[tt] = fmax(t, core_lim);
             }
           }
         }
       }
+      if (wave_clamp) {
 #pragma unroll
-      for (int tt = 0; tt < kChunkSteps; ++tt) {
-        rwv[tt] = exp_tab64(N * tot[tt], exp_lds);
+        for (int tt = 0; tt < kChunkSteps; ++tt) rwv[tt] = exp_tab128_nc(fmax(N * tot[tt], -1100.0), exp_lds);
+      } else {
+#pragma unroll
+        for (int tt = 0; tt < kChunkSteps; ++tt) rwv[tt] = exp_tab128_nc(N * tot[tt], exp_lds);
       }
     }
     // the chunk's per-pixel weights first -- 4 independent 7-tap + weight chains the scheduler can
     // interleave (one step at a time they were serial dependent chains of ~16 DP ops in front of each
     // step's MFMAs) -- then the 4 steps' MFMAs
+    // The 4 steps' 1/d share one reciprocal too (batch_rcp4_guarded: d = omega^2 a^2 + sigma^2 is
+    // not bounded a priori, so a wave whose product leaves [2^-1000, 2^1000] takes 4 reciprocals).
     double wgs[kChunkSteps], wus[kChunkSteps];
+    double abs_[kChunkSteps], rs[kChunkSteps], a2s[kChunkSteps], ds[kChunkSteps];
 #pragma unroll
     for (int tt = 0; tt < kChunkSteps; ++tt) {
       const double* row = cur + (tt * 4 + g) * kRowS;
@@ -486,26 +530,30 @@ __global__ __launch_bounds__(256, (K <= 20 ? 2 : 1)) void likelihood_kernel(Like
         w6 = raw(lam, wing_lds);
       }
       // instrumental broadening, voigt.c:297-299 (zero-initialised accumulator, taps in order)
-      double ab = w0 * kInstrumentProfile[0];
-      ab = fma(w1, kInstrumentProfile[1], ab);
-      ab = fma(w2, kInstrumentProfile[2], ab);
-      ab = fma(w3, kInstrumentProfile[3], ab);
-      ab = fma(w4, kInstrumentProfile[4], ab);
-      ab = fma(w5, kInstrumentProfile[5], ab);
+      double ab = win[(B + tt) % 10] * kInstrumentProfile[0];
+#pragma unroll
+      for (int i = 1; i < 6; ++i) ab = fma(win[(B + tt + i) % 10], kInstrumentProfile[i], ab);
       ab = fma(w6, kInstrumentProfile[6], ab);
-      w0 = w1; w1 = w2; w2 = w3; w3 = w4; w4 = w5; w5 = w6;
+      win[(B + tt + 6) % 10] = w6;
       // process_qsos.m:191-197 and log_mvnpdf_low_rank.m:11-15.  Masked / padding rows carry
       // y = mu = om2 = 0, noise = 1 and an all-zero Khatri-Rao row, so they add exactly nothing
       // (r = 0, d = 1, zero B operands) without a per-pixel select.
       const double r = fma(-mu, ab, y);
       const double a2 = ab * ab;
       const double d = fma(om2, a2, noise);
-      const double dinv = rcp_sweep(d);
-      const double rd = r * dinv;
-      wgs[tt] = a2 * dinv;
-      wus[tt] = ab * rd;
-      q1 = fma(r, rd, q1);
-      pm *= d;
+      abs_[tt] = ab; rs[tt] = r; a2s[tt] = a2; ds[tt] = d;
+    }
+    {
+      double dinv[kChunkSteps];
+      batch_rcp4_guarded(ds, dinv);
+#pragma unroll
+      for (int tt = 0; tt < kChunkSteps; ++tt) {
+        const double rd = rs[tt] * dinv[tt];
+        wgs[tt] = a2s[tt] * dinv[tt];
+        wus[tt] = abs_[tt] * rd;
+        q1 = fma(rs[tt], rd, q1);
+        pm *= ds[tt];
+      }
     }
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -523,6 +571,19 @@ __global__ __launch_bounds__(256, (K <= 20 ? 2 : 1)) void likelihood_kernel(Like
           acc[tp] = __builtin_amdgcn_mfma_f64_4x4x4f64(tp < kGT ? wg : wu, brow[tp], acc[tp], 0, 0, 0);
         }
       }
+    }
+    // One software pipeline over the chunk's 4 x kTiles MFMAs with the B-operand reads kD ahead
+    // (ds_read_b128 = 2 tiles; the default schedule kept 3 in flight and each MFMA pair waited on
+    // its read).  kD = 4 / 6 / 8 against the default: -0.2 / -0.3 / -0.0% kernel time (profiles/r5c).
+    {
+      constexpr int kReads = kChunkSteps * ((kTiles + 1) / 2), kD = 6;
+      __builtin_amdgcn_sched_group_barrier(0x100, kD, 0);
+#pragma unroll
+      for (int i = 0; i < kReads - kD; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, 2 * kD, 0);
       __builtin_amdgcn_sched_barrier(0);
     }
     {  // keep the running product in range
@@ -532,6 +593,18 @@ __global__ __launch_bounds__(256, (K <= 20 ? 2 : 1)) void likelihood_kernel(Like
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA for chunk c+1 landed
     __syncthreads();                                   // ... and everyone's; buffer c free again
+  };
+  using std::integral_constant;
+  for (int c = 0; c < nchunks; c += 5) {
+    chunk(c, integral_constant<int, 0>{});
+    if (c + 1 >= nchunks) break;
+    chunk(c + 1, integral_constant<int, 1>{});
+    if (c + 2 >= nchunks) break;
+    chunk(c + 2, integral_constant<int, 2>{});
+    if (c + 3 >= nchunks) break;
+    chunk(c + 3, integral_constant<int, 3>{});
+    if (c + 4 >= nchunks) break;
+    chunk(c + 4, integral_constant<int, 4>{});
   }
 
   // ---- combine the 4 segments of each sample (lanes l, l^16, l^32, l^48)

@@ -45,16 +45,17 @@ def test_i8_roofline_uses_the_gemm_launches(bench):
 
 
 def test_profiled_traffic_lookup(bench):
+    """Every bench workload's roofline traffic comes from the committed summary bench.py names, summed
+    over that path's roofline-kernel launches; other shapes claim no profiled number."""
     t, src = bench.profiled_traffic(1024, 10000, 20, "fused")
-    assert t is not None and t > 0 and "r3i_summary" in src
-    t24, src24 = bench.profiled_traffic(128, 100000, 50, "panel-GEMM-int8-24")
-    rows = json.loads((ROOT / "profiles" / "r3i_c5_summary.json").read_text())["kernels"]
-    assert t24 == sum(e["hbm_bytes_per_launch"] for e in rows if "gemm_i8_kernel" in e["kernel"])
-    assert "r3i_c5_summary" in src24
-    t5, src5 = bench.profiled_traffic(128, 100000, 50, "panel-GEMM-int8")
-    rows = json.loads((ROOT / "profiles" / "r2a_c5_summary.json").read_text())["kernels"]
-    want = sum(e["hbm_bytes_per_launch"] for e in rows if "gemm_i8_kernel" in e["kernel"])
-    assert t5 == want and "r2a_c5_summary" in src5
+    rows = json.loads(bench.PROFILE_SUMMARY.read_text())["kernels"]
+    want = [e["hbm_bytes_per_launch"] for e in rows if e["kernel"].startswith("void gpdla::likelihood_kernel<20")]
+    assert t is not None and t > 0 and t == want[0] and bench.PROFILE_SUMMARY.name in src
+    for path, (f, kname) in bench.PROFILE_SUMMARY_C5.items():
+        tp, srcp = bench.profiled_traffic(128, 100000, 50, path)
+        rows = json.loads(f.read_text())["kernels"]
+        assert tp == sum(e["hbm_bytes_per_launch"] for e in rows if kname in e["kernel"]) and tp > 0
+        assert f.name in srcp
     # other workloads / paths: no profiled number is claimed
-    assert bench.profiled_traffic(128, 100000, 50, "panel-GEMM") == (None, None)
+    assert bench.profiled_traffic(128, 100000, 50, "fused") == (None, None)
     assert bench.profiled_traffic(64, 10000, 20, "fused") == (None, None)
