@@ -258,11 +258,7 @@ __global__ __launch_bounds__(256, ND == 3 ? 3 : 2) void gemm_i8_kernel(GemmI8Arg
   // in its L2 beside the A digits of the sample tiles in flight (-3% GEMM time against EX = 1, which
   // re-reads all of B per sample tile; EX = 4 -2%)
   const int ny = a.ny, nst = (a.sc + kGTileS - 1) / kGTileS;
-#ifdef GPDLA_X_EX
-  const int EX = ny >= GPDLA_X_EX ? GPDLA_X_EX : 1, SX = 8 / EX;
-#else
   const int EX = ny >= 2 ? 2 : 1, SX = 8 / EX;  // (the u launch has one entry tile)
-#endif
   const int per = gridDim.x / 8;  // blocks per XCD (1-D grid, a multiple of 8)
   const int x = blockIdx.x % 8;
   const int ex = x % EX, sx = x / EX;
@@ -367,14 +363,12 @@ __global__ __launch_bounds__(256, ND == 3 ? 3 : 2) void gemm_i8_kernel(GemmI8Arg
           d[0] = make_double2(v[0], v[1]);
           d[1] = make_double2(v[2], v[3]);
         } else if (a.G32) {
-#ifdef GPDLA_X_NTG
+          // non-temporal: the fp32 Gram streams to the LDL^T kernel without being allocated in L2,
+          // where it evicted the A digits the XCD's other entry tiles still read (A fetched from
+          // beyond L2 1.66 -> 1.36 GB per launch, configs[4] +1.7%; profiles/r5e)
           typedef float f4v __attribute__((ext_vector_type(4)));
           __builtin_nontemporal_store((f4v){(float)v[0], (float)v[1], (float)v[2], (float)v[3]},
                                       reinterpret_cast<f4v*>(a.G32 + quad_index(s4, col, E)));
-#else
-          *reinterpret_cast<float4*>(a.G32 + quad_index(s4, col, E)) =
-              make_float4((float)v[0], (float)v[1], (float)v[2], (float)v[3]);
-#endif
         } else {
           double2* d = reinterpret_cast<double2*>(a.G + quad_index(s4, col, E));
           d[0] = make_double2(v[0], v[1]);

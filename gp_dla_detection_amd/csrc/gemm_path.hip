@@ -193,6 +193,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT <= 13 ? 
     q1 += __shfl_xor(q1, m);
     logdet_d += __shfl_xor(logdet_d, m);
   }
+  logdet_d += inf.de_shift * kLn2;  // prep's unit scaling (kernels.hip prep_kernel); 0 unless scaled
   // Load the tiles: straight-line code (unconditional loads from valid addresses), all issued up
   // front in row order; a row's values are formed only when its step comes (below), so the
   // factorisation of row J runs while rows > J are still in flight (the compiler's vmcnt waits count

@@ -76,7 +76,8 @@ struct SpecInfo {
   int64_t slot_base;  // first panel row of this spectrum
   int64_t lam_base;   // first element of this spectrum's padded-wavelength array
   int32_t flags;
-  int32_t pad_;
+  int32_t scale_e;    // prep's unit scaling: noise, omega^2 x 2^scale_e; flux, mu, M x 2^(scale_e / 2)
+  double de_shift;    // -n scale_e: log det D = log det D' + de_shift ln 2 (exact power-of-two scaling)
 };
 
 constexpr int kChunkSteps = 4;       // pixel steps staged per LDS chunk

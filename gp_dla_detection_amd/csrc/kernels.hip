@@ -43,6 +43,7 @@ __global__ __launch_bounds__(256) void prep_kernel(PrepArgs a) {
   const int i0 = min(tid * chunk, Lpix), i1 = min(i0 + chunk, Lpix);
   int c_in = 0, c_un = 0;
   double mn_in = INFINITY, mx_in = -INFINITY, mn_un = INFINITY, mx_un = -INFINITY;
+  double mn_e = INFINITY, mx_e = -INFINITY;  // binary exponents of the used pixels' noise variances
   for (int i = i0; i < i1; ++i) {
     const double lam = wl[i];
     const double rest = lam / (1 + z);                                  // :102
@@ -51,7 +52,11 @@ __global__ __launch_bounds__(256) void prep_kernel(PrepArgs a) {
     c_in += inr;
     c_un += un;
     if (inr) { mn_in = fmin(mn_in, lam); mx_in = fmax(mx_in, lam); }
-    if (un) { mn_un = fmin(mn_un, lam); mx_un = fmax(mx_un, lam); }
+    if (un) {
+      mn_un = fmin(mn_un, lam); mx_un = fmax(mx_un, lam);
+      const double nv = a.noise[pb + i];
+      if (nv > 0.0 && nv < INFINITY) { const double e = (double)ilogb(nv); mn_e = fmin(mn_e, e); mx_e = fmax(mx_e, e); }
+    }
   }
   int m = 0, n = 0;
   int pos_in = block_excl_scan(c_in, s_i4, &m);
@@ -60,6 +65,18 @@ __global__ __launch_bounds__(256) void prep_kernel(PrepArgs a) {
   mx_in = block_reduce_max(mx_in, s_d4);
   mn_un = block_reduce_min(mn_un, s_d4);
   mx_un = block_reduce_max(mx_un, s_d4);
+  mn_e = block_reduce_min(mn_e, s_d4);
+  mx_e = block_reduce_max(mx_e, s_d4);
+  // Units.  The sweeps keep prod d in a running product renormalised once per 4 (fused) or 16
+  // (panel weights) pixels, so a spectrum whose noise variances sit far from 1 (e.g. flux in cgs
+  // units, sigma^2 ~ 1e-34) would leave the double range.  Such a spectrum is evaluated in other
+  // units: flux, mu and M times 2^(E/2), sigma^2 and omega^2 times 2^E (E even, centring the
+  // exponents on 0).  Power-of-two scaling is exact: every Gram/u entry, r'D^-1 r and pivot is the
+  // same double, and log det D = log det D' - n E ln 2 (SpecInfo::de_shift).  Spectra with all
+  // exponents within +-60 are not scaled at all (E = 0), i.e. bitwise the unscaled evaluation.
+  int E = 0;
+  if (mn_e <= mx_e && (mn_e < -60.0 || mx_e > 60.0)) E = -2 * (int)rint(0.25 * (mn_e + mx_e));
+  const double fy = ldexp(1.0, E / 2), fv = ldexp(1.0, E);
 
   const int J = (n > 0 && m > 0) ? (a.absorption_mode ? m : n) : 0;
   const int L = (J + 3) / 4;
@@ -118,7 +135,8 @@ __global__ __launch_bounds__(256) void prep_kernel(PrepArgs a) {
     inf.slot_base = sb;
     inf.lam_base = lb;
     inf.flags = (J == 0);
-    inf.pad_ = 0;
+    inf.scale_e = E;
+    inf.de_shift = -(double)n * E;
     a.info[q] = inf;
   }
   __syncthreads();
@@ -181,10 +199,10 @@ __global__ __launch_bounds__(256) void prep_kernel(PrepArgs a) {
       double om2 = exp(2 * lom);                                            // :143
       const double sf = 1 - exp(-a.tau_0 * pow(1 + lya_z, a.beta)) + a.c_0;  // :145
       om2 = om2 * (sf * sf);                                                // :147
-      sc[1] = a.flux[pb + pix];
-      sc[2] = a.noise[pb + pix];
-      sc[3] = mu;
-      sc[4] = om2;
+      sc[1] = a.flux[pb + pix] * fy;   // unit scaling (pass 1): exact, 1.0 unless E != 0
+      sc[2] = a.noise[pb + pix] * fv;
+      sc[3] = mu * fy;
+      sc[4] = om2 * fv;
       sc[5] = 1.0;
     }
     if constexpr (K > 0) {
@@ -235,7 +253,7 @@ __global__ __launch_bounds__(256) void prep_kernel(PrepArgs a) {
           const double slope = (M1[col] - M0[col]) / (x1 - x0);
           v = slope * (rest - x0) + M0[col];
         }
-        sM[col] = v;
+        sM[col] = v * fy;
       }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the wave's LDS row before its reads
@@ -632,7 +650,7 @@ __global__ __launch_bounds__(256, (K <= 20 ? 2 : 1)) void likelihood_kernel(Like
   double A[NJJ][4 * NJJ], U[NJJ];
   fill_from_acc<K, 0>(A, U, acc, jq);
   bool bad;
-  const double ll = ldl_factor<K>(A, U, qs, dm, (double)de, jq, inf.n, bad);
+  const double ll = ldl_factor<K>(A, U, qs, dm, (double)de + inf.de_shift, jq, inf.n, bad);
   const int64_t s2 = s_base + sig;
   if (jq == 0 && s2 <= a.S) {
     if (bad) atomicOr(a.status, 1);

@@ -444,7 +444,7 @@ __global__ __launch_bounds__(256, 1) void likelihood_i8_kernel(LikelihoodI8Args 
     double* scl = scr + lane * F::kES + 4 * F::kTiles;
     scl[0] = q1;
     scl[1] = pm;
-    scl[2] = (double)pe;
+    scl[2] = (double)pe + inf.de_shift;  // prep's unit scaling (kernels.hip prep_kernel)
   }
   __syncthreads();
   const int jq = lane & 3, sq = lane >> 2;

@@ -15,19 +15,6 @@ VARIANTS: dict = {
     "ch50k": {"GPDLA_MAX_CHUNK": 50001},
     "ch25k": {"GPDLA_MAX_CHUNK": 25001},
     "ch16k": {"GPDLA_MAX_CHUNK": 16667},
-    "x_nobar": {"GPDLA_X_NOBAR": 1},
-    "x_nofix": {"GPDLA_X_NOFIX": 1},
-    "x_noepi": {"GPDLA_X_NOEPI": 1},
-    "x_rcp4": {"GPDLA_X_RCP4": 1},
-    "u5": {"GPDLA_VARIANT_U5": 1},
-    "u5_rcp4": {"GPDLA_X_RCP4": 1},
-    "u5_rcp4_e128": {"GPDLA_X_RCP4": 1, "GPDLA_X_E128": 1},
-    "h_d4": {"GPDLA_X_RCP4": 1, "GPDLA_X_E128": 1, "GPDLA_X_DEEP": 4},
-    "h_d6": {"GPDLA_X_RCP4": 1, "GPDLA_X_E128": 1, "GPDLA_X_DEEP": 6},
-    "h_d8": {"GPDLA_X_RCP4": 1, "GPDLA_X_E128": 1, "GPDLA_X_DEEP": 8},
-    "g_ntg": {"GPDLA_X_NTG": 1},
-    "g_ex4": {"GPDLA_X_EX": 4},
-    "g_ex1": {"GPDLA_X_EX": 1},
 }
 if __name__ == "__main__":
     names = sys.argv[1:] or list(VARIANTS)
