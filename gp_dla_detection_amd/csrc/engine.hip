@@ -276,6 +276,12 @@ int gpdla_engine_create(int32_t device, const gpdla_model* model, const gpdla_sa
       return set_error(GPDLA_EINVAL, "rest_wavelengths must be strictly increasing");
   if (samples->num_samples < 1 || !samples->offset_samples || !samples->nhi_samples)
     return set_error(GPDLA_EINVAL, "invalid samples");
+  // column densities: the sweeps' exp needs N >= 0 and finite (kernels.hip likelihood_kernel bounds
+  // N tot by them); generate_dla_samples.m:20-53 only produces positive N_HI
+  for (int64_t i = 0; i < samples->num_samples; ++i)
+    if (!(samples->nhi_samples[i] >= 0.0 && samples->nhi_samples[i] < INFINITY))
+      return set_error(GPDLA_EINVAL, "nhi_samples[%lld] = %g: column densities must be finite and >= 0",
+                       (long long)i, samples->nhi_samples[i]);
 
   HIP_TRY(hipSetDevice(device));
   gpdla_engine* e = new gpdla_engine();

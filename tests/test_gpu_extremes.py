@@ -116,3 +116,16 @@ def test_power_of_two_units_are_exact(e):
                                    outs[0]["sample_log_likelihoods_dla"] + shift[:, None], rtol=1e-11, atol=0)
         np.testing.assert_allclose(outs[1]["log_likelihoods_no_dla"], outs[0]["log_likelihoods_no_dla"] + shift,
                                    rtol=1e-11, atol=0)
+
+
+def test_invalid_column_densities_rejected():
+    """Negative, NaN and infinite N_HI are refused at engine creation (GPDLA_EINVAL), before any kernel
+    runs: the sweeps' exp relies on N >= 0 and finite."""
+    model = syn.make_model(k=20, seed=8)
+    base = syn.make_samples(16)
+    for bad in (-1e20, np.nan, np.inf):
+        nhi = base["nhi_samples"].copy()
+        nhi[5] = bad
+        samples = dict(base, nhi_samples=nhi)
+        with pytest.raises(L.GpdlaError, match="column densities"):
+            Engine(model, samples, set_parameters(k=20))
