@@ -51,15 +51,17 @@ __device__ inline void batch_rcp4(const double (&q)[4], double (&iq)[4]) {
   iq[3] = R01 * q[2];
 }
 
-// batch_rcp4 for unbounded positive q_i (the per-pixel d = omega^2 a^2 + sigma^2): when the product
-// leaves [2^-1000, 2^1000] (a d outside ~[1e-75, 1e75]) the wave takes four rcp_sweep instead.
-__device__ inline void batch_rcp4_guarded(const double (&q)[4], double (&iq)[4]) {
+// batch_rcp4 for unbounded positive q_i (the per-pixel d = omega^2 a^2 + sigma^2): P = q_0 q_1 q_2 q_3;
+// when P leaves [2^-1000, 2^1000] (some d outside ~[1e-75, 1e75]) the lane takes four rcp_sweep
+// instead and the function returns false (the caller then also keeps its running product of the q_i
+// in range one factor at a time).
+__device__ inline bool batch_rcp4_guarded(const double (&q)[4], double (&iq)[4], double& P) {
   const double q01 = q[0] * q[1], q23 = q[2] * q[3];
-  const double P = q01 * q23;
+  P = q01 * q23;
   if (__builtin_expect(!(P > 0x1p-1000 && P < 0x1p1000), 0)) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) iq[i] = rcp_sweep(q[i]);
-    return;
+    return false;
   }
   double R = __builtin_amdgcn_rcp(P);
   R = fma(R, fma(-P, R, 1.0), R);
@@ -68,6 +70,7 @@ __device__ inline void batch_rcp4_guarded(const double (&q)[4], double (&iq)[4])
   iq[1] = R23 * q[0];
   iq[2] = R01 * q[3];
   iq[3] = R01 * q[2];
+  return true;
 }
 
 // global -> LDS DMA of one 1 KiB piece (64 lanes x 16 B, per-lane global byte offsets from a

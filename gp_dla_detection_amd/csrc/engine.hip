@@ -113,6 +113,7 @@ struct gpdla_engine {
   double *d_rest = nullptr, *d_mu = nullptr, *d_M = nullptr, *d_logom = nullptr;
   int32_t num_rest = 0;
   double c0 = 0, tau0 = 0, beta = 0;
+  int32_t om2_hi_e = 0;  // binary exponent of max omega^2 (1 + c_0)^2 over the rest grid (prep units)
   double *d_off = nullptr, *d_nhi = nullptr;  // samples in ascending-offset (z_DLA) order
   int32_t* d_perm = nullptr;                   // sorted sample index -> caller's sample index
   double* d_lines = nullptr;
@@ -296,6 +297,12 @@ int gpdla_engine_create(int32_t device, const gpdla_model* model, const gpdla_sa
   e->c0 = std::exp(model->log_c_0);     // process_qsos.m:84-86
   e->tau0 = std::exp(model->log_tau_0);
   e->beta = std::exp(model->log_beta);
+  {  // omega^2 = exp(2 log omega) sf^2 with sf = 1 - exp(-tau_0 (1 + z)^beta) + c_0 in [c_0, 1 + c_0]
+    double lo_max = -INFINITY;
+    for (int i = 0; i < model->num_rest; ++i) lo_max = std::max(lo_max, model->log_omega[i]);
+    const double om2_max = std::exp(2 * lo_max) * (1 + e->c0) * (1 + e->c0);
+    e->om2_hi_e = (om2_max > 0 && om2_max < INFINITY) ? (int32_t)std::ilogb(om2_max) : 0;
+  }
   auto fail = [&](int code) { gpdla_engine_destroy(e); return code; };
 #define TRY_E(x) do { int r_ = (x); if (r_) return fail(r_); } while (0)
   if (hipStreamCreateWithFlags(&e->own_stream, hipStreamNonBlocking) != hipSuccess)
@@ -638,6 +645,7 @@ int gpdla_engine_process(gpdla_engine* e, const gpdla_spectra* sp, const gpdla_r
     pa.min_z_cut = e->params.min_z_cut; pa.max_z_cut = e->params.max_z_cut;
     pa.pixel_spacing = e->params.pixel_spacing;
     pa.absorption_mode = e->params.absorption_mode;
+    pa.om2_hi_e = e->om2_hi_e;
     pa.info = e->d_info; pa.panel = e->d_panel; pa.lam_pad = e->d_lam; pa.slot_pixel = e->d_smap;
     pa.k = e->K; pa.panel_m = e->d_pm; pa.srow = e->d_srow;
 

@@ -107,6 +107,7 @@ struct PrepArgs {
   double min_lambda, max_lambda, lya, lyman_limit, min_z_cut, max_z_cut, pixel_spacing;
   int32_t absorption_mode;
   int32_t k;                     // rank (read by the panel-GEMM layout, prep_kernel<0>)
+  int32_t om2_hi_e;              // binary exponent of the model's largest omega^2 (1 + c_0)^2 (units)
   // outputs
   SpecInfo* info;
   double* panel;                 // fused layout: [slots][kRow]; GEMM layout: [slots][k(k+1)/2]

@@ -67,15 +67,20 @@ __global__ __launch_bounds__(256) void prep_kernel(PrepArgs a) {
   mx_un = block_reduce_max(mx_un, s_d4);
   mn_e = block_reduce_min(mn_e, s_d4);
   mx_e = block_reduce_max(mx_e, s_d4);
-  // Units.  The sweeps keep prod d in a running product renormalised once per 4 (fused) or 16
-  // (panel weights) pixels, so a spectrum whose noise variances sit far from 1 (e.g. flux in cgs
-  // units, sigma^2 ~ 1e-34) would leave the double range.  Such a spectrum is evaluated in other
-  // units: flux, mu and M times 2^(E/2), sigma^2 and omega^2 times 2^E (E even, centring the
-  // exponents on 0).  Power-of-two scaling is exact: every Gram/u entry, r'D^-1 r and pivot is the
-  // same double, and log det D = log det D' - n E ln 2 (SpecInfo::de_shift).  Spectra with all
+  // Units.  The panel weights kernels keep prod d in a running product renormalised once per 16
+  // pixels (the fused sweep renormalises per 4, or per pixel when 4 d's leave the range), so a
+  // spectrum whose d = omega^2 a^2 + sigma^2 sit far from 1 (e.g. flux in cgs units, sigma^2 ~ 1e-34)
+  // would leave the double range.  Such a spectrum is evaluated in other units: flux, mu and M times
+  // 2^(E/2), sigma^2 and omega^2 times 2^E (E even).  d lies in [min sigma^2, max omega^2 + max sigma^2];
+  // E centres the binary exponents of that interval (sigma^2 from pass 1, the model's omega^2 bound
+  // from the engine) on 0.  Power-of-two scaling is exact: every Gram/u entry, r'D^-1 r and pivot is
+  // the same double, and log det D = log det D' - n E ln 2 (SpecInfo::de_shift).  Spectra with all
   // exponents within +-60 are not scaled at all (E = 0), i.e. bitwise the unscaled evaluation.
   int E = 0;
-  if (mn_e <= mx_e && (mn_e < -60.0 || mx_e > 60.0)) E = -2 * (int)rint(0.25 * (mn_e + mx_e));
+  if (mn_e <= mx_e) {
+    const double hi_e = fmax(mx_e, (double)a.om2_hi_e);
+    if (mn_e < -60.0 || hi_e > 60.0) E = -2 * (int)rint(0.25 * (mn_e + hi_e));
+  }
   const double fy = ldexp(1.0, E / 2), fv = ldexp(1.0, E);
 
   const int J = (n > 0 && m > 0) ? (a.absorption_mode ? m : n) : 0;
@@ -562,15 +567,26 @@ __global__ __launch_bounds__(256, (K <= 20 ? 2 : 1)) void likelihood_kernel(Like
       abs_[tt] = ab; rs[tt] = r; a2s[tt] = a2; ds[tt] = d;
     }
     {
-      double dinv[kChunkSteps];
-      batch_rcp4_guarded(ds, dinv);
+      double dinv[kChunkSteps], P;
+      const bool p_ok = batch_rcp4_guarded(ds, dinv, P);
 #pragma unroll
       for (int tt = 0; tt < kChunkSteps; ++tt) {
         const double rd = rs[tt] * dinv[tt];
         wgs[tt] = a2s[tt] * dinv[tt];
         wus[tt] = abs_[tt] * rd;
         q1 = fma(rs[tt], rd, q1);
-        pm *= ds[tt];
+      }
+      // prod d: the chunk's product P of the 4 d's when it is in range (pm stays in [2^-1001, 2^1000]
+      // until the per-chunk frexp below), otherwise one factor at a time, renormalised after each
+      if (p_ok) {
+        pm *= P;
+      } else {
+#pragma unroll
+        for (int tt = 0; tt < kChunkSteps; ++tt) {
+          int ex;
+          pm = frexp(pm * ds[tt], &ex);
+          pe += ex;
+        }
       }
     }
     __builtin_amdgcn_sched_barrier(0);

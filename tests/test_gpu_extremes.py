@@ -129,3 +129,21 @@ def test_invalid_column_densities_rejected():
         samples = dict(base, nhi_samples=nhi)
         with pytest.raises(L.GpdlaError, match="column densities"):
             Engine(model, samples, set_parameters(k=20))
+
+
+def test_scaled_and_unscaled_spectra_in_one_batch():
+    """prep_kernel picks the unit exponent per spectrum, from its sigma^2 and the model's largest
+    omega^2: a batch with one spectrum whose noise variances are 2^-100 times the usual (flux and model
+    unchanged, so d spans ~2^100 within it and r'D^-1 r ~ 1e30) beside ordinary ones, every path against
+    the oracle on the same inputs.  At 2^-200 (d spanning ~2^200) only the fused fp64 sweep keeps prod d
+    in range (one factor at a time when four leave it); the panel paths' weights kernels renormalise
+    once per 16 pixels and support a span of ~2^120.  fp64 paths only: with d
+    spanning 2^100, r'D^-1 r and u'B^-1 u are ~1e44 and cancel to ~1e30, far below the int8
+    contraction's error bound (relative to each slot's static scale)."""
+    model = syn.make_model(k=20, seed=9)
+    spectra = [syn.make_spectrum(model, q, z_qso=z, n_target=None, mask_fraction=0.05)
+               for q, z in enumerate((2.4, 2.9, 3.5))]
+    for e, paths in ((-100, (("auto", 1e-9), ("panel_gemm", 1e-9))), (-200, (("auto", 1e-9),))):
+        sp = list(spectra)
+        sp[1] = dict(sp[1], noise_variance=np.ldexp(sp[1]["noise_variance"], e))
+        _check(model, sp, syn.make_samples(100), paths)
