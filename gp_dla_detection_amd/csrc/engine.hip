@@ -397,6 +397,7 @@ static int run_panel_gemm(gpdla_engine* e, bool i8, int64_t nq, const int64_t* h
         // the 24-bit path stores the Gram in fp32 (half the GEMM -> LDL^T round trip; adds ~1e-8
         // to its ~2e-7 from fp64, tests/support/emulate_i8.py), in the same workspace
         gi.G32 = e->i8_nd == 3 ? reinterpret_cast<float*>(G) : nullptr;
+        gi.ks_bound = (int32_t)(((h_cap[q] - 16) / 4 + 15) / 16);  // slot_cap = 4 ceil(lpix / 4) + 16
         TimedLaunch tg{};
         int rc;
         if ((rc = record_start(e, &tg, 3))) return rc;

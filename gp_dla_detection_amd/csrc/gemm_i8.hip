@@ -413,6 +413,162 @@ __global__ __launch_bounds__(256, ND == 3 ? 3 : 2) void gemm_i8_kernel(GemmI8Arg
   }
 }
 
+// --------------------------------------------------------------------------------------------
+// B-stationary Gram GEMM (24-bit path, ND = 3): one 12-wave block per CU keeps the WHOLE K range of
+// one 64-entry tile's panel digits in LDS (nks x 12 KiB, nks <= kBstMaxKs) and streams sample tiles
+// past it.  gemm_i8_kernel re-reads an entry tile's B digits from L2 for every 128-sample tile (a
+// third of its L2 -> CU bytes); here each block reads them once, and after the prologue there is no
+// barrier at all: each wave walks its own 32 samples x 64 entries, K step by K step, with its A
+// digits prefetched one step ahead into the other of two register sets (same MFMAs, same per-
+// accumulator order, so the int32 sums and the epilogue are bit for bit gemm_i8_kernel<3>'s).
+// Work: XCD x owns entry tiles x % EX and sample tiles x / EX (EX = 4: each sample tile's A digits
+// are read by the 4 XCDs of its range); its blocks form nye entry-tile columns x G groups; round r
+// of group gi covers sample tiles s0 + 3 (r G + gi) .. + 2 (one per 4 waves), so all of an XCD's
+// blocks sweep the same 3 G sample tiles together and their A lines stay in its L2.
+// --------------------------------------------------------------------------------------------
+#ifndef GPDLA_BST_WAVES
+#define GPDLA_BST_WAVES 12
+#endif
+constexpr int kBstWaves = GPDLA_BST_WAVES;
+constexpr int kBstTiles = kBstWaves / 4;         // 128-sample tiles per block round
+constexpr int kBstMaxKs = 13;                    // 13 x 12 KiB = 156 KiB of LDS: spectra up to 832 slots
+#ifndef GPDLA_BST_EX
+#define GPDLA_BST_EX 4
+#endif
+constexpr int kBstEX = GPDLA_BST_EX;
+
+__global__ __launch_bounds__(64 * kBstWaves, 1) __attribute__((amdgpu_waves_per_eu(kBstWaves / 4, kBstWaves / 4)))
+void gemm_i8_bst_kernel(GemmI8Args a) {
+  constexpr int ND = 3;
+  constexpr int kStepBytes = ND * kGTileE * 64;  // 12 KiB: one K step of one entry tile, 3 planes
+  __shared__ __attribute__((aligned(16))) uint8_t Bs[kBstMaxKs * kStepBytes];
+  const SpecInfo inf = a.info[a.q];
+  if (inf.J == 0) return;
+  const int K = a.k;
+  const int E = K * (K + 1) / 2;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wave_s = __builtin_amdgcn_readfirstlane(wave);
+  const int ny = a.ny, nst = (a.sc + kGTileS - 1) / kGTileS;
+  const int EX = kBstEX, SX = 8 / EX;
+  const int per = gridDim.x / 8;
+  const int x = blockIdx.x % 8;
+  const int ex = x % EX, sx = x / EX;
+  const int e0 = ny * ex / EX, e1 = ny * (ex + 1) / EX;
+  const int s0 = nst * sx / SX, s1 = nst * (sx + 1) / SX;
+  const int nye = e1 - e0;
+  const int G = per / nye;                       // groups per entry tile (blocks past nye G idle)
+  const int j = blockIdx.x / 8;
+  if (nye <= 0 || G <= 0 || j >= nye * G) return;
+  const int e_tile = (a.e_tile0 + e0 + j % nye) * kGTileE;
+  const int gi = j / nye;
+  const int nks = (16 * ((inf.L + 15) / 16)) / 16;  // 64-slot K steps (<= ks_bound <= kBstMaxKs)
+  if (nks > kBstMaxKs) return;                   // never: the launch checks the bound (LDS safety)
+  const int64_t nksmax = a.kstride / 64;
+  // prologue: the entry tile's B digits for every K step, 1 KiB pieces round-robin over the waves
+  const uint32_t bs_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)&Bs[0];
+  {
+    const uint8_t* B0 = a.bdig + (int64_t)(e_tile >> 6) * nksmax * 4 * 4096;
+    const int npieces = nks * (kStepBytes / 1024);
+    for (int pc = wave_s; pc < npieces; pc += kBstWaves) {
+      const int ks = pc / (kStepBytes / 1024), w = pc - ks * (kStepBytes / 1024);
+      dma_piece(B0 + (int64_t)ks * 4 * 4096 + w * 1024, (uint32_t)(lane * 16), bs_base + (uint32_t)(pc * 1024));
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  const int g = lane >> 4;
+  const int wt = wave_s & 3;                     // the wave's 32 rows of its 128-sample tile
+  const int64_t a_lane = ((int64_t)g * 128 + 32 * wt + (lane & 15)) * 16;
+  v4i acc[ND][2][4];
+  auto zero_acc = [&]() {
+#pragma unroll
+    for (int l = 0; l < ND; ++l)
+#pragma unroll
+      for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+        for (int ct = 0; ct < 4; ++ct) acc[l][rt][ct] = (v4i){0, 0, 0, 0};
+  };
+  auto load_a = [&](const uint8_t* At, int ks, v4i (&r)[2][ND]) {
+    const uint8_t* A0 = At + (int64_t)ks * 16 * 2048 + a_lane;
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+      for (int p = 0; p < ND; ++p) r[rt][p] = *reinterpret_cast<const v4i*>(A0 + p * 8192 + rt * 256);
+  };
+  auto compute = [&](const v4i (&Ar)[2][ND], int ks) {
+    const uint8_t* Bc = Bs + ks * kStepBytes;
+#pragma unroll
+    for (int ct = 0; ct < 4; ++ct) {
+      const int row = 16 * ct + (lane & 15);
+      v4i Bd[ND];
+#pragma unroll
+      for (int p = 0; p < ND; ++p)
+        Bd[p] = *reinterpret_cast<const v4i*>(Bc + p * (kGTileE * 64) + row * 64 + 16 * ((g + 2 * ((row >> 2) & 3)) & 3));
+#pragma unroll
+      for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+        for (int l = 0; l < ND; ++l)
+#pragma unroll
+          for (int i = 0; i <= l; ++i) acc[l][rt][ct] = MFMA_I8(Ar[rt][i], Bd[l - i], acc[l][rt][ct]);
+    }
+  };
+  auto epilogue = [&](int s_tile) {
+#pragma unroll
+    for (int ct = 0; ct < 4; ++ct) {
+      const int col = e_tile + 16 * ct + (lane & 15);
+      if (col >= E) continue;
+      const double sc = a.ent[col], off0 = a.ent[i8_gemm_entries(K) + col];
+#pragma unroll
+      for (int rt = 0; rt < 2; ++rt) {
+        const int s4 = s_tile + 32 * wt + 16 * rt + 4 * (lane >> 4);
+        double v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          double val = (double)acc[ND - 1][rt][ct][r] * __builtin_ldexp(1.0, 48 - 8 * (ND - 1));
+#pragma unroll
+          for (int l = ND - 2; l >= 0; --l) val = fma((double)acc[l][rt][ct][r], __builtin_ldexp(1.0, 48 - 8 * l), val);
+          v[r] = (val + off0) * sc;
+        }
+        typedef float f4v __attribute__((ext_vector_type(4)));
+        __builtin_nontemporal_store((f4v){(float)v[0], (float)v[1], (float)v[2], (float)v[3]},
+                                    reinterpret_cast<f4v*>(a.G32 + quad_index(s4, col, E)));
+      }
+    }
+  };
+  const int span = kBstTiles * G;                // sample tiles per round of the XCD's blocks
+  for (int r0 = s0 + kBstTiles * gi; r0 < s1; r0 += span) {
+    const int st = r0 + (wave_s >> 2);           // this wave's sample tile
+    if (st >= s1) break;                         // wave-uniform (the round's last tiles)
+    const uint8_t* At = a.adig + (int64_t)st * nksmax * 16 * 2048;
+    zero_acc();
+    // two A register sets in turn, the loop unrolled by two (no copies); each step's loads are waited
+    // for after the previous step's MFMAs and handed over through an empty "+v" asm, so the
+    // compiler's waitcnt pass never drains the prefetch in flight (as gemm_i8_kernel's land())
+    v4i A0r[2][ND], A1r[2][ND];
+    auto land = [&](v4i (&Ar)[2][ND]) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+        for (int p = 0; p < ND; ++p) asm volatile("" : "+v"(Ar[rt][p]));
+    };
+    load_a(At, 0, A0r);
+    land(A0r);
+    for (int ks = 0; ks < nks; ks += 2) {
+      const bool m1 = ks + 1 < nks, m2 = ks + 2 < nks;
+      if (m1) load_a(At, ks + 1, A1r);
+      __builtin_amdgcn_sched_barrier(0);
+      compute(A0r, ks);
+      land(A1r);
+      if (m2) load_a(At, ks + 2, A0r);
+      __builtin_amdgcn_sched_barrier(0);
+      if (m1) compute(A1r, ks + 1);
+      land(A0r);
+    }
+    epilogue(st * kGTileS);
+  }
+}
+
 #undef MFMA_I8
 
 }  // namespace
@@ -452,7 +608,16 @@ hipError_t launch_gemm_i8(const GemmI8Args& a0, hipStream_t s) {
     hipLaunchKernelGGL(gemm_i8_kernel<4>, grid(a.ny, 2), dim3(256), 0, s, a);
   } else {
     a.e_tile0 = 0; a.ny = ng;
-    hipLaunchKernelGGL(gemm_i8_kernel<3>, grid(a.ny, 3), dim3(256), 0, s, a);
+    // B-stationary when the spectrum's K steps fit the block's LDS
+#ifdef GPDLA_NO_BST
+    if (false) {
+#else
+    if (a0.ks_bound > 0 && a0.ks_bound <= kBstMaxKs && ng >= kBstEX && a0.G32) {
+#endif
+      hipLaunchKernelGGL(gemm_i8_bst_kernel, dim3((unsigned)ncu), dim3(64 * kBstWaves), 0, s, a);
+    } else {
+      hipLaunchKernelGGL(gemm_i8_kernel<3>, grid(a.ny, 3), dim3(256), 0, s, a);
+    }
     a.e_tile0 = ng; a.ny = nu;
     hipLaunchKernelGGL(gemm_i8_kernel<4>, grid(a.ny, 2), dim3(256), 0, s, a);
   }
