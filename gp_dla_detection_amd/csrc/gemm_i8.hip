@@ -421,8 +421,9 @@ __global__ __launch_bounds__(256, ND == 3 ? 3 : 2) void gemm_i8_kernel(GemmI8Arg
 // barrier at all: each wave walks its own 32 samples x 64 entries, K step by K step, with its A
 // digits prefetched one step ahead into the other of two register sets (same MFMAs, same per-
 // accumulator order, so the int32 sums and the epilogue are bit for bit gemm_i8_kernel<3>'s).
-// Work: XCD x owns entry tiles x % EX and sample tiles x / EX (EX = 4: each sample tile's A digits
-// are read by the 4 XCDs of its range); its blocks form nye entry-tile columns x G groups; round r
+// Work: XCD x owns entry tiles x % EX and sample tiles x / EX (EX = 2: each sample tile's A digits
+// are read by the 2 XCDs of its range; EX = 4 / 8 measured -1.3% / -5%, profiles/r5j); its blocks
+// form nye entry-tile columns x G groups (at k = 50: 10 x 3 of an XCD's 32); round r
 // of group gi covers sample tiles s0 + 3 (r G + gi) .. + 2 (one per 4 waves), so all of an XCD's
 // blocks sweep the same 3 G sample tiles together and their A lines stay in its L2.
 // --------------------------------------------------------------------------------------------
@@ -433,7 +434,7 @@ constexpr int kBstWaves = GPDLA_BST_WAVES;
 constexpr int kBstTiles = kBstWaves / 4;         // 128-sample tiles per block round
 constexpr int kBstMaxKs = 13;                    // 13 x 12 KiB = 156 KiB of LDS: spectra up to 832 slots
 #ifndef GPDLA_BST_EX
-#define GPDLA_BST_EX 4
+#define GPDLA_BST_EX 2
 #endif
 constexpr int kBstEX = GPDLA_BST_EX;
 
