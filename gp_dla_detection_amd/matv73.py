@@ -997,8 +997,8 @@ def _decode(r: _Reader, addr: int):
     if kind == "ref":
         flat = arr.ravel()                       # C order over HDF5 dims == MATLAB column-major
         cells = np.empty(flat.size, dtype=object)
-        for i, a in enumerate(flat):
-            cells[i] = _decode(r, int(a))
+        for i, c in enumerate(_decode_cells(r, flat.astype(np.int64))):
+            cells[i] = c
         return cells.reshape(mshape, order="F")
     if kind == "compound":
         names = arr.dtype.names
@@ -1012,6 +1012,159 @@ def _decode(r: _Reader, addr: int):
         return rows[0] if len(rows) == 1 else rows
     if cls == "logical":
         return out.astype(bool)
+    return out
+
+
+# ------------------------------------------------------------------ batched cells
+@dataclass
+class _CellTemplate:
+    """One cell's v1 object header as a byte pattern: the cells of a cell array written by one
+    writer differ only in their dims and data address / size (MATLAB and savemat73 alike), so the
+    others are matched against it in bulk instead of parsed one by one.  ``fixed`` marks the bytes
+    that must be equal; ``dims`` / ``layout`` are the offsets of the dataspace dims and of the
+    contiguous layout's address and size in the header."""
+    raw: np.ndarray
+    fixed: np.ndarray
+    dims: int
+    rank: int
+    layout: int
+    dtype: np.dtype
+    cls: str
+    empty: bool
+
+
+_FAST_CLASSES = set(_CLASS_DTYPE) | {"logical"}
+
+
+def _cell_template(r: _Reader, addr: int) -> _CellTemplate | None:
+    """The byte pattern of the cell at ``addr``, or None for headers the bulk path does not
+    take (v2 headers, continuations, non-contiguous data, char / cell / struct cells)."""
+    head = r.read(addr, 16)
+    if len(head) < 16 or head[:4] == b"OHDR" or head[0] != 1:
+        return None
+    nmsg, size = struct.unpack("<HxxxxI", head[2:12])
+    span = 16 + size
+    if span > 4096 or addr + span + r.base > len(r.buf):
+        return None
+    raw = r.read(addr, span)
+    var = np.zeros(span, dtype=bool)
+    dims = layout = None
+    q = 16
+    for _ in range(nmsg):
+        if q + 8 > span:
+            return None
+        t, sz = struct.unpack("<HH", raw[q:q + 4])
+        b = q + 8
+        if t == 0x10:
+            return None
+        if t == 0x01:
+            ver, rank, flags = raw[b], raw[b + 1], raw[b + 2]
+            if ver == 2 and raw[b + 3] != 1:
+                return None
+            p = b + (8 if ver == 1 else 4)
+            dims = (p, rank)
+            var[p:p + 16 * rank if flags & 1 else p + 8 * rank] = True
+        elif t == 0x08:
+            if raw[b] not in (3, 4) or raw[b + 1] != 1:
+                return None
+            layout = b + 2
+            var[b + 2:b + 18] = True
+        elif t in (0x0E, 0x12):   # modification times (libhdf5 tracks them per object by default)
+            var[b:b + sz] = True
+        q = b + sz
+    if dims is None or layout is None or q > span:
+        return None
+    msgs = r.messages(addr)
+    attrs = r._attributes(msgs)
+    cls = attrs.get("MATLAB_class", None)
+    cls = cls.decode() if isinstance(cls, bytes) else cls
+    if cls not in _FAST_CLASSES:
+        return None
+    empty = bool(attrs.get("MATLAB_empty", 0))
+    dt = None
+    for t, body in msgs:
+        if t == 0x03:
+            dt, kind = r._datatype(body)
+            if kind not in ("int", "float"):
+                return None
+    if dt is None:
+        return None
+    return _CellTemplate(np.frombuffer(raw, dtype=np.uint8), ~var, dims[0], dims[1], layout, dt, cls, empty)
+
+
+def _match_cells(r: _Reader, tpl: _CellTemplate, addrs: np.ndarray):
+    """Which of ``addrs`` have ``tpl``'s header (every fixed byte equal, data contiguous, in the
+    file and of the size its dims give); for those, their HDF5 dims and data addresses / sizes."""
+    span = tpl.raw.size
+    a = addrs.astype(np.int64) + r.base
+    inb = (a >= 0) & (a + span <= len(r.buf))
+    ok = np.zeros(addrs.size, dtype=bool)
+    dims = np.zeros((addrs.size, tpl.rank), dtype=np.uint64)
+    dadr = np.zeros(addrs.size, dtype=np.uint64)
+    dsz = np.zeros(addrs.size, dtype=np.uint64)
+    sel = np.flatnonzero(inb)
+    al = int(a[sel[0]]) % 8 if sel.size else 0
+    if span % 8 == 0 and sel.size and np.all(a[sel] % 8 == al):
+        # 8-byte aligned headers (v1 header messages are): gather words, not bytes
+        words = np.frombuffer(r.buf, dtype="<u8", offset=al, count=(len(r.buf) - al) // 8)
+        gather = lambda part: words[((a[part] - al) // 8)[:, None] + np.arange(span // 8)].view(np.uint8)
+    else:
+        gather = lambda part: r.mm[a[part][:, None] + np.arange(span)]
+    for s0 in range(0, sel.size, 1 << 15):
+        part = sel[s0:s0 + (1 << 15)]
+        h = gather(part)
+        good = ~np.any(h[:, tpl.fixed] != tpl.raw[tpl.fixed], axis=1)
+        d = np.ascontiguousarray(h[:, tpl.dims:tpl.dims + 8 * tpl.rank]).view("<u8")
+        lay = np.ascontiguousarray(h[:, tpl.layout:tpl.layout + 16]).view("<u8")
+        ok[part], dims[part], dadr[part], dsz[part] = good, d, lay[:, 0], lay[:, 1]
+    nel = np.prod(dims, axis=1, dtype=np.uint64) if tpl.rank else np.ones(addrs.size, np.uint64)
+    ok &= (dadr != UNDEF) & (dsz == nel * np.uint64(tpl.dtype.itemsize)) & (nel > 0)
+    ok &= dadr.astype(np.float64) + dsz.astype(np.float64) + r.base <= len(r.buf)
+    return ok, dims, dadr.astype(np.int64) + r.base, dsz.astype(np.int64)
+
+
+def _bulk_cells(r: _Reader, addrs: np.ndarray):
+    """Yield (indices, template, dims, data addresses, sizes) for the cells of ``addrs`` that
+    match a template taken from the first cell not yet matched (at most 8 tries), and finally
+    (indices, None, ...) for the rest, which are decoded one by one."""
+    rest = np.arange(addrs.size)
+    single = []
+    for _ in range(8):
+        if rest.size == 0:
+            break
+        tpl = _cell_template(r, int(addrs[rest[0]]))
+        ok = _match_cells(r, tpl, addrs[rest]) if tpl is not None else None
+        if ok is None or not ok[0][0]:
+            single.append(int(rest[0]))
+            rest = rest[1:]
+            continue
+        good, dims, dadr, dsz = ok
+        yield rest[good], tpl, dims[good], dadr[good], dsz[good]
+        rest = rest[~good]
+    if single or rest.size:
+        yield np.concatenate([np.asarray(single, dtype=np.int64), rest]), None, None, None, None
+
+
+def _decode_cells(r: _Reader, addrs: np.ndarray) -> list:
+    """``[_decode(r, a) for a in addrs]``, with numeric / logical cells read in bulk."""
+    out = [None] * addrs.size
+    buf = r.buf
+    for idx, tpl, dims, dadr, dsz in _bulk_cells(r, addrs):
+        if tpl is None:
+            for i in idx.tolist():
+                out[i] = _decode(r, int(addrs[i]))
+            continue
+        dt, native = tpl.dtype, tpl.dtype.newbyteorder("=")
+        if tpl.empty:
+            zdt = bool if tpl.cls == "logical" else _CLASS_DTYPE[tpl.cls]
+            for i, a, n in zip(idx.tolist(), dadr.tolist(), dsz.tolist()):
+                raw = np.frombuffer(buf[a:a + n], dtype=dt)
+                out[i] = np.zeros(tuple(int(x) for x in raw), dtype=zdt)
+            continue
+        logical = tpl.cls == "logical"
+        for i, d, a, n in zip(idx.tolist(), dims.tolist(), dadr.tolist(), dsz.tolist()):
+            x = np.frombuffer(buf[a:a + n], dtype=dt).reshape(d).T.astype(native, copy=False)
+            out[i] = x.astype(bool) if logical else x
     return out
 
 
@@ -1035,7 +1188,69 @@ class MatFile:
         if kind != "ref":
             raise TypeError(f"{name} is not a cell array")
         flat = arr.ravel()                  # MATLAB column-major order
-        return [_decode(self._r, int(flat[i])) for i in np.asarray(indices, dtype=np.int64)]
+        return _decode_cells(self._r, flat[np.asarray(indices, dtype=np.int64)].astype(np.int64))
+
+    def cell_vectors(self, name: str, indices, dtype) -> tuple[np.ndarray, np.ndarray]:
+        """The selected cells of a cell array of vectors, ravelled and concatenated in ``dtype``:
+        (values, per-cell lengths) -- ``np.concatenate([c.ravel() for c in cell_elements(...)])``
+        without a Python object per cell where the cells match a header template (logical cells
+        come back as 0 / 1).  A matrix cell is ravelled in MATLAB (column-major) order.  Cells
+        that follow each other in the selection and in the file (writers lay a cell array's data
+        out in order, at most a few alignment bytes apart) are copied as one run."""
+        arr, _, kind = self._r.dataset(self._links[name])
+        if kind != "ref":
+            raise TypeError(f"{name} is not a cell array")
+        addrs = arr.ravel()[np.asarray(indices, dtype=np.int64)].astype(np.int64)
+        dtype = np.dtype(dtype)
+        lengths = np.zeros(addrs.size, dtype=np.int64)
+        slow, groups = {}, []
+        for idx, tpl, dims, dadr, dsz in _bulk_cells(self._r, addrs):
+            if tpl is None or tpl.empty:
+                for i in idx.tolist():
+                    c = np.asarray(_decode(self._r, int(addrs[i])))
+                    if c.dtype.kind not in "biuf":
+                        raise TypeError(f"{name}: cell {i} is not a real numeric or logical array")
+                    slow[i] = c.ravel(order="F")
+                    lengths[i] = slow[i].size
+            else:
+                lengths[idx] = dsz // tpl.dtype.itemsize
+                groups.append((idx, tpl, dadr, dsz))
+        offs = np.zeros(addrs.size + 1, dtype=np.int64)
+        np.cumsum(lengths, out=offs[1:])
+        vals = np.empty(int(offs[-1]), dtype=dtype)
+        for i, c in slow.items():
+            vals[offs[i]:offs[i + 1]] = c
+        for idx, tpl, dadr, dsz in groups:
+            self._copy_runs(vals, offs, idx, tpl, dadr, dsz)
+        return vals, lengths
+
+    def _copy_runs(self, vals, offs, idx, tpl, dadr, dsz):
+        """vals[offs[i]:offs[i+1]] = cell i's data for the cells ``idx`` of one template, one
+        numpy copy per run of cells adjacent in the selection and in the file."""
+        src, logical = tpl.dtype, tpl.cls == "logical"
+        end = dadr + dsz
+        gap = dadr[1:] - end[:-1]
+        brk = np.flatnonzero((idx[1:] != idx[:-1] + 1) | (gap < 0) | (gap >= 64)) + 1
+        starts = np.concatenate([[0], brk]).tolist()
+        stops = np.concatenate([brk, [idx.size]]).tolist()
+        u8 = self._r.mm
+        direct = not logical and src == vals.dtype
+        for j0, j1 in zip(starts, stops):
+            lo, hi = int(dadr[j0]), int(end[j1 - 1])
+            o0, o1 = int(offs[idx[j0]]), int(offs[idx[j1 - 1] + 1])
+            if direct and hi - lo == (o1 - o0) * src.itemsize:
+                # one read straight into the output (no faults on the file map)
+                if os.preadv(self._r.f.fileno(), [vals[o0:o1].view(np.uint8)], lo) != hi - lo:
+                    raise ValueError(f"{self._r.f.name}: short read at {lo}")
+                continue
+            span = u8[lo:hi]                                  # a view of the file map
+            if hi - lo != int(dsz[j0:j1].sum()):              # alignment gaps between the cells
+                runs = np.empty(2 * (j1 - j0) - 1, dtype=np.int64)
+                runs[0::2], runs[1::2] = dsz[j0:j1], gap[j0:j1 - 1]
+                keep = np.repeat(np.arange(runs.size) % 2 == 0, runs)
+                span = span[keep]
+            x = span.view(src)
+            vals[o0:o1] = x != 0 if logical else x
 
     def cell_count(self, name: str) -> int:
         arr, _, kind = self._r.dataset(self._links[name])
@@ -1043,6 +1258,68 @@ class MatFile:
 
     def close(self):
         self._r.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
+class LazyMat(dict):
+    """``loadmat73(path)`` that decodes each variable on first access: a dict whose ``[]``,
+    ``get`` and ``in`` see every variable of the file, while iteration, ``len`` and ``items``
+    decode the rest first.  ``close()`` (or a ``with`` block) releases the file; values decoded
+    by then stay valid."""
+
+    def __init__(self, path: str):
+        super().__init__()
+        self._mf = MatFile(path)
+        self._names = [n for n in self._mf.names()]
+
+    def __missing__(self, key):
+        if self._mf is None or key not in self._names:
+            raise KeyError(key)
+        val = self._mf.load(key)
+        self[key] = val
+        return val
+
+    def __contains__(self, key):
+        return dict.__contains__(self, key) or key in self._names
+
+    def get(self, key, default=None):
+        return self[key] if key in self else default
+
+    def _load_all(self):
+        for n in self._names:
+            if not dict.__contains__(self, n):
+                self[n]                                            # noqa: B018 (decodes it)
+
+    def keys(self):
+        self._load_all()
+        return super().keys()
+
+    def values(self):
+        self._load_all()
+        return super().values()
+
+    def items(self):
+        self._load_all()
+        return super().items()
+
+    def __iter__(self):
+        self._load_all()
+        return super().__iter__()
+
+    def __len__(self):
+        self._load_all()
+        return super().__len__()
+
+    def close(self):
+        if self._mf is not None:
+            self._mf.close()
+            self._mf = None
+            self._names = [n for n in self._names if dict.__contains__(self, n)]
 
     def __enter__(self):
         return self

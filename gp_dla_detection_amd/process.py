@@ -259,6 +259,38 @@ def load_preloaded_qsos(path: str, test_ind=None) -> list[dict]:
                                   cols["all_pixel_mask"])]
 
 
+def load_preloaded_qsos_packed(path: str, test_ind=None) -> dict:
+    """``pack_spectra(load_preloaded_qsos(path, test_ind))`` without z_qsos (the caller attaches
+    them from the catalogue): the engine's CSR arrays straight from the file, with the cells of a
+    v7.3 file read in bulk (matv73.MatFile.cell_vectors) rather than decoded one by one."""
+    from .matv73 import MatFile, is_matv73
+    if not is_matv73(path):
+        lst = load_preloaded_qsos(path, test_ind)
+        if not lst:
+            return dict(offsets=np.zeros(1, np.int64), wavelengths=np.zeros(0), flux=np.zeros(0),
+                        noise_variance=np.zeros(0), pixel_mask=np.zeros(0, np.uint8))
+        out = pack_spectra([dict(s, z_qso=0.0) for s in lst])
+        del out["z_qsos"]
+        return out
+    keys = (("wavelengths", "all_wavelengths", np.float64), ("flux", "all_flux", np.float64),
+            ("noise_variance", "all_noise_variance", np.float64), ("pixel_mask", "all_pixel_mask", np.uint8))
+    out = {}
+    with MatFile(path) as mf:
+        idx = _indices(test_ind, mf.cell_count("all_wavelengths"))
+        lengths = None
+        for key, var, dt in keys:
+            out[key], n = mf.cell_vectors(var, idx, dt)
+            if lengths is None:
+                lengths = n
+            elif not np.array_equal(n, lengths):
+                q = int(np.flatnonzero(n != lengths)[0])
+                raise ValueError(f"preloaded_qsos: spectrum {int(idx[q])} has {int(lengths[q])} wavelengths "
+                                 f"but {int(n[q])} entries in {var}")
+    out["offsets"] = np.zeros(idx.size + 1, dtype=np.int64)
+    np.cumsum(lengths, out=out["offsets"][1:])
+    return out
+
+
 def _indices(sel, n: int) -> np.ndarray:
     if sel is None:
         return np.arange(n)
@@ -301,7 +333,7 @@ def run_process_qsos(base_directory: str, training_release: str, training_set_na
     v7.3 file, :222-249).
     Rank 0 returns the saved scalars; other ranks their local results."""
     import time
-    from .matv73 import LazyArray, auto_chunk_rows, loadmat, write_chunks
+    from .matv73 import LazyArray, LazyMat, auto_chunk_rows, is_matv73, loadmat, write_chunks
     from .shard import block_lpt_shards, expected_pixels, merge_shards
     compute = compute or _engine_compute
     tm = timings if timings is not None else {}
@@ -316,7 +348,8 @@ def run_process_qsos(base_directory: str, training_release: str, training_set_na
     model = load_model(f"{tdir}/learned_qso_model_{training_set_name}.mat")
     samples = load_dla_samples(f"{tdir}/dla_samples.mat")
     params = params or set_parameters(k=np.asarray(model["M"]).shape[1])
-    catalog = loadmat(f"{rdir}/catalog.mat")
+    # the release catalogue: only what test_ind names, and z_qsos, is decoded (not its z_dlas cells)
+    catalog = LazyMat(f"{rdir}/catalog.mat") if is_matv73(f"{rdir}/catalog.mat") else loadmat(f"{rdir}/catalog.mat")
     side = f"{rdir}/catalog_filter_flags.mat"
     if os.path.exists(side):
         # preload_qsos's filter_flags when catalog.mat could not take them in place (ingest.py:
@@ -325,16 +358,14 @@ def run_process_qsos(base_directory: str, training_release: str, training_set_na
     tind = evaluate_index(test_ind, catalog=catalog).astype(bool).ravel()
     tidx = np.flatnonzero(tind)
     z_all = np.asarray(catalog["z_qsos"], dtype=np.float64).ravel()[tidx]
+    if isinstance(catalog, LazyMat):
+        catalog.close()
     S = np.asarray(samples["nhi_samples"]).size
     chunk_rows = chunk_rows or auto_chunk_rows(S, 8, tidx.size)
     shards = block_lpt_shards(expected_pixels(z_all), chunk_rows, world)
     mine = shards[rank]
-    spectra = load_preloaded_qsos(f"{rdir}/preloaded_qsos.mat", tidx[mine])
-    for sp, z in zip(spectra, z_all[mine]):
-        sp["z_qso"] = float(z)
-    packed = pack_spectra(spectra) if spectra else dict(
-        offsets=np.zeros(1, np.int64), wavelengths=np.zeros(0), flux=np.zeros(0), noise_variance=np.zeros(0),
-        pixel_mask=np.zeros(0, np.uint8), z_qsos=np.zeros(0))
+    packed = load_preloaded_qsos_packed(f"{rdir}/preloaded_qsos.mat", tidx[mine])
+    packed["z_qsos"] = np.ascontiguousarray(z_all[mine], dtype=np.float64)
     t_load = time.perf_counter()
     tm["load_s"] = t_load - t_start
     if compute is _engine_compute:  # the compute phase split: engine creation, then the batches

@@ -154,6 +154,21 @@ def test_reads_libhdf5_written_matlab_files(tag):
     cells = r["all_flux"].ravel(order="F")
     assert np.array_equal([c.shape[0] for c in cells], exp[f"{tag}__cell_lengths"])
     assert np.array_equal(np.concatenate([c[:, 0] for c in cells]), exp[f"{tag}__cell_concat"])
+    # the bulk cell reader: libhdf5's v1 headers (with their modification-time messages) match a
+    # template, its chunked cells and v2 headers are decoded one by one; same values either way
+    with M.MatFile(str(GOLDEN / f"mat73_{tag}.mat")) as mf:
+        n = mf.cell_count("all_flux")
+        vals, lens = mf.cell_vectors("all_flux", np.arange(n), np.float64)
+        assert np.array_equal(lens, exp[f"{tag}__cell_lengths"]) and np.array_equal(vals, exp[f"{tag}__cell_concat"])
+        sel = np.arange(n)[::-3]
+        vals, lens = mf.cell_vectors("all_flux", sel, np.float32)
+        assert vals.dtype == np.float32 and np.array_equal(vals, np.concatenate([cells[i][:, 0] for i in sel]).astype(np.float32))
+        if tag == "earliest":
+            addrs = mf._r.dataset(mf._links["all_flux"])[0].ravel().astype(np.int64)
+            groups = list(M._bulk_cells(mf._r, addrs))
+            assert [g[1] is not None for g in groups] == [True, False]
+            chunked = [i for i in range(n) if dict(mf._r.messages(int(addrs[i])))[0x08][1] == 2]
+            assert sorted(groups[1][0].tolist()) == chunked and len(chunked) == 11   # the deflated ones
     if tag == "earliest":
         assert r["release"] == "dr12q" and r["empty_var"].shape == (0, 5)
 
@@ -326,6 +341,89 @@ def test_reference_tree_loaders(tmp_path):
     assert len(sp) == len(spectra)
     for a, b in zip(sp, spectra):
         assert np.array_equal(a["flux"], b["flux"]) and np.array_equal(a["pixel_mask"], b["pixel_mask"])
+
+
+def _per_cell(mf, name, idx):
+    addrs = mf._r.dataset(mf._links[name])[0].ravel().astype(np.int64)
+    return [M._decode(mf._r, int(addrs[i])) for i in idx]
+
+
+def test_bulk_cells_match_per_cell_decode(tmp_path):
+    """matv73's bulk cell reader (header templates, run-coalesced copies) against decoding every cell
+    on its own: cell arrays mixing doubles of every length (empty included), a matrix, single,
+    int32, logical (1-byte data, padded apart in the file), char and nested cells; sorted, reversed,
+    repeated and sparse selections."""
+    rng = np.random.default_rng(11)
+    mixed = [rng.standard_normal(int(n)) for n in rng.integers(1, 40, 50)]
+    mixed[3] = np.zeros(0)
+    mixed[7] = rng.standard_normal((3, 4))
+    mixed[9] = np.float32([1.5, -2.5, 3.0])
+    mixed[11] = np.arange(5, dtype=np.int32)
+    mixed[13] = rng.uniform(size=6) < 0.5
+    mixed[20] = "abc"
+    mixed[21] = [np.arange(2.0), "x"]
+    masks = [rng.uniform(size=int(n)) < 0.3 for n in rng.integers(1, 30, 40)]
+    path = str(tmp_path / "cells.mat")
+    M.savemat73(path, dict(mixed=mixed, masks=masks, plain=[rng.standard_normal(int(n)) for n in rng.integers(1, 9, 64)]))
+    with M.MatFile(path) as mf:
+        for name, n in (("mixed", 50), ("masks", 40), ("plain", 64)):
+            for idx in (np.arange(n), np.arange(n)[::-1], np.array([0, 0, 5, 4, n - 1, 5]), np.arange(1, n, 3)):
+                ref = _per_cell(mf, name, idx)
+                got = mf.cell_elements(name, idx)
+                for a, b in zip(ref, got):
+                    if isinstance(a, np.ndarray) and a.dtype != object:
+                        assert a.dtype == b.dtype and a.shape == b.shape and np.array_equal(a, b)
+                    else:
+                        assert type(a) is type(b)
+                if name == "mixed":
+                    idx = idx[~np.isin(idx, (20, 21))]   # char / cell cells are not numeric vectors
+                    ref = _per_cell(mf, name, idx)
+                for dt in (np.float64, np.uint8) if name == "masks" else (np.float64,):
+                    vals, lens = mf.cell_vectors(name, idx, dt)
+                    exp = [np.asarray(c).ravel(order="F") for c in ref]
+                    assert np.array_equal(lens, [c.size for c in exp])
+                    assert vals.dtype == dt and np.array_equal(vals, np.concatenate(exp).astype(dt))
+        with pytest.raises(TypeError):
+            mf.cell_vectors("mixed", [20], np.float64)
+        addrs = mf._r.dataset(mf._links["plain"])[0].ravel().astype(np.int64)
+        assert [t is not None for _, t, *_ in M._bulk_cells(mf._r, addrs)] == [True]
+
+
+def test_preloaded_packed_matches_per_spectrum_load(tmp_path):
+    """process.load_preloaded_qsos_packed (run_process_qsos's loader) == pack_spectra of the per-
+    spectrum load, for a test_ind selection with gaps; cells of unequal length are refused."""
+    _, _, spectra, catalog = write_reference_tree(tmp_path)
+    pre = str(tmp_path / "dr12q" / "processed" / "preloaded_qsos.mat")
+    for sel in (None, np.arange(len(spectra)) % 3 != 1, np.array([4, 0, 2])):
+        lst = PR.load_preloaded_qsos(pre, sel)
+        exp = syn.pack_spectra([dict(s, z_qso=0.0) for s in lst])
+        got = PR.load_preloaded_qsos_packed(pre, sel)
+        for k in ("offsets", "wavelengths", "flux", "noise_variance", "pixel_mask"):
+            assert got[k].dtype == exp[k].dtype and np.array_equal(got[k], exp[k]), k
+    empty = PR.load_preloaded_qsos_packed(pre, np.zeros(len(spectra), dtype=bool))
+    assert empty["offsets"].tolist() == [0] and empty["flux"].size == 0
+    bad = str(tmp_path / "bad.mat")
+    M.savemat73(bad, dict(all_wavelengths=[np.arange(3.0), np.arange(4.0)], all_flux=[np.arange(3.0), np.arange(5.0)],
+                          all_noise_variance=[np.ones(3), np.ones(4)], all_pixel_mask=[np.zeros(3, bool), np.zeros(4, bool)]))
+    with pytest.raises(ValueError, match="spectrum 1 has 4 wavelengths"):
+        PR.load_preloaded_qsos_packed(bad)
+
+
+def test_lazy_mat_decodes_on_access(tmp_path):
+    path = str(tmp_path / "c.mat")
+    M.savemat73(path, dict(z_qsos=np.arange(4.0), filter_flags=np.zeros(4, np.uint8),
+                           z_dlas=dict(dr9q_concordance=[np.arange(2.0), np.zeros(0)])))
+    with M.LazyMat(path) as lz:
+        assert "z_dlas" in lz and "nope" not in lz and dict.__len__(lz) == 0
+        assert np.array_equal(lz["z_qsos"].ravel(), np.arange(4.0)) and dict.__len__(lz) == 1
+        lz["filter_flags"] = np.ones(4)
+        assert lz.get("nope") is None and lz.get("filter_flags").sum() == 4
+        assert sorted(lz) == ["filter_flags", "z_dlas", "z_qsos"]
+        full = M.loadmat73(path)
+        assert np.array_equal(lz["z_dlas"]["dr9q_concordance"][0, 0], full["z_dlas"]["dr9q_concordance"][0, 0])
+    assert np.array_equal(lz["z_qsos"], full["z_qsos"])     # decoded values outlive the file
+    with pytest.raises(KeyError):
+        lz["nope"]
 
 
 def test_update_variable_requires_matching_shape(tmp_path):
