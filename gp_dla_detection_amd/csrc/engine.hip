@@ -96,6 +96,22 @@ struct TimedLaunch {
   int kind;  // 0 prep, 1 likelihood, 2 reduce, 3 contraction (panel-GEMM paths, inside 1)
 };
 
+// One of the two staging sets of the host-buffer pipeline (gpdla_engine_process with host inputs
+// and host results): the batch's inputs and results on the device, and the events that order the
+// copy stream against the compute stream.
+struct HostStage {
+  double *wl = nullptr, *flux = nullptr, *noise = nullptr, *z = nullptr;
+  uint8_t* mask = nullptr;
+  double *sll = nullptr, *llnull = nullptr, *lldla = nullptr, *zmin = nullptr, *zmax = nullptr;
+  int32_t* npix = nullptr;
+  size_t cap_wl = 0, cap_flux = 0, cap_noise = 0, cap_mask = 0, cap_z = 0, cap_sll = 0;
+  size_t cap_o[5] = {0, 0, 0, 0, 0};
+  hipEvent_t in_ready = nullptr;   // copy stream: this batch's inputs are on the device
+  hipEvent_t in_free = nullptr;    // compute stream: prep_kernel has read them
+  hipEvent_t out_ready = nullptr;  // compute stream: the batch's results are written
+  hipEvent_t out_free = nullptr;   // copy stream: they are back on the host
+};
+
 }  // namespace
 
 struct gpdla_engine {
@@ -145,6 +161,11 @@ struct gpdla_engine {
   size_t cap_ai8 = 0;
   double *d_psc = nullptr, *d_pent = nullptr;
   size_t cap_pi8 = 0, cap_psc = 0, cap_pent = 0;
+
+  // host-buffer pipeline: batch b's results are copied back, and batch b + 1's inputs copied in, on
+  // copy_stream while batch b + 1 (resp. b) computes; the two stages alternate
+  HostStage hs[2];
+  hipStream_t copy_stream = nullptr;
 
   // pinned host metadata (reused after meta_ready completes)
   int64_t* h_meta = nullptr;
@@ -230,7 +251,16 @@ void gpdla_engine_destroy(gpdla_engine* e) {
   if (!e) return;
   (void)hipSetDevice(e->device);
   if (e->stream) (void)hipStreamSynchronize(e->stream);
+  if (e->copy_stream) (void)hipStreamSynchronize(e->copy_stream);
   for (auto& t : e->pending) { (void)hipEventDestroy(t.start); (void)hipEventDestroy(t.stop); }
+  for (HostStage& h : e->hs) {
+    void* hb[] = {h.wl, h.flux, h.noise, h.z, h.mask, h.sll, h.llnull, h.lldla, h.zmin, h.zmax, h.npix};
+    for (void* b : hb)
+      if (b) (void)hipFree(b);
+    for (hipEvent_t ev : {h.in_ready, h.in_free, h.out_ready, h.out_free})
+      if (ev) (void)hipEventDestroy(ev);
+  }
+  if (e->copy_stream) (void)hipStreamDestroy(e->copy_stream);
   void* bufs[] = {e->d_rest, e->d_mu, e->d_M, e->d_logom, e->d_off, e->d_nhi, e->d_perm, e->d_lines,
                   e->d_status, e->d_meta, e->d_wl, e->d_flux, e->d_noise, e->d_mask, e->d_z,
                   e->d_info, e->d_panel, e->d_lam, e->d_smap, e->d_scratch, e->d_sll,
@@ -438,6 +468,48 @@ static int run_panel_gemm(gpdla_engine* e, bool i8, int64_t nq, const int64_t* h
   return GPDLA_OK;
 }
 
+// The host-buffer pipeline's stages, sized for the largest batch of this call (no reallocation
+// while copies or kernels may still use a stage), its copy stream and events.
+static int host_stages_prepare(gpdla_engine* e, int64_t max_pix, int64_t max_q) {
+  if (!e->copy_stream) HIP_TRY(hipStreamCreateWithFlags(&e->copy_stream, hipStreamNonBlocking));
+  for (HostStage& h : e->hs) {
+    int rc;
+    if ((rc = grow(&h.wl, &h.cap_wl, (size_t)max_pix))) return rc;
+    if ((rc = grow(&h.flux, &h.cap_flux, (size_t)max_pix))) return rc;
+    if ((rc = grow(&h.noise, &h.cap_noise, (size_t)max_pix))) return rc;
+    if ((rc = grow(&h.mask, &h.cap_mask, (size_t)max_pix))) return rc;
+    if ((rc = grow(&h.z, &h.cap_z, (size_t)max_q))) return rc;
+    if ((rc = grow(&h.sll, &h.cap_sll, (size_t)(max_q * e->S)))) return rc;
+    if ((rc = grow(&h.llnull, &h.cap_o[0], (size_t)max_q))) return rc;
+    if ((rc = grow(&h.lldla, &h.cap_o[1], (size_t)max_q))) return rc;
+    if ((rc = grow(&h.zmin, &h.cap_o[2], (size_t)max_q))) return rc;
+    if ((rc = grow(&h.zmax, &h.cap_o[3], (size_t)max_q))) return rc;
+    if ((rc = grow(&h.npix, &h.cap_o[4], (size_t)max_q))) return rc;
+    for (hipEvent_t* ev : {&h.in_ready, &h.in_free, &h.out_ready, &h.out_free})
+      if (!*ev) HIP_TRY(hipEventCreateWithFlags(ev, hipEventDisableTiming));
+  }
+  return GPDLA_OK;
+}
+
+// Batch [q0, q0 + nq)'s results from its stage back to the host, on the copy stream once the
+// compute stream has written them.  With pageable host memory the call returns when the copy is
+// done; the caller has already queued the next batch's kernels, so the device keeps computing.
+static int host_stage_copy_out(gpdla_engine* e, const gpdla_results* res, int64_t bi, int64_t q0, int64_t nq) {
+  HostStage& h = e->hs[bi & 1];
+  hipStream_t cs = e->copy_stream;
+  HIP_TRY(hipStreamWaitEvent(cs, h.out_ready, 0));
+  HIP_TRY(hipMemcpyAsync(res->log_likelihoods_no_dla + q0, h.llnull, nq * 8, hipMemcpyDeviceToHost, cs));
+  HIP_TRY(hipMemcpyAsync(res->log_likelihoods_dla + q0, h.lldla, nq * 8, hipMemcpyDeviceToHost, cs));
+  if (res->min_z_dlas) HIP_TRY(hipMemcpyAsync(res->min_z_dlas + q0, h.zmin, nq * 8, hipMemcpyDeviceToHost, cs));
+  if (res->max_z_dlas) HIP_TRY(hipMemcpyAsync(res->max_z_dlas + q0, h.zmax, nq * 8, hipMemcpyDeviceToHost, cs));
+  if (res->num_pixels) HIP_TRY(hipMemcpyAsync(res->num_pixels + q0, h.npix, nq * 4, hipMemcpyDeviceToHost, cs));
+  if (res->sample_log_likelihoods_dla)
+    HIP_TRY(hipMemcpy2DAsync(res->sample_log_likelihoods_dla + q0 * res->sample_ld, res->sample_ld * 8, h.sll,
+                             e->S * 8, e->S * 8, nq, hipMemcpyDeviceToHost, cs));
+  HIP_TRY(hipEventRecord(h.out_free, cs));
+  return GPDLA_OK;
+}
+
 int gpdla_engine_process(gpdla_engine* e, const gpdla_spectra* sp, const gpdla_results* res) {
   if (!e || !sp || !res) return set_error(GPDLA_EINVAL, "null argument");
   const int64_t Q = sp->num_spectra;
@@ -485,8 +557,26 @@ int gpdla_engine_process(gpdla_engine* e, const gpdla_spectra* sp, const gpdla_r
     e->cap_hmeta = per_batch * nbatch;
   }
 
+  // host inputs and host results: the two-stage pipeline (copies beside the kernels)
+  const bool pipe = !in_dev && !out_dev;
+  if (pipe) {
+    int64_t max_pix = 0;
+    for (int64_t bi = 0; bi < nbatch; ++bi)
+      max_pix = std::max(max_pix, sp->offsets[std::min(Q, (bi + 1) * QB)] - sp->offsets[bi * QB]);
+    int rc;
+    if ((rc = host_stages_prepare(e, max_pix, std::min(Q, QB)))) return rc;
+    // the previous call's copies are done (it synchronised); order this call after any other
+    // work on the engine's stream, then keep the two streams apart except through the events
+    HIP_TRY(hipStreamSynchronize(e->copy_stream));
+    for (HostStage& h : e->hs) {
+      HIP_TRY(hipEventRecord(h.in_free, st));
+      HIP_TRY(hipEventRecord(h.out_free, e->copy_stream));
+    }
+  }
+
   for (int64_t bi = 0; bi < nbatch; ++bi) {
     const int64_t q0 = bi * QB, q1 = std::min(Q, q0 + QB), nq = q1 - q0;
+    HostStage& hst = e->hs[bi & 1];
     int64_t* hm = e->h_meta + bi * per_batch;
     int64_t* h_off = hm;
     int64_t* h_sb = hm + (QB + 1);
@@ -584,6 +674,18 @@ int gpdla_engine_process(gpdla_engine* e, const gpdla_spectra* sp, const gpdla_r
     if (in_dev) {
       wl = sp->wavelengths + pbase; fl = sp->flux + pbase; nv = sp->noise_variance + pbase;
       mk = sp->pixel_mask + pbase; zq = sp->z_qsos + q0;
+    } else if (pipe) {
+      // into this batch's stage once batch bi - 2's prep_kernel has read it, beside batch bi - 1
+      hipStream_t cs = e->copy_stream;
+      HIP_TRY(hipStreamWaitEvent(cs, hst.in_free, 0));
+      HIP_TRY(hipMemcpyAsync(hst.wl, sp->wavelengths + pbase, npix * 8, hipMemcpyHostToDevice, cs));
+      HIP_TRY(hipMemcpyAsync(hst.flux, sp->flux + pbase, npix * 8, hipMemcpyHostToDevice, cs));
+      HIP_TRY(hipMemcpyAsync(hst.noise, sp->noise_variance + pbase, npix * 8, hipMemcpyHostToDevice, cs));
+      HIP_TRY(hipMemcpyAsync(hst.mask, sp->pixel_mask + pbase, npix, hipMemcpyHostToDevice, cs));
+      HIP_TRY(hipMemcpyAsync(hst.z, sp->z_qsos + q0, nq * 8, hipMemcpyHostToDevice, cs));
+      HIP_TRY(hipEventRecord(hst.in_ready, cs));
+      HIP_TRY(hipStreamWaitEvent(st, hst.in_ready, 0));
+      wl = hst.wl; fl = hst.flux; nv = hst.noise; mk = hst.mask; zq = hst.z;
     } else {
       if ((rc = grow(&e->d_wl, &e->cap_wl, (size_t)npix))) return rc;
       if ((rc = grow(&e->d_flux, &e->cap_flux, (size_t)npix))) return rc;
@@ -602,7 +704,7 @@ int gpdla_engine_process(gpdla_engine* e, const gpdla_spectra* sp, const gpdla_r
     double *o_sll, *o_null, *o_dla, *o_zmin, *o_zmax;
     int32_t* o_npix;
     int64_t ld;
-    const bool need_internal_sll = !out_dev || !res->sample_log_likelihoods_dla;
+    const bool need_internal_sll = !pipe && (!out_dev || !res->sample_log_likelihoods_dla);
     if (need_internal_sll) {
       if ((rc = grow(&e->d_sll, &e->cap_sll, (size_t)nq * e->S))) return rc;
     }
@@ -614,6 +716,11 @@ int gpdla_engine_process(gpdla_engine* e, const gpdla_spectra* sp, const gpdla_r
       o_zmin = res->min_z_dlas ? res->min_z_dlas + q0 : nullptr;
       o_zmax = res->max_z_dlas ? res->max_z_dlas + q0 : nullptr;
       o_npix = res->num_pixels ? res->num_pixels + q0 : nullptr;
+    } else if (pipe) {
+      // this batch's stage, once batch bi - 2's results have left it
+      HIP_TRY(hipStreamWaitEvent(st, hst.out_free, 0));
+      o_sll = hst.sll; ld = e->S;
+      o_null = hst.llnull; o_dla = hst.lldla; o_zmin = hst.zmin; o_zmax = hst.zmax; o_npix = hst.npix;
     } else {
       if (e->cap_qout < (size_t)QB) {
         for (double** p : {&e->d_llnull, &e->d_lldla, &e->d_zmin, &e->d_zmax})
@@ -677,6 +784,7 @@ int gpdla_engine_process(gpdla_engine* e, const gpdla_spectra* sp, const gpdla_r
     TimedLaunch t0{}, t1{}, t2{};
     if ((rc = record_start(e, &t0, 0))) return rc;
     HIP_TRY(launch_prep(e->gemm ? 0 : e->K, pa, st));
+    if (pipe) HIP_TRY(hipEventRecord(hst.in_free, st));
     if (batch_i8) HIP_TRY(launch_convert_i8(e->K, ca, st));
     if (batch_gemm_i8) {
       ConvertGemmI8Args cg{};
@@ -706,7 +814,11 @@ int gpdla_engine_process(gpdla_engine* e, const gpdla_spectra* sp, const gpdla_r
     e->stats.spectra += nq;
     e->stats.sample_evals += nq * e->S;
 
-    if (!out_dev) {
+    if (pipe) {
+      HIP_TRY(hipEventRecord(hst.out_ready, st));
+      // the previous batch's results, now that this batch is queued behind it
+      if (bi > 0 && (rc = host_stage_copy_out(e, res, bi - 1, q0 - QB, QB))) return rc;
+    } else if (!out_dev) {
       HIP_TRY(hipMemcpyAsync(res->log_likelihoods_no_dla + q0, o_null, nq * 8, hipMemcpyDeviceToHost, st));
       HIP_TRY(hipMemcpyAsync(res->log_likelihoods_dla + q0, o_dla, nq * 8, hipMemcpyDeviceToHost, st));
       if (res->min_z_dlas) HIP_TRY(hipMemcpyAsync(res->min_z_dlas + q0, o_zmin, nq * 8, hipMemcpyDeviceToHost, st));
@@ -723,7 +835,13 @@ int gpdla_engine_process(gpdla_engine* e, const gpdla_spectra* sp, const gpdla_r
     }
     // otherwise the next batch reuses the panel workspace in stream order
   }
+  if (pipe) {
+    const int64_t bl = nbatch - 1;
+    const int rc = host_stage_copy_out(e, res, bl, bl * QB, Q - bl * QB);
+    if (rc) return rc;
+  }
   HIP_TRY(hipEventRecord(e->meta_done, st));
+  if (pipe) HIP_TRY(hipStreamSynchronize(e->copy_stream));
   if (!out_dev) return gpdla_engine_synchronize(e);
   return GPDLA_OK;
 }

@@ -279,6 +279,39 @@ def test_device_path_equals_host_path():
     assert st["likelihood_launches"] == 2 and st["likelihood_ms"] > 0
 
 
+@pytest.mark.parametrize("path", ["auto", "fused_i8", "panel_gemm"])
+def test_host_pipeline_equals_device_path(path):
+    """The host-buffer pipeline (engine.hip: two device stages, inputs in and results out on a copy
+    stream beside the kernels) against the device-resident call, bitwise: 37 DR12Q-shaped spectra
+    in batches of 4 (10 batches, the last partial), then a second, longer call on the same engine
+    (its stages grow), results without the sample array, and one batch."""
+    model = syn.make_model(k=20)
+    samples = syn.make_samples(300)
+    spectra = syn.make_dr12q_like_spectra(model, 53, seed=4)
+    D = L.DeviceArray.from_numpy
+
+    def device_run(eng, packed):
+        t = {k: D(packed[k]) for k in ("wavelengths", "flux", "noise_variance", "pixel_mask", "z_qsos")}
+        Q = packed["z_qsos"].size
+        o = [L.DeviceArray(0, Q, np.float64) for _ in range(2)] + [L.DeviceArray(0, (Q, 300), np.float64)]
+        eng.process_device(packed["offsets"], t["wavelengths"].ptr, t["flux"].ptr, t["noise_variance"].ptr,
+                           t["pixel_mask"].ptr, t["z_qsos"].ptr, o[0].ptr, o[1].ptr, o[2].ptr, 300)
+        eng.synchronize()
+        return [x.numpy() for x in o]
+
+    with Engine(model, samples, set_parameters(k=20), max_batch_spectra=4, path=path) as eng:
+        for sel in (slice(0, 37), slice(0, 53), slice(40, 43)):
+            packed = syn.pack_spectra(spectra[sel])
+            host = eng.process(packed)
+            dev = device_run(eng, packed)
+            np.testing.assert_array_equal(host["log_likelihoods_no_dla"], dev[0])
+            np.testing.assert_array_equal(host["log_likelihoods_dla"], dev[1])
+            np.testing.assert_array_equal(host["sample_log_likelihoods_dla"], dev[2])
+        scalars = eng.process(packed, want_samples=False)
+        np.testing.assert_array_equal(scalars["log_likelihoods_dla"], dev[1])
+        assert "sample_log_likelihoods_dla" not in scalars
+
+
 TORCH_INTEROP = r"""
 import sys, numpy as np
 sys.path.insert(0, sys.argv[1])
