@@ -148,13 +148,16 @@ int gpdla_engine_create(int32_t device, const gpdla_model* model, const gpdla_sa
                         const gpdla_params* params, gpdla_engine** out);
 /* Enqueue the whole pipeline for all spectra.  With GPDLA_MEM_HOST results the call blocks until
  * the outputs are copied back; with device results it returns after enqueueing (use
- * gpdla_engine_synchronize).  Spectra may be processed in several device batches. */
+ * gpdla_engine_synchronize).  Spectra may be processed in several device batches.  With host
+ * inputs and host results the batches are pipelined: batch b's inputs are copied in, and batch
+ * b - 1's results copied out, on a copy stream of the engine's own while the kernels run. */
 int gpdla_engine_process(gpdla_engine* engine, const gpdla_spectra* spectra,
                          const gpdla_results* results);
 /* Wait for enqueued work; returns GPDLA_ENUMERIC if any pivot was non-positive since the last call. */
 int gpdla_engine_synchronize(gpdla_engine* engine);
-/* Use an external hipStream_t (NULL restores the engine's own stream).  All work of a process call
- * is ordered on that stream. */
+/* Use an external hipStream_t (NULL restores the engine's own stream).  All kernels of a process
+ * call are ordered on that stream (after the work already on it); the host-buffer copies above run on
+ * the engine's copy stream, ordered against it by events. */
 int gpdla_engine_set_stream(gpdla_engine* engine, void* hip_stream);
 int gpdla_engine_get_stats(gpdla_engine* engine, gpdla_stats* stats);
 /* The same, writing at most stats_bytes bytes (a caller's sizeof(gpdla_stats) from an older header). */
