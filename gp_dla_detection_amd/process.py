@@ -273,7 +273,7 @@ def load_preloaded_qsos_packed(path: str, test_ind=None) -> dict:
         del out["z_qsos"]
         return out
     keys = (("wavelengths", "all_wavelengths", np.float64), ("flux", "all_flux", np.float64),
-            ("noise_variance", "all_noise_variance", np.float64), ("pixel_mask", "all_pixel_mask", np.uint8))
+            ("noise_variance", "all_noise_variance", np.float64), ("pixel_mask", "all_pixel_mask", np.bool_))
     out = {}
     with MatFile(path) as mf:
         idx = _indices(test_ind, mf.cell_count("all_wavelengths"))
@@ -286,6 +286,7 @@ def load_preloaded_qsos_packed(path: str, test_ind=None) -> dict:
                 q = int(np.flatnonzero(n != lengths)[0])
                 raise ValueError(f"preloaded_qsos: spectrum {int(idx[q])} has {int(lengths[q])} wavelengths "
                                  f"but {int(n[q])} entries in {var}")
+    out["pixel_mask"] = out["pixel_mask"].view(np.uint8)   # 0 / 1, as pack_spectra of the bool masks
     out["offsets"] = np.zeros(idx.size + 1, dtype=np.int64)
     np.cumsum(lengths, out=out["offsets"][1:])
     return out

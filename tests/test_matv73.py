@@ -400,6 +400,12 @@ def test_preloaded_packed_matches_per_spectrum_load(tmp_path):
         got = PR.load_preloaded_qsos_packed(pre, sel)
         for k in ("offsets", "wavelengths", "flux", "noise_variance", "pixel_mask"):
             assert got[k].dtype == exp[k].dtype and np.array_equal(got[k], exp[k]), k
+    # a mask stored as uint8 (not logical) with values other than 0 / 1 still comes back 0 / 1
+    odd = str(tmp_path / "odd.mat")
+    M.savemat73(odd, dict(all_wavelengths=[np.arange(3.0)], all_flux=[np.ones(3)], all_noise_variance=[np.ones(3)],
+                          all_pixel_mask=[np.array([0, 2, 255], dtype=np.uint8)]))
+    assert PR.load_preloaded_qsos_packed(odd)["pixel_mask"].tolist() == [0, 1, 1]
+    assert PR.load_preloaded_qsos(odd)[0]["pixel_mask"].tolist() == [False, True, True]
     empty = PR.load_preloaded_qsos_packed(pre, np.zeros(len(spectra), dtype=bool))
     assert empty["offsets"].tolist() == [0] and empty["flux"].size == 0
     bad = str(tmp_path / "bad.mat")
