@@ -258,7 +258,7 @@ def run_e2e(args, world: int, rank: int, local_rank: int, dist) -> None:
 
 
 # rocprofv3 summaries of the bench workloads (tools/profile.sh + tools/summarize_profile.py), committed
-PROFILE_SUMMARY = ROOT / "profiles" / "r5e_c2_summary.json"     # configs[1], fused fp64
+PROFILE_SUMMARY = ROOT / "profiles" / "r5s_c2_summary.json"     # configs[1], fused fp64 (final round-3 tree)
 # configs[4]: summary file and the roofline kernel's name
 PROFILE_SUMMARY_C5 = {"panel-GEMM-int8": (ROOT / "profiles" / "r2a_c5_summary.json", "gemm_i8_kernel"),      # 32-bit
                       "panel-GEMM-int8-24": (ROOT / "profiles" / "r5k_c5_summary.json", "gemm_i8_"),  # 24-bit: bst + u
