@@ -115,19 +115,45 @@ def _numpy_worker(task):
     return done, el
 
 
+def host_cores() -> dict:
+    """The host cores this process may use: the affinity mask (sched_getaffinity), the cgroup CPU
+    quota (cpu.max, cgroup v2; a leased GPU box grants a share of a larger host this way), nproc and
+    the CPU model.  ``usable`` = the affinity count, capped by the quota when one is set."""
+    import math
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, period = Path("/sys/fs/cgroup/cpu.max").read_text().split()[:2]
+        if q != "max":
+            quota = float(q) / float(period)
+    except (OSError, ValueError):
+        pass
+    model = None
+    try:
+        for line in Path("/proc/cpuinfo").read_text().splitlines():
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    usable = aff if quota is None else max(1, min(aff, math.floor(quota)))
+    return {"affinity": aff, "cgroup_quota_cpus": quota, "nproc": os.cpu_count(), "cpu_model": model,
+            "usable": usable}
+
+
 def cpu_baseline(model, samples, spectra, budget_s: float, k: int) -> dict:
     """The reference's CPU path, restated in C++ with OpenMP over the DLA samples like its parfor
     (oracle/cpu_ref.cpp: process_qsos.m:184-198, voigt.c:253-304 with an own Faddeeva function in
-    place of libcerf, log_mvnpdf_low_rank.m:5-33 in MATLAB operation order), on the host threads
-    OpenMP is given (OMP_NUM_THREADS; the GPU box sets it to its 16-core per-GPU share).
+    place of libcerf, log_mvnpdf_low_rank.m:5-33 in MATLAB operation order), on every host core the
+    process is granted (host_cores(): the affinity mask capped by the cgroup quota).
     configs[0] (one spectrum, the null model only) is timed in full; the bench workload on a
     bounded subset: whole spectra (all S samples each), at least 16, until ``budget_s`` is spent.
     The numpy restatement on one core is reported beside it.  Runs before the GPU is touched."""
     import multiprocessing as mp
     from oracle import cpu_ref as CR
     from oracle import gpdla_oracle as O
-    threads = CR.threads()
-    preps = []
+    hc = host_cores()
+    threads = hc["usable"]
     # configs[0]: one spectrum, null-model log_mvnpdf_low_rank (process_qsos.m:150-152)
     s0 = spectra[0]
     p0 = O.prepare_spectrum(s0["wavelengths"], s0["flux"], s0["noise_variance"], s0["pixel_mask"], s0["z_qso"], model)
@@ -157,8 +183,10 @@ def cpu_baseline(model, samples, spectra, budget_s: float, k: int) -> dict:
     return {"value": done / el, "unit": "evals/s", "cores": threads, "kind": "port",
             "sample": f"{done} (spectrum, DLA-sample) evaluations = {nspec} whole spectra x {off.size} samples of the "
                       f"bench workload in {el:.1f} s; C++ OpenMP restatement of process_qsos.m:184-198 "
-                      f"(oracle/cpu_ref.cpp, MATLAB operation order, {threads} OpenMP threads = OMP_NUM_THREADS; "
-                      f"the host shows {os.cpu_count()} logical CPUs); MATLAB is not available; n=800, k={k}, 3 lines",
+                      f"(oracle/cpu_ref.cpp, MATLAB operation order, {threads} OpenMP threads = every core granted: "
+                      f"affinity {hc['affinity']}, cgroup quota {hc['cgroup_quota_cpus']}, nproc {hc['nproc']}); "
+                      f"MATLAB is not available; n=800, k={k}, 3 lines",
+            "host": hc,
             "configs0_null_eval_us": c1_us, "configs0_log_likelihood_no_dla": ll0,
             "numpy_1core": {"value": nd / nel, "unit": "evals/s", "cores": 1,
                             "sample": f"{nd} evaluations of spectrum 0 in {nel:.1f} s (oracle/gpdla_oracle.py)"}}
@@ -247,8 +275,11 @@ def run_e2e(args, world: int, rank: int, local_rank: int, dist) -> None:
                     "compute_split_rank0": {k: tm[k] for k in ("engine_create_s", "host_alloc_s", "engine_process_s")
                                             if k in tm},
                     "setup_untimed_s": setup_s, "output_bytes": out_bytes, "output_dir": base,
-                    "projection_8_gpus_s": {"load and compute scaled to 8 GPUs, write as measured": proj8 + write_s,
-                                            "devices_used": ndev},
+                    "projection_8_gpus_ideal_s": {
+                        "value": proj8 + write_s, "devices_used": ndev,
+                        "note": "ideal-scaling estimate, not a measurement: load x world/8 + compute x "
+                                "devices_used/8 (linear speed-up from the devices used to 8 assumed) + write "
+                                "as measured"},
                     "note": "load = catalogues, model, samples and this rank's preloaded_qsos cells "
                             "(process_qsos.m:1-63); compute = the engine incl. its creation (:88-212); "
                             "write = priors/posteriors and the v7.3 file (:222-249), page cache, no fsync"}}),
@@ -259,24 +290,37 @@ def run_e2e(args, world: int, rank: int, local_rank: int, dist) -> None:
 
 # rocprofv3 summaries of the bench workloads (tools/profile.sh + tools/summarize_profile.py), committed
 PROFILE_SUMMARY = ROOT / "profiles" / "r5s_c2_summary.json"     # configs[1], fused fp64 (final round-3 tree)
-# configs[4]: summary file and the roofline kernel's name
-PROFILE_SUMMARY_C5 = {"panel-GEMM-int8": (ROOT / "profiles" / "r2a_c5_summary.json", "gemm_i8_kernel"),      # 32-bit
-                      "panel-GEMM-int8-24": (ROOT / "profiles" / "r5k_c5_summary.json", "gemm_i8_"),  # 24-bit: bst + u
-                      "panel-GEMM": (ROOT / "profiles" / "r5f_c5f64_summary.json", "gemm_f64_kernel")}     # fp64
+# configs[4] (128 spectra x 10^5 samples, k = 50): the summary file and the EXACT names of the roofline
+# kernel's launches (the GEMM launches of one spectrum and sample chunk; per-batch conversion kernels
+# such as convert_gemm_i8_kernel are not part of it)
+PROFILE_SUMMARY_C5 = {
+    "panel-GEMM-int8": (ROOT / "profiles" / "r2a_c5_summary.json",
+                        ("gpdla::gemm_i8_kernel(gpdla::GemmI8Args)",)),
+    "panel-GEMM-int8-24": (ROOT / "profiles" / "r5k_c5_summary.json",
+                           ("gpdla::gemm_i8_bst_kernel(gpdla::GemmI8Args)",
+                            "void gpdla::gemm_i8_kernel<4>(gpdla::GemmI8Args)")),
+    "panel-GEMM": (ROOT / "profiles" / "r5f_c5f64_summary.json", ("gpdla::gemm_f64_kernel(gpdla::GemmF64Args)",)),
+}
+# the roofline kernel's label per path
+ROOFLINE_KERNEL = {"fused": "likelihood_kernel<{k}>", "fused-int8": "likelihood_i8_kernel<{k}>",
+                   "panel-GEMM-int8": "gemm_i8_kernel (Gram + u)",
+                   "panel-GEMM-int8-24": "gemm_i8_bst_kernel (Gram) + gemm_i8_kernel<4> (u)",
+                   "panel-GEMM": "gemm_f64_kernel (Gram + u)"}
 
 
 def profiled_traffic(Q: int, S: int, k: int, path: str = "fused"):
     """HBM bytes per launch of the roofline kernel from the committed PMC profile of the workload
     (2 x FETCH_SIZE + WRITE_SIZE, gfx950 correction per MI355X_MICROARCH.md; includes Infinity-Cache
-    hits): the fused kernel for configs[1]; for configs[4] the int8 GEMM launches of one spectrum and
-    sample chunk (the Gram and u launches of the 24-bit path together).  None for other workloads or
-    if no summary is present."""
+    hits): the fused kernel for configs[1]; for configs[4] the GEMM launches of one spectrum and
+    sample chunk (the Gram and u launches of the 24-bit path together), matched by exact kernel
+    name.  None for other workloads or if no summary is present."""
     if (Q, S, k) == (128, 100000, 50) and path in PROFILE_SUMMARY_C5 and PROFILE_SUMMARY_C5[path][0].exists():
-        f, kname = PROFILE_SUMMARY_C5[path]
+        f, names = PROFILE_SUMMARY_C5[path]
         d = json.loads(f.read_text())
-        rows = [e for e in d["kernels"] if kname in e["kernel"] and "hbm_bytes_per_launch" in e]
-        if rows:
-            return sum(e["hbm_bytes_per_launch"] for e in rows), f"{f.relative_to(ROOT)} (rocprofv3 PMC, {kname} launches)"
+        rows = [e for e in d["kernels"] if e["kernel"] in names and "hbm_bytes_per_launch" in e]
+        if len(rows) == len(names):
+            return (sum(e["hbm_bytes_per_launch"] for e in rows),
+                    f"{f.relative_to(ROOT)} (rocprofv3 PMC: {' + '.join(e['kernel'] for e in rows)})")
         return None, None
     if (Q, S, k) != (1024, 10000, 20) or path != "fused" or not PROFILE_SUMMARY.exists():
         return None, None
@@ -340,6 +384,148 @@ class _stdout_to_stderr:
         os.close(self.saved)
 
 
+def launch_ranks(n: int, argv: list) -> int:
+    """``python bench.py --gpus N`` (N > 1) outside a launcher: start the N ranks -- one process per
+    GPU -- as children through torch.distributed.run (rendezvous on 127.0.0.1), before this process
+    has made any GPU call and without exec; forward their logs to stderr, print rank 0's JSON line,
+    and return non-zero if any rank fails.  The ranks split process_qsos.m:88's spectrum loop."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), str(ROOT / "bench.py"), *argv]
+    print("[bench] launching " + " ".join(cmd), file=sys.stderr, flush=True)
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True)
+    result = None
+    for line in proc.stdout:
+        if line.lstrip().startswith("{") and '"n_gpus"' in line:
+            result = line.strip()
+        else:
+            sys.stderr.write(line)
+            sys.stderr.flush()
+    rc = proc.wait()
+    if rc != 0:
+        print(f"[bench] a rank failed (torch.distributed.run exit status {rc})", file=sys.stderr, flush=True)
+        return rc
+    if result is None:
+        print("[bench] rank 0 printed no JSON line", file=sys.stderr, flush=True)
+        return 1
+    print(result, flush=True)
+    return 0
+
+
+def rank_spectrum_ids(wl: dict, rank: int, world: int, pool_pixels=None) -> np.ndarray:
+    """Ids of this rank's spectra.  configs[1]/[4]: synthetic spectrum seeds rank*Q .. rank*Q+Q-1 (Q per
+    GPU, weak scaling, disjoint); configs[3]: the LPT share of DR12Q positions 0..162,860
+    (dr12q_shard_ids, disjoint); configs[2]: all positions on every rank (one-GPU config)."""
+    if wl["dr12q"]:
+        return dr12q_shard_ids(pool_pixels, wl["spectra"], rank, world, split=wl["scaling"] == "strong")
+    return rank * wl["spectra"] + np.arange(wl["spectra"])
+
+
+def dr12q_pool(model):
+    """The 4096 DR12Q-shaped spectra configs[2]/[3] tile to the full count."""
+    from gp_dla_detection_amd import synthetic as syn
+    return syn.make_dr12q_like_spectra(model, 4096, seed=12, mask_fraction=0.0)
+
+
+def gather(obj, world: int, dist):
+    """Every rank's ``obj`` on every rank (gloo; host-side bookkeeping, not the data path)."""
+    if dist is None or world == 1:
+        return [obj]
+    out = [None] * world
+    dist.all_gather_object(out, obj)
+    return out
+
+
+def plan_only(wl: dict, world: int, rank: int, local_rank: int, dist) -> None:
+    """--plan-only: the multi-rank layout (which spectra each rank evaluates and on which device)
+    through the same launcher and process group as a measured run, without any GPU call."""
+    pool_pixels = None
+    if wl["dr12q"]:
+        from gp_dla_detection_amd import synthetic as syn
+        pool_pixels = [p["wavelengths"].size for p in dr12q_pool(syn.make_model(k=wl["k"]))]
+    ids = rank_spectrum_ids(wl, rank, world, pool_pixels)
+    allr = gather({"rank": rank, "local_rank": local_rank, "device": local_rank, "ids": ids}, world, dist)
+    if rank == 0:
+        cat = np.concatenate([r["ids"] for r in allr])
+        print(json.dumps({
+            "plan_only": True, "n_gpus": world,
+            "world_size": dist.get_world_size() if dist is not None else 1,
+            "workload": wl["label"],
+            "ranks": [{"rank": r["rank"], "local_rank": r["local_rank"], "device": r["device"],
+                       "spectra": int(r["ids"].size), "first_spectrum": int(r["ids"][0]),
+                       "last_spectrum": int(r["ids"][-1])} for r in allr],
+            "disjoint": bool(np.unique(cat).size == cat.size), "total_spectra": int(cat.size)}), flush=True)
+
+
+def configs4_alternative(dev: int, steps: int) -> dict:
+    """BASELINE configs[4] beside the headline: 128 spectra x 10^5 DLA samples, k = 50, on the
+    panel_gemm_i8_24 path, ``steps`` timed steps on resident inputs after one warm-up step; its GEMM
+    roofline (HIP events around the GEMM launches) with the committed PMC traffic of the same
+    kernels, and its deviation from the fp64 panel path (gemm_f64) on the first 8 spectra
+    (log_mvnpdf_low_rank.m:22-32, process_qsos.m:184-198)."""
+    from gp_dla_detection_amd import _lib as L
+    from gp_dla_detection_amd import synthetic as syn
+    from gp_dla_detection_amd.engine import Engine
+    from gp_dla_detection_amd.parameters import set_parameters
+    wl = WORKLOADS["c5"]
+    Q, S, k = wl["spectra"], wl["samples"], wl["k"]
+    model = syn.make_model(k=k)
+    samples = syn.make_samples(S)
+    spectra = [syn.make_spectrum(model, q) for q in range(Q)]
+    packed = syn.pack_spectra(spectra)
+    t = {key: L.DeviceArray.from_numpy(packed[key], device=dev)
+         for key in ("wavelengths", "flux", "noise_variance", "pixel_mask", "z_qsos")}
+    o_null, o_dla = L.DeviceArray(dev, Q, np.float64), L.DeviceArray(dev, Q, np.float64)
+    o_s, o_n = L.DeviceArray(dev, (Q, S), np.float64), L.DeviceArray(dev, Q, np.int32)
+    with Engine(model, samples, set_parameters(k=k), device=dev, path="panel_gemm_i8_24") as eng:
+        def step():
+            eng.process_device(packed["offsets"], t["wavelengths"].ptr, t["flux"].ptr, t["noise_variance"].ptr,
+                               t["pixel_mask"].ptr, t["z_qsos"].ptr, o_null.ptr, o_dla.ptr, o_s.ptr, S,
+                               npix_ptr=o_n.ptr)
+        step()
+        eng.synchronize()
+        eng.reset_stats()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        eng.synchronize()
+        el = time.perf_counter() - t0
+        st = eng.stats()
+    sub = 8
+    with Engine(model, samples, set_parameters(k=k), device=dev, path="panel_gemm") as e64:
+        ref = e64.process(syn.pack_spectra(spectra[:sub]))
+    rel = lambda got, want: float(np.max(np.abs(got - want) / np.maximum(np.abs(want), 1.0)))
+    sll = o_s.numpy(rows=sub)
+    lld, lln = o_dla.numpy(), o_null.numpy()
+    errs = {"sample_log_likelihoods_dla": rel(sll, ref["sample_log_likelihoods_dla"]),
+            "log_likelihoods_dla": rel(lld[:sub], ref["log_likelihoods_dla"]),
+            "log_likelihoods_no_dla": rel(lln[:sub], ref["log_likelihoods_no_dla"])}
+    inv = np.exp(sll - (lld[:sub, None] + np.log(S))).sum(axis=1)
+    n_mean = float(np.mean(o_n.numpy()))
+    path = "panel-GEMM-int8-24"
+    roof = i8_roofline(st, n_mean, k, Q, S, steps, path)
+    traffic, src = profiled_traffic(Q, S, k, path)
+    roof.update({"kernel": ROOFLINE_KERNEL[path], "traffic": traffic, "traffic_source": src})
+    for a in (*t.values(), o_null, o_dla, o_s, o_n):
+        a.free()
+    return {"value": Q * S * steps / el, "unit": "evals/s", "ms_per_step": el / steps * 1e3, "steps": steps,
+            "warmup": 1,
+            "config": {"workload": wl["label"], "spectra": Q, "num_samples": S, "k": k, "n_pixels": n_mean,
+                       "likelihood_path": path},
+            "kernel_ms": {"prep": st["prep_ms"] / max(st["prep_launches"], 1),
+                          "gemm_per_chunk": st["contraction_ms"] / max(st["contraction_launches"], 1),
+                          "batch": st["likelihood_ms"] / max(st["likelihood_launches"], 1),
+                          "reduce": st["reduce_ms"] / max(st["reduce_launches"], 1)},
+            "roofline": roof,
+            "max_rel_err_vs_fp64_panel": errs, "parity_subset": f"first {sub} of {Q} spectra, all {S} samples",
+            "checks_ok": bool(np.all(np.isfinite(sll)) and errs["sample_log_likelihoods_dla"] < 5e-7
+                              and np.max(np.abs(inv - 1)) < 1e-10)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -360,11 +546,19 @@ def main():
     ap.add_argument("--no-alt", action="store_true",
                     help="skip the alternative-path measurement (fused_i8 next to the fp64 line, 1 GPU, c2)")
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU-baseline work (0 = skip)")
+    ap.add_argument("--plan-only", action="store_true",
+                    help="print the rank/spectrum/device layout through the launcher, no GPU call")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # no launcher: start the N ranks as children (nothing has touched the GPU yet)
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks", file=sys.stderr)
+        sys.exit(2)
     dist = None
     if world > 1:
         import torch.distributed as dist
@@ -379,29 +573,35 @@ def main():
                 dist.destroy_process_group()
         return
 
+    wl = dict(WORKLOADS[args.workload])
+    for key in ("spectra", "samples", "k"):
+        if getattr(args, key) is not None:
+            wl[key] = getattr(args, key)
+    if args.plan_only:
+        plan_only(wl, world, rank, local_rank, dist if world > 1 else None)
+        if world > 1:
+            with _stdout_to_stderr():
+                dist.destroy_process_group()
+        return
+
     from gp_dla_detection_amd import _lib as L
     from gp_dla_detection_amd import synthetic as syn
     from gp_dla_detection_amd.engine import Engine
     from gp_dla_detection_amd.parameters import set_parameters
 
-    wl = dict(WORKLOADS[args.workload])
-    for key in ("spectra", "samples", "k"):
-        if getattr(args, key) is not None:
-            wl[key] = getattr(args, key)
     args.k, args.samples = wl["k"], wl["samples"]
     model = syn.make_model(k=args.k)
     samples = syn.make_samples(args.samples)
     if wl["dr12q"]:
         # full DR12Q count (162,861) of DR12Q-shaped spectra (n ~ 270-1250): a pool of 4096
         # distinct synthetic spectra tiled to the count; c3 = all on one GPU, c4 = split over ranks
-        pool = syn.make_dr12q_like_spectra(model, 4096, seed=12, mask_fraction=0.0)
-        mine = dr12q_shard([p["wavelengths"].size for p in pool], wl["spectra"], rank, world,
-                           split=args.workload == "c4")
-        Q = mine.size
-        spectra = [pool[i] for i in mine]
+        pool = dr12q_pool(model)
+        ids = rank_spectrum_ids(wl, rank, world, [p["wavelengths"].size for p in pool])
+        spectra = [pool[i % len(pool)] for i in ids]
     else:
-        Q = wl["spectra"]
-        spectra = [syn.make_spectrum(model, rank * Q + q) for q in range(Q)]
+        ids = rank_spectrum_ids(wl, rank, world)
+        spectra = [syn.make_spectrum(model, int(i)) for i in ids]
+    Q = ids.size
     packed = syn.pack_spectra(spectra)
     # CPU baseline first, while no process has touched the GPU (its workers are spawned)
     cpu = None
@@ -416,6 +616,11 @@ def main():
     o_dla = L.DeviceArray(dev, Q, np.float64)
     o_s = L.DeviceArray(dev, (Q, S), np.float64)
     o_n = L.DeviceArray(dev, Q, np.int32)
+
+    # which physical GPU each rank drives (N distinct devices on an N-GPU node)
+    ranks = gather({"rank": rank, "local_rank": local_rank, "device": dev, "pci_bus_id": L.pci_bus_id(dev),
+                    "spectra": int(Q), "first_spectrum": int(ids[0]), "last_spectrum": int(ids[-1])},
+                   world, dist if world > 1 else None)
 
     if args.path == "auto" and "default_path" in wl:
         args.path = wl["default_path"]
@@ -477,6 +682,8 @@ def main():
                     "32-bit-quantised weights/panel (4 digits, levels <= 3), fp64 everywhere else; "
                     "within the 1e-6 contract, not bitwise-fp64 (DESIGN.md section 4)"}}
         del o_s2, o_null2, o_dla2
+        # BASELINE configs[4] (k = 50, 10^5 samples) on the int8 panel-GEMM path, driver-timed
+        alt["configs4"] = configs4_alternative(dev, args.steps)
 
     # sanity: finite outputs and the calc_cddf.py:246 normalisation invariant
     sll = o_s.numpy(rows=2048)  # the check covers the leading spectra (c3/c4 outputs are 13 GB)
@@ -508,6 +715,9 @@ def main():
         "value": value,
         "unit": "evals/s",
         "n_gpus": world,
+        "world_size": dist.get_world_size() if world > 1 else 1,
+        "ranks": ranks,
+        "distinct_devices": len({r["pci_bus_id"] for r in ranks}),
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
@@ -526,11 +736,7 @@ def main():
         "roofline": {"bound": "mfma", "achieved": achieved_tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved_tf / FP64_PEAK_TFLOPS, "traffic": traffic,
                      "traffic_source": traffic_src,
-                     "kernel": {"fused": f"likelihood_kernel<{args.k}>",
-                                "fused-int8": f"likelihood_i8_kernel<{args.k}>",
-                                "panel-GEMM-int8": "gemm_i8_kernel<4>",
-                                "panel-GEMM-int8-24": "gemm_i8_kernel<3> (Gram) + gemm_i8_kernel<4> (u)",
-                                "panel-GEMM": "gemm_f64_kernel (Gram + u)"}.get(path, path),
+                     "kernel": ROOFLINE_KERNEL.get(path, path).format(k=args.k),
                      "avg_launch_ms": avg_ms,
                      "flops_per_eval": algorithmic_flops_per_eval(n_mean, args.k),
                      "evals_per_launch": evals_per_launch,

@@ -102,7 +102,11 @@ SIGNATURES = {
     "gpdla_last_error": (C.c_char_p, []),
     "gpdla_version": (C.c_int32, []),
     "gpdla_device_count": (C.c_int32, []),
+    "gpdla_device_pci_bus_id": (C.c_int, [C.c_int32, C.c_char_p, C.c_int32]),
 }
+
+# GPDLA_ABI_VERSION of include/gpdla.h this binding is written against
+ABI_VERSION = 3
 
 _lib = None
 
@@ -125,14 +129,27 @@ def load() -> C.CDLL:
             raise ImportError(f"{LIB_PATH} not built; run __graft_entry__.build() "
                               "(there is no CPU fallback for the GP-DLA hot path)")
         lib = C.CDLL(str(LIB_PATH))
+        missing = [name for name in SIGNATURES if getattr(lib, name, None) is None]
+        if missing:
+            raise ImportError(f"{LIB_PATH} lacks {', '.join(missing)}: a stale or foreign build "
+                              "(rebuild with __graft_entry__.build())")
+        lib.gpdla_version.restype = C.c_int32
+        if lib.gpdla_version() != ABI_VERSION:
+            raise ImportError(f"{LIB_PATH} has ABI version {lib.gpdla_version()}, this binding needs "
+                              f"{ABI_VERSION} (rebuild with __graft_entry__.build())")
         for name, (res, args) in SIGNATURES.items():
-            fn = getattr(lib, name, None)
-            if fn is None:   # an older A/B build (GPDLA_LIB); tests/test_library.py pins the in-tree one
-                continue
+            fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
         _lib = lib
     return _lib
+
+
+def pci_bus_id(device: int) -> str:
+    """PCI bus id of a HIP device (which physical GPU a rank drives)."""
+    buf = C.create_string_buffer(64)
+    check(load().gpdla_device_pci_bus_id(device, buf, len(buf)))
+    return buf.value.decode()
 
 
 def check(rc: int) -> int:

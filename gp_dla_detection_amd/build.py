@@ -46,9 +46,10 @@ def build_mex_mocks(verbose: bool = False) -> list[Path]:
     outs = []
     if not cc or not (PKG.parent / "matlab").is_dir():
         return outs
-    for src in sorted((PKG.parent / "matlab").glob("*.c")):
+    for src in sorted((PKG.parent / "matlab").glob("*.c")):   # each includes matlab/mex_widen.h
         out = MEX_API / f"lib{src.stem}_mock.so"
-        deps = [src, MEX_API / "mex_mock.c", MEX_API / "mex.h", PKG.parent / "include" / "gpdla.h"]
+        deps = [src, MEX_API / "mex_mock.c", MEX_API / "mex.h", PKG.parent / "include" / "gpdla.h",
+                PKG.parent / "matlab" / "mex_widen.h"]
         if not (out.exists() and all(out.stat().st_mtime >= d.stat().st_mtime for d in deps)):
             cmd = [cc, "-std=c99", "-O1", "-Wall", "-fPIC", "-shared", f"-I{MEX_API}", f"-I{PKG.parent / 'include'}",
                    str(src), str(MEX_API / "mex_mock.c"), f"-L{PKG}", "-lgpdla",

@@ -237,6 +237,15 @@ int32_t gpdla_device_count(void) {
   return c;
 }
 
+int gpdla_device_pci_bus_id(int32_t device, char* buf, int32_t len) {
+  if (!buf || len < 13) return set_error(GPDLA_EINVAL, "pci bus id buffer needs >= 13 bytes");
+  int c = gpdla_device_count();
+  if (c == 0) return set_error(GPDLA_EDEVICE, "no HIP device");
+  if (device < 0 || device >= c) return set_error(GPDLA_EINVAL, "device %d outside [0, %d)", device, c);
+  HIP_TRY(hipDeviceGetPCIBusId(buf, len, device));
+  return GPDLA_OK;
+}
+
 const char* gpdla_last_error(void) { return g_last_error.c_str(); }
 
 int gpdla_diag_faddeeva_w(double x, double y, double* re, double* im);  // faddeeva_host.cpp
@@ -564,9 +573,13 @@ int gpdla_engine_process(gpdla_engine* e, const gpdla_spectra* sp, const gpdla_r
     for (int64_t bi = 0; bi < nbatch; ++bi)
       max_pix = std::max(max_pix, sp->offsets[std::min(Q, (bi + 1) * QB)] - sp->offsets[bi * QB]);
     int rc;
+    // no copy or kernel of an earlier call (one that returned an error mid-loop included) may still
+    // use a stage that host_stages_prepare is about to free and grow
+    if (e->copy_stream) HIP_TRY(hipStreamSynchronize(e->copy_stream));
+    HIP_TRY(hipStreamSynchronize(st));
     if ((rc = host_stages_prepare(e, max_pix, std::min(Q, QB)))) return rc;
-    // the previous call's copies are done (it synchronised); order this call after any other
-    // work on the engine's stream, then keep the two streams apart except through the events
+    // order this call after any other work on the engine's stream, then keep the two streams apart
+    // except through the events
     HIP_TRY(hipStreamSynchronize(e->copy_stream));
     for (HostStage& h : e->hs) {
       HIP_TRY(hipEventRecord(h.in_free, st));

@@ -362,7 +362,12 @@ def run_process_qsos(base_directory: str, training_release: str, training_set_na
     if isinstance(catalog, LazyMat):
         catalog.close()
     S = np.asarray(samples["nhi_samples"]).size
-    chunk_rows = chunk_rows or auto_chunk_rows(S, 8, tidx.size)
+    if not chunk_rows:
+        chunk_rows = auto_chunk_rows(S, 8, tidx.size)
+        if world > 1:
+            # at least ~4 blocks per rank, so a small Q still spreads over every rank (every rank
+            # derives the same value from Q and world before the file exists)
+            chunk_rows = max(1, min(chunk_rows, -(-tidx.size // (4 * world) // 8) * 8 or 8))
     shards = block_lpt_shards(expected_pixels(z_all), chunk_rows, world)
     mine = shards[rank]
     packed = load_preloaded_qsos_packed(f"{rdir}/preloaded_qsos.mat", tidx[mine])

@@ -43,8 +43,8 @@ extern "C" {
 
 /* ABI version (gpdla_version()).  2: gpdla_stats gained contraction_ms / contraction_launches
  * (its size changed: a caller compiled against a version-1 header must use gpdla_engine_get_stats_n
- * with its own sizeof(gpdla_stats), or be rebuilt). */
-#define GPDLA_ABI_VERSION 2
+ * with its own sizeof(gpdla_stats), or be rebuilt).  3: gpdla_device_pci_bus_id. */
+#define GPDLA_ABI_VERSION 3
 
 #define GPDLA_MEM_HOST 0
 #define GPDLA_MEM_DEVICE 1
@@ -213,6 +213,9 @@ int gpdla_memcpy_dtoh(int32_t device, void* dst, const void* src, int64_t bytes)
 const char* gpdla_last_error(void);
 int32_t gpdla_version(void);
 int32_t gpdla_device_count(void);
+/* PCI bus id ("dddd:bb:dd.f") of a device, into buf (len >= 13): which physical GPU a rank drives
+ * (the multi-GPU bench reports it per rank; process_qsos.m:88's spectra loop split over devices). */
+int gpdla_device_pci_bus_id(int32_t device, char* buf, int32_t len);
 
 #ifdef __cplusplus
 }

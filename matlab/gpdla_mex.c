@@ -20,7 +20,8 @@
  *   [log_likelihoods_no_dla, sample_log_likelihoods_dla, log_likelihoods_dla, min_z_dlas,
  *    max_z_dlas, num_pixels] = gpdla_mex('process', eng, all_wavelengths, all_flux,
  *                                        all_noise_variance, all_pixel_mask, z_qsos)
- *       The preloaded_qsos cells of the selected spectra (process_qsos.m:45-61) and their z_QSO.
+ *       The preloaded_qsos cells of the selected spectra (process_qsos.m:45-61) and their z_QSO,
+ *       double or single (fitsread's class for the speclite columns; widened exactly, mex_widen.h).
  *       Outputs as process_qsos.m:74-82 shapes them: Q x 1 vectors and the Q x S sample matrix
  *       (:195), with NaN where a spectrum has no usable pixel.  A non-positive pivot (MATLAB's chol
  *       would raise, log_mvnpdf_low_rank.m:24) leaves NaN likelihoods and raises 'MATLAB:posdef'
@@ -42,6 +43,7 @@
 
 #include "mex.h"
 #include "gpdla.h"
+#include "mex_widen.h"
 
 enum { kMaxEngines = 64, kBatch = 4096, kTile = 64 };
 static gpdla_engine* g_engines[kMaxEngines];
@@ -60,14 +62,9 @@ static void fail(int rc, const char* what) {
   mexErrMsgIdAndTxt("gpdla:engine", "%s failed (%d): %s", what, rc, gpdla_last_error());
 }
 
-static const double* dbl(const mxArray* a, const char* name, size_t want) {
-  if (!mxIsDouble(a) || mxIsComplex(a)) mexErrMsgIdAndTxt("gpdla:type", "%s must be real double", name);
-  if (want && mxGetNumberOfElements(a) != want)
-    mexErrMsgIdAndTxt("gpdla:size", "%s has %zu elements, expected %zu", name, mxGetNumberOfElements(a), want);
-  return mxGetDoubles(a);
-}
+static const double* dbl(const mxArray* a, const char* name, size_t want) { return widen(a, name, want); }
 
-static double scalar(const mxArray* a, const char* name) { return *dbl(a, name, 1); }
+static double scalar(const mxArray* a, const char* name) { return widen_scalar(a, name); }
 
 static int path_code(const mxArray* a) {
   if (!mxIsChar(a)) return (int)scalar(a, "path");
@@ -183,16 +180,22 @@ static void do_process(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[
   for (size_t q = 0; q < Q; ++q) {
     const size_t a = (size_t)off[q], n = (size_t)(off[q + 1] - off[q]);
     if (!n) continue;
-    memcpy(wl + a, dbl(mxGetCell(prhs[2], q), "wavelengths", n), n * sizeof(double));
-    memcpy(fl + a, dbl(mxGetCell(prhs[3], q), "flux", n), n * sizeof(double));
-    memcpy(nv + a, dbl(mxGetCell(prhs[4], q), "noise_variance", n), n * sizeof(double));
+    widen_into(wl + a, mxGetCell(prhs[2], q), "wavelengths", n);
+    widen_into(fl + a, mxGetCell(prhs[3], q), "flux", n);
+    widen_into(nv + a, mxGetCell(prhs[4], q), "noise_variance", n);
     const mxArray* m = mxGetCell(prhs[5], q);
     if (mxIsLogical(m)) {
       const mxLogical* src = mxGetLogicals(m);
       for (size_t i = 0; i < n; ++i) mk[a + i] = src[i] ? 1 : 0;
     } else {
-      const double* src = dbl(m, "pixel_mask", n);
-      for (size_t i = 0; i < n; ++i) mk[a + i] = src[i] != 0.0;
+      widen_check(m, "pixel_mask", n);
+      if (mxIsDouble(m)) {
+        const double* src = mxGetDoubles(m);
+        for (size_t i = 0; i < n; ++i) mk[a + i] = src[i] != 0.0;
+      } else {
+        const float* src = mxGetSingles(m);
+        for (size_t i = 0; i < n; ++i) mk[a + i] = src[i] != 0.0f;
+      }
     }
   }
   /* outputs in process_qsos.m's shapes (nan(num_quasars, 1), nan(num_quasars, num_dla_samples)) */
@@ -247,6 +250,7 @@ void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
     mexAtExit(destroy_all);
     registered = 1;
   }
+  g_num_widened = 0;   /* copies of a call an error unwound were freed by MATLAB */
   if (nrhs < 1 || !mxIsChar(prhs[0])) mexErrMsgIdAndTxt("gpdla:args", "first argument: 'create', 'process' or 'destroy'");
   char* cmd = mxArrayToString(prhs[0]);
   const int c = !strcmp(cmd, "create") ? 0 : !strcmp(cmd, "process") ? 1 : !strcmp(cmd, "destroy") ? 2 : -1;
@@ -264,4 +268,5 @@ void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
   } else {
     mexErrMsgIdAndTxt("gpdla:args", "unknown command");
   }
+  widen_release();
 }

@@ -11,20 +11,25 @@
 
 #include "mex.h"
 #include "gpdla.h"
+#include "mex_widen.h"
 
 void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
   (void)nlhs;
   if (nrhs != 4) mexErrMsgIdAndTxt("gpdla:mvn", "usage: log_mvnpdf_low_rank(y, mu, M, d)");
-  for (int i = 0; i < 4; ++i)
-    if (!mxIsDouble(prhs[i])) mexErrMsgIdAndTxt("gpdla:mvn", "argument %d must be double", i + 1);
+  g_num_widened = 0;   /* copies of a call an error unwound were freed by MATLAB */
   const int64_t n = (int64_t)mxGetM(prhs[2]);
   const int32_t k = (int32_t)mxGetN(prhs[2]);
   if ((int64_t)mxGetNumberOfElements(prhs[0]) != n || (int64_t)mxGetNumberOfElements(prhs[1]) != n ||
       (int64_t)mxGetNumberOfElements(prhs[3]) != n)
     mexErrMsgIdAndTxt("gpdla:mvn", "y, mu and d must have size(M, 1) elements");
+  /* double or single (e.g. process_qsos.m:196's this_flux from single preloaded cells), widened */
+  const double* y = widen(prhs[0], "y", 0);
+  const double* mu = widen(prhs[1], "mu", 0);
+  const double* M = widen(prhs[2], "M", 0);
+  const double* d = widen(prhs[3], "d", 0);
   double out = 0.0;
-  const int rc = gpdla_log_mvnpdf_low_rank_f64(mxGetDoubles(prhs[0]), mxGetDoubles(prhs[1]),
-                                               mxGetDoubles(prhs[2]), mxGetDoubles(prhs[3]), n, k, &out);
+  const int rc = gpdla_log_mvnpdf_low_rank_f64(y, mu, M, d, n, k, &out);
+  widen_release();
   if (rc == GPDLA_ENUMERIC) mexErrMsgIdAndTxt("MATLAB:posdef", "%s", gpdla_last_error());
   if (rc != GPDLA_OK) mexErrMsgIdAndTxt("gpdla:mvn", "%s", gpdla_last_error());
   plhs[0] = mxCreateDoubleScalar(out);

@@ -10,17 +10,22 @@
 
 #include "mex.h"
 #include "gpdla.h"
+#include "mex_widen.h"
 
 void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
   (void)nlhs;
   if (nrhs < 3 || nrhs > 4) mexErrMsgIdAndTxt("gpdla:voigt", "usage: voigt(lambdas, z, N[, num_lines])");
-  if (!mxIsDouble(prhs[0])) mexErrMsgIdAndTxt("gpdla:voigt", "lambdas must be double");
+  g_num_widened = 0;   /* copies of a call an error unwound were freed by MATLAB */
+  /* a single lambdas (process_qsos.m:171-177 on single preloaded cells) is widened exactly, where
+   * voigt.c:262's mxGetPr would reinterpret its bytes as doubles */
+  const double* lambdas = widen(prhs[0], "lambdas", 0);
   const int64_t n = (int64_t)mxGetNumberOfElements(prhs[0]);
   if (n <= 6) mexErrMsgIdAndTxt("gpdla:voigt", "need more than 6 wavelengths (2 width)");
-  const double z = mxGetScalar(prhs[1]), N = mxGetScalar(prhs[2]);
-  const int32_t num_lines = nrhs > 3 ? (int32_t)mxGetScalar(prhs[3]) : 31;
+  const double z = widen_scalar(prhs[1], "z"), N = widen_scalar(prhs[2], "N");
+  const int32_t num_lines = nrhs > 3 ? (int32_t)widen_scalar(prhs[3], "num_lines") : 31;
   mxArray* out = mxCreateDoubleMatrix((size_t)(n - 6), 1, mxREAL);
-  const int rc = gpdla_voigt_f64(mxGetDoubles(prhs[0]), n, z, N, num_lines, mxGetDoubles(out));
+  const int rc = gpdla_voigt_f64(lambdas, n, z, N, num_lines, mxGetDoubles(out));
+  widen_release();
   if (rc != GPDLA_OK) {
     mxDestroyArray(out);
     mexErrMsgIdAndTxt("gpdla:voigt", "%s", gpdla_last_error());

@@ -22,6 +22,7 @@ mxArray* mxCreateDoubleScalar(double v);
 mxArray* mxCreateNumericMatrix(mwSize m, mwSize n, mxClassID cls, mxComplexity c);
 mxArray* mxCreateUninitNumericMatrix(size_t m, size_t n, mxClassID cls, mxComplexity c);
 double* mxGetDoubles(const mxArray* a);
+float* mxGetSingles(const mxArray* a);
 uint64_t* mxGetUint64s(const mxArray* a);
 int32_t* mxGetInt32s(const mxArray* a);
 mxLogical* mxGetLogicals(const mxArray* a);
@@ -31,6 +32,7 @@ size_t mxGetN(const mxArray* a);
 size_t mxGetNumberOfElements(const mxArray* a);
 bool mxIsCell(const mxArray* a);
 bool mxIsDouble(const mxArray* a);
+bool mxIsSingle(const mxArray* a);
 bool mxIsLogical(const mxArray* a);
 bool mxIsUint64(const mxArray* a);
 bool mxIsChar(const mxArray* a);

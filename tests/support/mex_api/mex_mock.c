@@ -43,6 +43,7 @@ mxArray* mxCreateDoubleScalar(double v) { mxArray* a = make(mxDOUBLE_CLASS, 1, 1
 mxArray* mxCreateNumericMatrix(mwSize m, mwSize n, mxClassID cls, mxComplexity c) { (void)c; return make(cls, m, n); }
 mxArray* mxCreateUninitNumericMatrix(size_t m, size_t n, mxClassID cls, mxComplexity c) { (void)c; return make(cls, m, n); }
 double* mxGetDoubles(const mxArray* a) { return a->cls == mxDOUBLE_CLASS ? (double*)a->data : NULL; }
+float* mxGetSingles(const mxArray* a) { return a->cls == mxSINGLE_CLASS ? (float*)a->data : NULL; }
 uint64_t* mxGetUint64s(const mxArray* a) { return a->cls == mxUINT64_CLASS ? (uint64_t*)a->data : NULL; }
 int32_t* mxGetInt32s(const mxArray* a) { return a->cls == mxINT32_CLASS ? (int32_t*)a->data : NULL; }
 mxLogical* mxGetLogicals(const mxArray* a) { return a->cls == mxLOGICAL_CLASS ? (mxLogical*)a->data : NULL; }
@@ -52,6 +53,7 @@ size_t mxGetN(const mxArray* a) { return a->n; }
 size_t mxGetNumberOfElements(const mxArray* a) { return a->m * a->n; }
 bool mxIsCell(const mxArray* a) { return a->cls == mxCELL_CLASS; }
 bool mxIsDouble(const mxArray* a) { return a->cls == mxDOUBLE_CLASS; }
+bool mxIsSingle(const mxArray* a) { return a->cls == mxSINGLE_CLASS; }
 bool mxIsLogical(const mxArray* a) { return a->cls == mxLOGICAL_CLASS; }
 bool mxIsUint64(const mxArray* a) { return a->cls == mxUINT64_CLASS; }
 bool mxIsChar(const mxArray* a) { return a->cls == mxCHAR_CLASS; }

@@ -51,11 +51,12 @@ def test_profiled_traffic_lookup(bench):
     rows = json.loads(bench.PROFILE_SUMMARY.read_text())["kernels"]
     want = [e["hbm_bytes_per_launch"] for e in rows if e["kernel"].startswith("void gpdla::likelihood_kernel<20")]
     assert t is not None and t > 0 and t == want[0] and bench.PROFILE_SUMMARY.name in src
-    for path, (f, kname) in bench.PROFILE_SUMMARY_C5.items():
+    for path, (f, names) in bench.PROFILE_SUMMARY_C5.items():
         tp, srcp = bench.profiled_traffic(128, 100000, 50, path)
         rows = json.loads(f.read_text())["kernels"]
-        assert tp == sum(e["hbm_bytes_per_launch"] for e in rows if kname in e["kernel"]) and tp > 0
-        assert f.name in srcp
+        # exact names: per-batch kernels whose names contain the GEMM's (convert_gemm_i8_kernel) excluded
+        assert tp == sum(e["hbm_bytes_per_launch"] for e in rows if e["kernel"] in names) and tp > 0
+        assert f.name in srcp and "convert" not in srcp
     # other workloads / paths: no profiled number is claimed
     assert bench.profiled_traffic(128, 100000, 50, "fused") == (None, None)
     assert bench.profiled_traffic(64, 10000, 20, "fused") == (None, None)

@@ -1,6 +1,7 @@
 """bench.py's multi-rank machinery on CPU (gloo, world size 2): the timed region's barriers and
 max-over-ranks reduction (timed_steps) and the configs[3] LPT spectrum split (dr12q_shard)."""
 import importlib.util
+import json
 import os
 import socket
 import time
@@ -71,3 +72,53 @@ def test_dr12q_lpt_shards_cover_and_balance():
         loads = np.array([pixels[s].sum() for s in shards], dtype=np.float64)
         assert loads.max() / loads.mean() < 1.001
     np.testing.assert_array_equal(bench.dr12q_shard(pixels, total, 0, 8, split=False), np.arange(total) % 4096)
+
+
+def _run_bench(*argv, env=None, timeout=240):
+    import subprocess
+    import sys
+    e = dict(os.environ)
+    e.pop("WORLD_SIZE", None)
+    e.update(env or {})
+    return subprocess.run([sys.executable, str(ROOT / "bench.py"), *argv], capture_output=True, text=True,
+                          timeout=timeout, env=e)
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("workload,total", [("c2", 2048), ("c4", 162861)])
+def test_launcher_starts_n_ranks(workload, total):
+    """bench.py --gpus 2 with no launcher starts 2 ranks itself (torch.distributed.run children, gloo),
+    and rank 0's single JSON line reports both ranks, their devices and disjoint spectrum shards."""
+    r = _run_bench("--gpus", "2", "--plan-only", "--workload", workload)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["world_size"] == 2
+    assert [x["rank"] for x in d["ranks"]] == [0, 1]
+    assert {x["device"] for x in d["ranks"]} == {0, 1}
+    assert d["disjoint"] and d["total_spectra"] == total
+    if workload == "c2":
+        assert [x["spectra"] for x in d["ranks"]] == [1024, 1024]
+
+
+def test_launcher_world_mismatch_fails():
+    r = _run_bench("--gpus", "1", "--plan-only", env={"WORLD_SIZE": "2", "RANK": "0"})
+    assert r.returncode == 2 and "WORLD_SIZE=2" in r.stderr
+
+
+def test_host_cores_reports_the_grant():
+    hc = _bench().host_cores()
+    assert 1 <= hc["usable"] <= hc["affinity"] <= hc["nproc"]
+    assert hc["cgroup_quota_cpus"] is None or hc["usable"] <= max(1, hc["cgroup_quota_cpus"])
+
+
+def test_profiled_traffic_matches_exact_kernel_names():
+    """configs[4]'s roofline traffic counts the GEMM launches only (not convert_gemm_i8_kernel)."""
+    bench = _bench()
+    f, names = bench.PROFILE_SUMMARY_C5["panel-GEMM-int8-24"]
+    d = json.loads(f.read_text())
+    want = sum(e["hbm_bytes_per_launch"] for e in d["kernels"] if e["kernel"] in names)
+    got, src = bench.profiled_traffic(128, 100000, 50, "panel-GEMM-int8-24")
+    assert got == want and "convert" not in src
+    assert all(any(e["kernel"] == n for e in d["kernels"]) for n in names)

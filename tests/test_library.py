@@ -26,7 +26,7 @@ def test_library_exports_every_declared_symbol():
     for name in names:
         assert hasattr(lib, name), name
         assert name in L.SIGNATURES, f"{name} missing from the ctypes binding"
-    assert lib.gpdla_version() == 2      # GPDLA_ABI_VERSION: gpdla_stats grew in version 2
+    assert lib.gpdla_version() == L.ABI_VERSION == 3   # 2: gpdla_stats grew; 3: gpdla_device_pci_bus_id
 
 
 def test_faddeeva_host_matches_scipy():
@@ -56,6 +56,8 @@ def test_no_cpu_fallback_without_device():
     out = np.zeros(14)
     rc = lib.gpdla_voigt_f64(L.ptr(lam), 20, 2.0, 1e20, 3, L.ptr(out))
     assert rc == L.GPDLA_EDEVICE
+    with pytest.raises(L.GpdlaError):
+        L.pci_bus_id(0)
     assert b"no HIP device" in lib.gpdla_last_error()
     from gp_dla_detection_amd.engine import log_mvnpdf_low_rank
     with pytest.raises(L.GpdlaError):

@@ -19,7 +19,7 @@ import pytest
 from gp_dla_detection_amd import _lib as L
 
 MOCK = Path(__file__).parent / "support" / "mex_api"
-DOUBLE, LOGICAL, CHAR, CELL, UINT64, INT32 = 6, 3, 4, 1, 15, 12
+DOUBLE, SINGLE, LOGICAL, CHAR, CELL, UINT64, INT32 = 6, 7, 3, 4, 1, 15, 12
 
 
 class Gateway:
@@ -50,7 +50,8 @@ class Gateway:
             elems = (C.c_void_p * max(len(v), 1))(*[self.mx(e) for e in v])
             return lib.mock_cell(len(v), elems)
         a = np.asarray(v)
-        cls = {np.dtype(bool): LOGICAL, np.dtype(np.uint64): UINT64, np.dtype(np.int32): INT32}.get(a.dtype, DOUBLE)
+        cls = {np.dtype(bool): LOGICAL, np.dtype(np.uint64): UINT64, np.dtype(np.int32): INT32,
+               np.dtype(np.float32): SINGLE}.get(a.dtype, DOUBLE)
         if cls == DOUBLE:
             a = a.astype(np.float64)
         m, n = (a.size, 1) if a.ndim <= 1 else a.shape
@@ -186,3 +187,113 @@ def test_objective_gateway_matches_python_binding():
     np.testing.assert_array_equal(g[:, 0], g_ref)
     f2, _ = go(2, x, F.T, lya.T, nv.T)             # cached handle, same data
     assert f2[0, 0] == f_ref
+
+
+# ------------------------------------------------------------------ single-precision inputs
+def test_gateways_accept_single_inputs():
+    """Single arrays pass the gateways' type checks (they are widened, mex_widen.h): without a
+    device the call gets as far as the engine's GPDLA_EDEVICE; other classes are still refused."""
+    if L.load().gpdla_device_count() > 0:
+        pytest.skip("a HIP device is present")
+    from gp_dla_detection_amd import synthetic as syn
+    from gp_dla_detection_amd.parameters import set_parameters
+    lam = np.linspace(3700.0, 3900.0, 406, dtype=np.float32)
+    with pytest.raises(RuntimeError, match="no HIP device"):
+        Gateway("voigt_mex")(1, lam, np.float32(2.1), 1e20)
+    with pytest.raises(RuntimeError, match="must be real double or single"):
+        Gateway("voigt_mex")(1, np.arange(10, dtype=np.int32), 2.1, 1e20)
+    n = 40
+    y = np.ones(n, np.float32)
+    with pytest.raises(RuntimeError, match="no HIP device"):
+        Gateway("log_mvnpdf_low_rank_mex")(1, y, y, np.ones((n, 3), np.float32), y)
+    model = {k: (v.astype(np.float32) if isinstance(v, np.ndarray) else v) for k, v in syn.make_model(k=8).items()}
+    with pytest.raises(RuntimeError, match="no HIP device"):
+        Gateway("gpdla_mex")(1, *_create_args(model, syn.make_samples(8), set_parameters(k=8)))
+
+
+def _m_call_args(text, call):
+    """The argument names of the first ``call(...)`` in MATLAB source (continuations joined)."""
+    import re
+    src = re.sub(r"\.\.\.[^\n]*\n", " ", text)
+    i = src.index(call + "(")
+    depth, j = 0, i + len(call)
+    while True:
+        depth += {"(": 1, ")": -1}.get(src[j], 0)
+        if depth == 0:
+            break
+        j += 1
+    return [a.strip() for a in src[i + len(call) + 1:j].split(",")]
+
+
+def test_process_qsos_gpu_script_matches_the_gateway():
+    """matlab/process_qsos_gpu.m passes gpdla_mex('create') the arguments in the order gpdla_mex.c
+    reads them (the order the GPU tests drive), 'process' the preloaded cells, and saves the 22
+    variables of process_qsos.m:235-249 (process.PROCESSED_VARIABLES)."""
+    import re
+    from gp_dla_detection_amd.process import PROCESSED_VARIABLES
+    root = Path(__file__).resolve().parents[1]
+    script = (root / "matlab" / "process_qsos_gpu.m").read_text()
+    create = _m_call_args(script, "gpdla_mex")
+    assert create == ["'create'", "gpu_device", "rest_wavelengths", "mu", "M", "log_omega", "log_c_0", "log_tau_0",
+                      "log_beta", "offset_samples", "nhi_samples", "num_lines", "width", "pixel_spacing",
+                      "min_lambda", "max_lambda", "lya_wavelength", "lyman_limit", "min_z_cut", "max_z_cut",
+                      "absorption_mode", "likelihood_path"]
+    gateway = (root / "matlab" / "gpdla_mex.c").read_text()
+    doc = gateway[gateway.index("eng = gpdla_mex('create',") + 25:gateway.index("[, absorption_mode [, path]])")]
+    assert ["gpu_device"] + re.findall(r"[A-Za-z_0-9]+", doc)[1:] == create[1:20]
+    proc = script[script.index("gpdla_mex('process'"):]
+    assert _m_call_args(proc, "gpdla_mex") == ["'process'", "eng", "all_wavelengths", "all_flux",
+                                               "all_noise_variance", "all_pixel_mask", "z_qsos"]
+    saved = re.findall(r"'([a-z_0-9]+)'", script[script.index("variables_to_save = {"):script.index("};")])
+    assert tuple(saved) == tuple(PROCESSED_VARIABLES) and len(saved) == 22
+    for v in saved:   # every saved variable is set by the script or by set_parameters / the caller
+        assert re.search(rf"\b{v}\b\s*(=|,|\])", script) or v in (
+            "training_release", "training_set_name", "dla_catalog_name", "release", "test_set_name",
+            "prior_z_qso_increase", "max_z_cut", "num_lines"), v
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("path", ["auto", "panel_gemm_i8_24"])
+def test_engine_gateway_single_cells(path):
+    """process_qsos_gpu.m's engine calls on single cells (the class of the reference's
+    preloaded_qsos.mat cells): bitwise equal to the Python engine on the exactly widened doubles."""
+    from gp_dla_detection_amd import synthetic as syn
+    from gp_dla_detection_amd.engine import Engine
+    from gp_dla_detection_amd.parameters import set_parameters
+    k = 20 if path == "auto" else 12
+    model = syn.make_model(k=k)
+    samples = syn.make_samples(80)
+    spectra = syn.make_dr12q_like_spectra(model, 6, seed=8, mask_fraction=0.05)
+    cells = {key: [np.asarray(s[key], np.float32) for s in spectra] for key in ("wavelengths", "flux", "noise_variance")}
+    widened = [dict(wavelengths=cells["wavelengths"][q].astype(np.float64), flux=cells["flux"][q].astype(np.float64),
+                    noise_variance=cells["noise_variance"][q].astype(np.float64), pixel_mask=s["pixel_mask"],
+                    z_qso=s["z_qso"]) for q, s in enumerate(spectra)]
+    params = set_parameters(k=k)
+    with Engine(model, samples, params, path=path) as eng:
+        ref = eng.process(syn.pack_spectra(widened))
+    g = Gateway("gpdla_mex")
+    (h,) = g(1, *_create_args(model, samples, params, path))
+    outs = g(5, "process", h, cells["wavelengths"], cells["flux"], cells["noise_variance"],
+             [np.asarray(s["pixel_mask"], bool) for s in spectra], np.array([s["z_qso"] for s in spectra]))
+    g(0, "destroy", h)
+    for name, got in zip(("log_likelihoods_no_dla", "sample_log_likelihoods_dla", "log_likelihoods_dla",
+                          "min_z_dlas", "max_z_dlas"), outs):
+        want = np.asarray(ref[name])
+        np.testing.assert_array_equal(got.reshape(want.shape), want, err_msg=name)
+    assert np.all(np.isfinite(outs[2]))
+
+
+@pytest.mark.gpu
+def test_voigt_and_mvn_gateways_single_inputs():
+    from gp_dla_detection_amd import synthetic as syn
+    from gp_dla_detection_amd.engine import log_mvnpdf_low_rank, voigt
+    lam = np.linspace(3700.0, 3900.0, 406).astype(np.float32)
+    (got,) = Gateway("voigt_mex")(1, lam, 2.1, 10 ** 20.5, 3.0)
+    np.testing.assert_array_equal(got[:, 0], voigt(lam.astype(np.float64), 2.1, 10 ** 20.5, 3))
+    rng = np.random.default_rng(5)
+    n, k = 300, 20
+    y, mu, d = (rng.standard_normal(n).astype(np.float32), rng.standard_normal(n).astype(np.float32),
+                rng.uniform(0.1, 0.5, n).astype(np.float32))
+    M = (syn.make_model(k=k)["M"][:n] * 3).astype(np.float32)
+    (got,) = Gateway("log_mvnpdf_low_rank_mex")(1, y, mu, M, d)
+    assert got[0, 0] == log_mvnpdf_low_rank(*(a.astype(np.float64) for a in (y, mu, M, d)))
