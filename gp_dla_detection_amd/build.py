@@ -13,22 +13,48 @@ SOURCES = ["kernels.hip", "kernels_i8.hip", "gemm_path.hip", "gemm_i8.hip", "gem
 OUT = PKG / "libgpdla.so"
 
 
+OBJ_DIR = PKG.parent / "build" / "obj"
+
+
 def build(verbose: bool = False, force: bool = False, out: Path | None = None,
-          defines: dict | None = None) -> Path:
-    """Compile libgpdla.so (or a variant with -D``defines`` into ``out``, for A/B experiments)."""
+          defines: dict | None = None, jobs: int | None = None) -> Path:
+    """Compile libgpdla.so (or a variant with -D``defines`` into ``out``, for A/B experiments).
+
+    Each translation unit is compiled to its own object in parallel (no cross-TU device code: every
+    kernel is launched from the file that defines it), then linked; objects are reused while they
+    are newer than their source and every header."""
+    import hashlib
+    from concurrent.futures import ThreadPoolExecutor
     OUT_ = Path(out) if out else OUT
     srcs = [CSRC / s for s in SOURCES]
-    deps = srcs + list(CSRC.glob("*.h")) + [PKG.parent / "include" / "gpdla.h"]
+    headers = list(CSRC.glob("*.h")) + [PKG.parent / "include" / "gpdla.h"]
+    deps = srcs + headers
     if OUT_.exists() and not force and not defines and all(OUT_.stat().st_mtime >= d.stat().st_mtime for d in deps):
         return OUT_
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-    cmd = [hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-Wno-unused-result", "-o", str(OUT_)] + [f"-D{k}={v}" for k, v in (defines or {}).items()] \
-        + [str(s) for s in srcs]
+    dflags = [f"-D{k}={v}" for k, v in sorted((defines or {}).items())]
+    objdir = OBJ_DIR / (hashlib.sha1(" ".join(dflags).encode()).hexdigest()[:12] if dflags else "head")
+    objdir.mkdir(parents=True, exist_ok=True)
+    hdr_mtime = max(h.stat().st_mtime for h in headers)
+
+    def compile_one(src: Path) -> Path:
+        obj = objdir / (src.name + ".o")
+        if not force and obj.exists() and obj.stat().st_mtime >= max(src.stat().st_mtime, hdr_mtime):
+            return obj
+        cmd = [hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-c", "-Wno-unused-result",
+               *dflags, "-o", str(obj) + ".tmp", str(src)]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        subprocess.run(cmd, check=True, cwd=CSRC)
+        Path(str(obj) + ".tmp").replace(obj)
+        return obj
+
+    with ThreadPoolExecutor(max_workers=jobs or min(len(srcs), os.cpu_count() or 4)) as ex:
+        objs = list(ex.map(compile_one, srcs))
+    tmp = OUT_.with_suffix(".so.tmp")
+    cmd = [hipcc, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", str(tmp), *map(str, objs)]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
-    tmp = OUT_.with_suffix(".so.tmp")
-    cmd[cmd.index("-o") + 1] = str(tmp)
     subprocess.run(cmd, check=True, cwd=CSRC)
     tmp.replace(OUT_)
     return OUT_

@@ -129,9 +129,10 @@ __global__ __launch_bounds__(256) void weights_i8_kernel(WeightsI8Args a) {
   const int L = inf.L;
   const int Ls = ((L + kChunkSteps - 1) / kChunkSteps) * kChunkSteps;
   const int Ls16 = 16 * ((L + 15) / 16);
-  const int Lq16 = 16 * ((Ls16 / 16 + kWeightQuarters - 1) / kWeightQuarters);
+  // quarter h: 16-slot groups h G16 / 4 .. (h + 1) G16 / 4 - 1 (balanced: 13 groups go 3, 3, 3, 4)
+  const int G16 = Ls16 / 16;
   const int h = blockIdx.y;
-  const int t0 = min(h * Lq16, Ls16), t1 = min(t0 + Lq16, Ls16);
+  const int t0 = 16 * (h * G16 / kWeightQuarters), t1 = 16 * ((h + 1) * G16 / kWeightQuarters);
   const double off = (s < a.S) ? a.offsets[s] : 0.5;
   const double N = (s < a.S) ? a.nhi[s] : 0.0;  // null model / idle lanes: absorption exactly 1
   const double zdla = inf.zmin + (inf.zmax - inf.zmin) * off;  // process_qsos.m:163-165
@@ -194,8 +195,10 @@ __global__ __launch_bounds__(256) void weights_i8_kernel(WeightsI8Args a) {
         const double rd = r * dinv;
         q1 = fma(r, rd, q1);
         pm *= d;
-        xg[e] = (uint32_t)__builtin_rint(a2 * dinv * sg) ^ 0x80808080u;
-        xu[e] = (uint32_t)__builtin_rint(fma(ab * rd, su, 0x1p31)) ^ 0x80808080u;
+        // rint to an integer in [0, 2^32) by the 1.5 2^52 shifter: one fma rounds at the units place
+        // and the low mantissa word is the integer (v_rndne + v_cvt_u32 saved, twice per slot)
+        xg[e] = (uint32_t)__double2loint(fma(a2 * dinv, sg, 0x1.8p52)) ^ 0x80808080u;
+        xu[e] = (uint32_t)__double2loint(fma(ab * rd, su, 0x1.8p52 + 0x1p31)) ^ 0x80808080u;
         asm volatile("" : "+v"(xg[e]), "+v"(xu[e]), "+v"(q1), "+v"(pm));  // no sinking across slots
       }
     }
@@ -610,11 +613,7 @@ hipError_t launch_gemm_i8(const GemmI8Args& a0, hipStream_t s) {
   } else {
     a.e_tile0 = 0; a.ny = ng;
     // B-stationary when the spectrum's K steps fit the block's LDS
-#ifdef GPDLA_NO_BST
-    if (false) {
-#else
     if (a0.ks_bound > 0 && a0.ks_bound <= kBstMaxKs && ng >= kBstEX && a0.G32) {
-#endif
       hipLaunchKernelGGL(gemm_i8_bst_kernel, dim3((unsigned)ncu), dim3(64 * kBstWaves), 0, s, a);
     } else {
       hipLaunchKernelGGL(gemm_i8_kernel<3>, grid(a.ny, 3), dim3(256), 0, s, a);

@@ -15,7 +15,6 @@ VARIANTS: dict = {
     "ch50k": {"GPDLA_MAX_CHUNK": 50001},
     "ch25k": {"GPDLA_MAX_CHUNK": 25001},
     "ch16k": {"GPDLA_MAX_CHUNK": 16667},
-    "nobst": {"GPDLA_NO_BST": 1},
     "bst8": {"GPDLA_BST_WAVES": 8},
     "bst_ex2": {"GPDLA_BST_EX": 2},
     "bst_ex8": {"GPDLA_BST_EX": 8},
