@@ -14,9 +14,17 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
+#include <type_traits>
 
 #include "device_common.h"
 #include "internal.h"
+
+#ifndef GPDLA_U_FIRST
+#define GPDLA_U_FIRST 0
+#endif
+#ifndef GPDLA_WEIGHTS_F32
+#define GPDLA_WEIGHTS_F32 1
+#endif
 
 namespace gpdla {
 
@@ -105,33 +113,92 @@ __global__ __launch_bounds__(256) void convert_gemm_i8_kernel(ConvertGemmI8Args 
 }
 
 // --------------------------------------------------------------------------------------------
-// weights: grid (ceil(sc / 64), 4 quarters), 4 waves = 4 segments, lane = sample.  Each wave walks
-// its quarter of the segment (whole 16-slot groups) with the register sliding window, and stores
-// each 16-slot group as 16 bytes per digit plane (K-contiguous rows: the GEMM's A operand).
+// Raw profiles of two padded positions in packed fp32 (the 24-bit path's weights, kF32 below).  x_j
+// stays fp64 (lambda fac_j / (1 + z) - c / (sigma sqrt 2) cancels from ~2.3e4 to the few Doppler
+// units that matter), then the three lines' damping wings (T_j = 1/x_j^2 from one reciprocal, the
+// outer polynomial) and the exp run as v_pk_* fp32 on the pair.  Lanes with some |x_j| < kOuterX
+// (core or inner wing; one wave-level branch per pair) recompute their total in fp64 as
+// raw_profile3 does.  Emulated on configs[4] spectra: the log-likelihood error of the 24-bit path
+// moves from 9.25e-8 to 9.9e-8 against fp64 (fp32 profile, instrument broadening and exp; DESIGN.md
+// section 4.2); its Gram is quantised to 24 bits anyway.
 // --------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void weights_i8_kernel(WeightsI8Args a) {
-  constexpr int kWingLds = 4 * ((3 * kWingStride + 3) / 4);
-  __shared__ __attribute__((aligned(16))) double tables[3 * kCoreTable + kWingLds + 64];
-  const SpecInfo inf = a.info[a.q];
-  if (inf.J == 0) return;  // the LDL kernel writes NaN
-  const int lane = threadIdx.x & 63;
-  const int g = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int sl = blockIdx.x * 64 + lane;
+typedef float f2v __attribute__((ext_vector_type(2)));
+
+__device__ inline double total3_f64(double x0, double x1, double x2, const double* __restrict__ core,
+                                    const double* __restrict__ wing_lds) {
+  const double xs[3] = {x0, x1, x2};
+  double t = 0.0;
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const double ax = fabs(xs[j]);
+    const double T = rcp_nr(fma(xs[j], xs[j], 0x1p-1000));
+    double f = outer_poly(wing_lds + j * kWingStride, T);
+    if (ax < kOuterX) f = wing_poly(wing_lds + j * kWingStride, T);
+    if (ax < kCoreX) f = core_eval(core + j * kCoreTable, ax);
+    t -= f;
+  }
+  return t;
+}
+
+__device__ inline f2v raw_profile3_pair_f32(double lam0, double lam1, const double (&afac)[3], float nl2e,
+                                            const float (&oc)[3][kOuterDeg + 1],
+                                            const double* __restrict__ core,
+                                            const double* __restrict__ wing_lds) {
+  double xd0[3], xd1[3];
+  f2v x[3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    xd0[j] = fma(lam0, afac[j], -kC2);
+    xd1[j] = fma(lam1, afac[j], -kC2);
+    x[j] = (f2v){(float)xd0[j], (float)xd1[j]};
+  }
+  const f2v tiny = (f2v){0x1p-60f, 0x1p-60f};
+  const f2v a0 = x[0] * x[0] + tiny, a1 = x[1] * x[1] + tiny, a2 = x[2] * x[2] + tiny;
+  const f2v p01 = a0 * a1, q = p01 * a2;
+  const f2v R = (f2v){__builtin_amdgcn_rcpf(q.x), __builtin_amdgcn_rcpf(q.y)};
+  const f2v r01 = R * a2;
+  const f2v T[3] = {a1 * r01, a0 * r01, p01 * R};
+  f2v tot = (f2v){0.0f, 0.0f};
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    f2v f = (f2v){oc[j][kOuterDeg], oc[j][kOuterDeg]};
+#pragma unroll
+    for (int n = kOuterDeg - 1; n >= 0; --n) f = f * T[j] + (f2v){oc[j][n], oc[j][n]};
+    tot = tot - T[j] * f;
+  }
+  const float m0 = fminf(fabsf(x[0].x), fminf(fabsf(x[1].x), fabsf(x[2].x)));
+  const float m1 = fminf(fabsf(x[0].y), fminf(fabsf(x[1].y), fabsf(x[2].y)));
+  const bool n0 = m0 < (float)kOuterX, n1 = m1 < (float)kOuterX;
+  if (n0 || n1) {  // rare: a line's core or inner wing -- the whole total in fp64
+    if (n0) tot.x = (float)total3_f64(xd0[0], xd0[1], xd0[2], core, wing_lds);
+    if (n1) tot.y = (float)total3_f64(xd1[0], xd1[1], xd1[2], core, wing_lds);
+  }
+  const f2v v = tot * (f2v){nl2e, nl2e};  // N tot log2(e) <= 0
+  return (f2v){__builtin_amdgcn_exp2f(v.x), __builtin_amdgcn_exp2f(v.y)};
+}
+
+// --------------------------------------------------------------------------------------------
+// weights: one task = 64 consecutive samples (lane = sample) x one segment g x one quarter h of the
+// segment's slots.  The wave walks its quarter (whole 16-slot groups) with the register sliding
+// window, and stores each 16-slot group as 16 bytes per digit plane (K-contiguous rows: the GEMM's
+// A operand).  core / wing_lds / exp_lds: the line cores, wing polynomials and 2^(j/64) table in LDS.
+// kF32 (the 24-bit path, nd = 3): raw profiles and the 7-tap broadening in fp32 (pairs of positions
+// in packed fp32, raw_profile3_pair_f32); everything from the broadened absorption on in fp64.
+// --------------------------------------------------------------------------------------------
+template <bool kF32>
+__device__ inline void weights_i8_task(const WeightsI8Args& a, const SpecInfo& inf, int blk, int g, int h,
+                                       int lane, const double* __restrict__ core,
+                                       const double* __restrict__ wing_lds, const double* __restrict__ exp_lds) {
+  using W = typename std::conditional<kF32, float, double>::type;
+  constexpr int kB = kF32 ? 2 : kWB;              // raw profiles per batch
+  const int sl = blk * 64 + lane;
   const bool active = sl < a.sc;
   const int64_t s = a.s0 + sl;
-  double* core_lds = tables;
-  double* wing_lds = tables + 3 * kCoreTable;
-  double* exp_lds = wing_lds + kWingLds;
-  for (int i = threadIdx.x; i < 3 * kCoreTable; i += 256) core_lds[i] = a.lines.buf[i];
-  if (threadIdx.x < 64) exp_lds[threadIdx.x] = a.lines.buf[kLineBufExp2 + threadIdx.x];
-  if (threadIdx.x < 3 * kWingStride) wing_lds[threadIdx.x] = a.lines.buf[kLineBufWing + threadIdx.x];
-  __syncthreads();
   const int L = inf.L;
   const int Ls = ((L + kChunkSteps - 1) / kChunkSteps) * kChunkSteps;
   const int Ls16 = 16 * ((L + 15) / 16);
   // quarter h: 16-slot groups h G16 / 4 .. (h + 1) G16 / 4 - 1 (balanced: 13 groups go 3, 3, 3, 4)
   const int G16 = Ls16 / 16;
-  const int h = blockIdx.y;
   const int t0 = 16 * (h * G16 / kWeightQuarters), t1 = 16 * ((h + 1) * G16 / kWeightQuarters);
   const double off = (s < a.S) ? a.offsets[s] : 0.5;
   const double N = (s < a.S) ? a.nhi[s] : 0.0;  // null model / idle lanes: absorption exactly 1
@@ -140,10 +207,28 @@ __global__ __launch_bounds__(256) void weights_i8_kernel(WeightsI8Args a) {
   double afac[3];
 #pragma unroll
   for (int j = 0; j < 3; ++j) afac[j] = a.lines.buf[kLineBufFac + j] * zfac;
-  auto raw = [&](double lam) { return raw_profile3_t3(lam, afac, N, core_lds, wing_lds, exp_lds); };
+  float oc[3][kOuterDeg + 1];
+  const float nl2e = (float)(N * 1.4426950408889634);
+  if constexpr (kF32) {
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+#pragma unroll
+      for (int n = 0; n <= kOuterDeg; ++n) oc[j][n] = (float)wing_lds[j * kWingStride + kOuterOff + n];
+  }
   const double* lamp = a.lam_pad + (int64_t)g * L + t0;  // padded positions g L + t0 + 0..5
-  double w0 = raw(lamp[0]), w1 = raw(lamp[1]), w2 = raw(lamp[2]);
-  double w3 = raw(lamp[3]), w4 = raw(lamp[4]), w5 = raw(lamp[5]);
+  W w0, w1, w2, w3, w4, w5;
+  if constexpr (kF32) {
+    f2v p = raw_profile3_pair_f32(lamp[0], lamp[1], afac, nl2e, oc, core, wing_lds);
+    w0 = p.x; w1 = p.y;
+    p = raw_profile3_pair_f32(lamp[2], lamp[3], afac, nl2e, oc, core, wing_lds);
+    w2 = p.x; w3 = p.y;
+    p = raw_profile3_pair_f32(lamp[4], lamp[5], afac, nl2e, oc, core, wing_lds);
+    w4 = p.x; w5 = p.y;
+  } else {
+    auto raw = [&](double lam) { return raw_profile3_t3(lam, afac, N, core, wing_lds, exp_lds); };
+    w0 = raw(lamp[0]); w1 = raw(lamp[1]); w2 = raw(lamp[2]);
+    w3 = raw(lamp[3]); w4 = raw(lamp[4]); w5 = raw(lamp[5]);
+  }
   double q1 = 0.0, pm = 1.0;
   int pe = 0;
   // A layout (tile-major, like B): [type 2][sample tile 128][K step][plane 4][group 4][sample 128][16 B];
@@ -156,38 +241,46 @@ __global__ __launch_bounds__(256) void weights_i8_kernel(WeightsI8Args a) {
   // byte offset of 16-slot group G (= K index / 16), plane i
   auto goff = [&](int G, int i) { return ((int64_t)((G >> 2) * 4 + i) * 4 + (G & 3)) * 2048; };
   for (int tg = t0; tg < t1; tg += 16) {
-    // 16 slots' quantised weights collected for the digit planes, the raw profiles 4 slots at a time
-    // (raw_profile3_batch: one fix-up branch per 4 slots; a block's 64 samples are consecutive in z)
+    // 16 slots' quantised weights collected for the digit planes, the raw profiles kB slots at a time
+    // (one fix-up branch per batch; a task's 64 samples are consecutive in z)
     uint32_t xg[16], xu[16];
 #pragma unroll
-    for (int qb = 0; qb < 16 / kWB; ++qb) {
+    for (int qb = 0; qb < 16 / kB; ++qb) {
       // neutral past the segment (quantisation scales as prep_kernel computes them for y = mu = om2 = 0,
       // noise = 1: u_bound = 1)
-      double lam[kWB], w6v[kWB];
+      double lam[kB];
+      W w6v[kB];
 #pragma unroll
-      for (int b = 0; b < kWB; ++b) {
-        const int t = tg + kWB * qb + b;
+      for (int b = 0; b < kB; ++b) {
+        const int t = tg + kB * qb + b;
         lam[b] = t < L ? a.srow[((int64_t)g * Ls + t) * 8] : a.lam_pad[(int64_t)g * L + t + 2 * kWidth];
       }
-      raw_profile3_batch<kWB>(lam, afac, N, core_lds, wing_lds, exp_lds, w6v);
+      if constexpr (kF32) {
+        const f2v p = raw_profile3_pair_f32(lam[0], lam[1], afac, nl2e, oc, core, wing_lds);
+        w6v[0] = p.x;
+        w6v[1] = p.y;
+      } else {
+        raw_profile3_batch<kB>(lam, afac, N, core, wing_lds, exp_lds, w6v);
+      }
 #pragma unroll
-      for (int b = 0; b < kWB; ++b) {
-        const int e = kWB * qb + b;
+      for (int b = 0; b < kB; ++b) {
+        const int e = kB * qb + b;
         const int t = tg + e;
         double y = 0.0, noise = 1.0, mu = 0.0, om2 = 0.0, su = kI8ScaleU, sg = kI8ScaleG;
         if (t < L) {
           const double* sr = a.srow + ((int64_t)g * Ls + t) * 8;
           y = sr[1]; noise = sr[2]; mu = sr[3]; om2 = sr[4]; su = sr[6]; sg = sr[7];
         }
-        const double w6 = w6v[b];
-        double ab = w0 * kInstrumentProfile[0];  // voigt.c:297-299
-        ab = fma(w1, kInstrumentProfile[1], ab);
-        ab = fma(w2, kInstrumentProfile[2], ab);
-        ab = fma(w3, kInstrumentProfile[3], ab);
-        ab = fma(w4, kInstrumentProfile[4], ab);
-        ab = fma(w5, kInstrumentProfile[5], ab);
-        ab = fma(w6, kInstrumentProfile[6], ab);
+        const W w6 = w6v[b];
+        W abw = w0 * (W)kInstrumentProfile[0];  // voigt.c:297-299
+        abw = fma(w1, (W)kInstrumentProfile[1], abw);
+        abw = fma(w2, (W)kInstrumentProfile[2], abw);
+        abw = fma(w3, (W)kInstrumentProfile[3], abw);
+        abw = fma(w4, (W)kInstrumentProfile[4], abw);
+        abw = fma(w5, (W)kInstrumentProfile[5], abw);
+        abw = fma(w6, (W)kInstrumentProfile[6], abw);
         w0 = w1; w1 = w2; w2 = w3; w3 = w4; w4 = w5; w5 = w6;
+        const double ab = (double)abw;
         const double r = fma(-mu, ab, y);  // process_qsos.m:191-197, log_mvnpdf_low_rank.m:11-15
         const double a2 = ab * ab;
         const double d = fma(om2, a2, noise);
@@ -220,6 +313,25 @@ __global__ __launch_bounds__(256) void weights_i8_kernel(WeightsI8Args a) {
     a.q1p[(int64_t)sl * kWeightParts + g * kWeightQuarters + h] = q1;
     a.ldp[(int64_t)sl * kWeightParts + g * kWeightQuarters + h] = log(pm) + pe * kLn2;
   }
+}
+
+constexpr int kWingLds = 4 * ((3 * kWingStride + 3) / 4);
+
+// grid (ceil(sc / 64), 4 quarters), 4 waves = the 4 segments of one task column
+template <bool kF32>
+__global__ __launch_bounds__(256) void weights_i8_kernel(WeightsI8Args a) {
+  __shared__ __attribute__((aligned(16))) double tables[3 * kCoreTable + kWingLds + 64];
+  const SpecInfo inf = a.info[a.q];
+  if (inf.J == 0) return;  // the LDL kernel writes NaN
+  double* core_lds = tables;
+  double* wing_lds = tables + 3 * kCoreTable;
+  double* exp_lds = wing_lds + kWingLds;
+  for (int i = threadIdx.x; i < 3 * kCoreTable; i += 256) core_lds[i] = a.lines.buf[i];
+  if (threadIdx.x < 64) exp_lds[threadIdx.x] = a.lines.buf[kLineBufExp2 + threadIdx.x];
+  if (threadIdx.x < 3 * kWingStride) wing_lds[threadIdx.x] = a.lines.buf[kLineBufWing + threadIdx.x];
+  __syncthreads();
+  weights_i8_task<kF32>(a, inf, blockIdx.x, __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), blockIdx.y,
+                        threadIdx.x & 63, core_lds, wing_lds, exp_lds);
 }
 
 constexpr int kGTileS = 128, kGTileE = 64;
@@ -434,7 +546,6 @@ __global__ __launch_bounds__(256, ND == 3 ? 3 : 2) void gemm_i8_kernel(GemmI8Arg
 #define GPDLA_BST_WAVES 12
 #endif
 constexpr int kBstWaves = GPDLA_BST_WAVES;
-constexpr int kBstTiles = kBstWaves / 4;         // 128-sample tiles per block round
 constexpr int kBstMaxKs = 13;                    // 13 x 12 KiB = 156 KiB of LDS: spectra up to 832 slots
 #ifndef GPDLA_BST_EX
 #define GPDLA_BST_EX 2
@@ -445,6 +556,7 @@ __global__ __launch_bounds__(64 * kBstWaves, 1) __attribute__((amdgpu_waves_per_
 void gemm_i8_bst_kernel(GemmI8Args a) {
   constexpr int ND = 3;
   constexpr int kStepBytes = ND * kGTileE * 64;  // 12 KiB: one K step of one entry tile, 3 planes
+  constexpr int kTiles = kBstWaves / 4;          // 128-sample tiles per block round
   __shared__ __attribute__((aligned(16))) uint8_t Bs[kBstMaxKs * kStepBytes];
   const SpecInfo inf = a.info[a.q];
   if (inf.J == 0) return;
@@ -539,8 +651,8 @@ void gemm_i8_bst_kernel(GemmI8Args a) {
       }
     }
   };
-  const int span = kBstTiles * G;                // sample tiles per round of the XCD's blocks
-  for (int r0 = s0 + kBstTiles * gi; r0 < s1; r0 += span) {
+  const int span = kTiles * G;                   // sample tiles per round of the XCD's blocks
+  for (int r0 = s0 + kTiles * gi; r0 < s1; r0 += span) {
     const int st = r0 + (wave_s >> 2);           // this wave's sample tile
     if (st >= s1) break;                         // wave-uniform (the round's last tiles)
     const uint8_t* At = a.adig + (int64_t)st * nksmax * 16 * 2048;
@@ -585,13 +697,18 @@ hipError_t launch_convert_gemm_i8(const ConvertGemmI8Args& a, int32_t q_count, h
 }
 
 hipError_t launch_weights_i8(const WeightsI8Args& a, hipStream_t s) {
-  hipLaunchKernelGGL(weights_i8_kernel, dim3((unsigned)((a.sc + 63) / 64), kWeightQuarters), dim3(256), 0, s, a);
+  // the 24-bit path (3 Gram digit planes) takes the fp32 raw profiles
+  const dim3 grid((unsigned)((a.sc + 63) / 64), kWeightQuarters);
+  if (a.nd == 3 && GPDLA_WEIGHTS_F32)
+    hipLaunchKernelGGL(weights_i8_kernel<true>, grid, dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL(weights_i8_kernel<false>, grid, dim3(256), 0, s, a);
   return hipGetLastError();
 }
 
 // nd = 4: one launch over all entry tiles.  nd = 3: the Gram tiles on the 3-digit kernel, then the u
 // tiles on the 4-digit one (the u contraction carries most of the 24-bit scheme's error: emulated
-// 2.1e-7 with 3 u digits, 7e-8 with 4, tests/support/emulate_i8.py; the u tiles are 1 of 21 at k = 50)
+// 2.1e-7 with 3 u digits, 7e-8 with 4, tests/support/emulate_i8.py; the u tiles are 1 of 21 at k = 50).
 hipError_t launch_gemm_i8(const GemmI8Args& a0, hipStream_t s) {
   if (a0.k < 1 || a0.k > kGemmMaxK || a0.rows % kGTileS != 0 || a0.rows < a0.sc || a0.kstride % 64 != 0 ||
       (a0.nd != 3 && a0.nd != 4))
@@ -611,6 +728,9 @@ hipError_t launch_gemm_i8(const GemmI8Args& a0, hipStream_t s) {
     a.e_tile0 = 0; a.ny = ng + nu;
     hipLaunchKernelGGL(gemm_i8_kernel<4>, grid(a.ny, 2), dim3(256), 0, s, a);
   } else {
+    GemmI8Args au = a0;
+    au.e_tile0 = ng; au.ny = nu;
+    if (GPDLA_U_FIRST) hipLaunchKernelGGL(gemm_i8_kernel<4>, grid(au.ny, 2), dim3(256), 0, s, au);
     a.e_tile0 = 0; a.ny = ng;
     // B-stationary when the spectrum's K steps fit the block's LDS
     if (a0.ks_bound > 0 && a0.ks_bound <= kBstMaxKs && ng >= kBstEX && a0.G32) {
@@ -618,8 +738,7 @@ hipError_t launch_gemm_i8(const GemmI8Args& a0, hipStream_t s) {
     } else {
       hipLaunchKernelGGL(gemm_i8_kernel<3>, grid(a.ny, 3), dim3(256), 0, s, a);
     }
-    a.e_tile0 = ng; a.ny = nu;
-    hipLaunchKernelGGL(gemm_i8_kernel<4>, grid(a.ny, 2), dim3(256), 0, s, a);
+    if (!GPDLA_U_FIRST) hipLaunchKernelGGL(gemm_i8_kernel<4>, grid(au.ny, 2), dim3(256), 0, s, au);
   }
   return hipGetLastError();
 }

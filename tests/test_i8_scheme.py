@@ -63,3 +63,21 @@ def test_level3_truncation_bound_and_int32_level_sums():
     kept = sum((2 ** (8 * (6 - i - j))) * int(np.dot(dA[i].astype(object), dB[j].astype(object)))
                for i in range(4) for j in range(4) if i + j <= 3)
     assert abs(full - kept) <= n * bound_per_slot
+
+
+def test_fp32_raw_profile_adds_little_to_the_24_bit_scheme():
+    """The 24-bit panel path evaluates its weights' raw Voigt profiles in packed fp32 (gemm_i8.hip
+    raw_profile3_pair_f32; x_j stays fp64).  Emulated on configs[4]-shaped spectra (k = 50, 10^5
+    samples): against the fp64 oracle the fp32 profiles add less than 5e-8 to the scheme's own
+    log-likelihood error, which stays under 2e-7 (the GPU tests' bar is 5e-7)."""
+    from gp_dla_detection_amd import synthetic as syn
+    from support.emulate_f32_profile import worst_errors
+    model = syn.make_model(k=50)
+    samples = syn.make_samples(100000)
+    rng = np.random.default_rng(3)
+    spectra = [syn.make_spectrum(model, q) for q in range(2)]
+    picks = [(q, int(s)) for q in range(2) for s in rng.choice(100000, 6, replace=False)]
+    w = worst_errors(model, spectra, samples, picks)
+    assert w["f64"] < 2e-7
+    assert w["f32"] - w["f64"] < 5e-8
+    assert w["f32"] < 2e-7
