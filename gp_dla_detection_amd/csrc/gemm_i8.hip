@@ -19,13 +19,6 @@
 #include "device_common.h"
 #include "internal.h"
 
-#ifndef GPDLA_U_FIRST
-#define GPDLA_U_FIRST 0
-#endif
-#ifndef GPDLA_WEIGHTS_F32
-#define GPDLA_WEIGHTS_F32 1
-#endif
-
 namespace gpdla {
 
 namespace {
@@ -213,7 +206,9 @@ __device__ inline void weights_i8_task(const WeightsI8Args& a, const SpecInfo& i
 #pragma unroll
     for (int j = 0; j < 3; ++j)
 #pragma unroll
-      for (int n = 0; n <= kOuterDeg; ++n) oc[j][n] = (float)wing_lds[j * kWingStride + kOuterOff + n];
+      for (int n = 0; n <= kOuterDeg; ++n)  // wave-uniform: kept in SGPRs
+        oc[j][n] = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(
+                       __builtin_bit_cast(int, (float)wing_lds[j * kWingStride + kOuterOff + n])));
   }
   const double* lamp = a.lam_pad + (int64_t)g * L + t0;  // padded positions g L + t0 + 0..5
   W w0, w1, w2, w3, w4, w5;
@@ -699,7 +694,7 @@ hipError_t launch_convert_gemm_i8(const ConvertGemmI8Args& a, int32_t q_count, h
 hipError_t launch_weights_i8(const WeightsI8Args& a, hipStream_t s) {
   // the 24-bit path (3 Gram digit planes) takes the fp32 raw profiles
   const dim3 grid((unsigned)((a.sc + 63) / 64), kWeightQuarters);
-  if (a.nd == 3 && GPDLA_WEIGHTS_F32)
+  if (a.nd == 3)
     hipLaunchKernelGGL(weights_i8_kernel<true>, grid, dim3(256), 0, s, a);
   else
     hipLaunchKernelGGL(weights_i8_kernel<false>, grid, dim3(256), 0, s, a);
@@ -728,9 +723,6 @@ hipError_t launch_gemm_i8(const GemmI8Args& a0, hipStream_t s) {
     a.e_tile0 = 0; a.ny = ng + nu;
     hipLaunchKernelGGL(gemm_i8_kernel<4>, grid(a.ny, 2), dim3(256), 0, s, a);
   } else {
-    GemmI8Args au = a0;
-    au.e_tile0 = ng; au.ny = nu;
-    if (GPDLA_U_FIRST) hipLaunchKernelGGL(gemm_i8_kernel<4>, grid(au.ny, 2), dim3(256), 0, s, au);
     a.e_tile0 = 0; a.ny = ng;
     // B-stationary when the spectrum's K steps fit the block's LDS
     if (a0.ks_bound > 0 && a0.ks_bound <= kBstMaxKs && ng >= kBstEX && a0.G32) {
@@ -738,7 +730,8 @@ hipError_t launch_gemm_i8(const GemmI8Args& a0, hipStream_t s) {
     } else {
       hipLaunchKernelGGL(gemm_i8_kernel<3>, grid(a.ny, 3), dim3(256), 0, s, a);
     }
-    if (!GPDLA_U_FIRST) hipLaunchKernelGGL(gemm_i8_kernel<4>, grid(au.ny, 2), dim3(256), 0, s, au);
+    a.e_tile0 = ng; a.ny = nu;
+    hipLaunchKernelGGL(gemm_i8_kernel<4>, grid(a.ny, 2), dim3(256), 0, s, a);
   }
   return hipGetLastError();
 }

@@ -16,8 +16,6 @@ VARIANTS: dict = {
     "ch25k": {"GPDLA_MAX_CHUNK": 25001},
     "ch16k": {"GPDLA_MAX_CHUNK": 16667},
     "bst8": {"GPDLA_BST_WAVES": 8},
-    "wf64": {"GPDLA_WEIGHTS_F32": 0},
-    "ufirst": {"GPDLA_U_FIRST": 1},
     "bst_ex2": {"GPDLA_BST_EX": 2},
     "bst_ex8": {"GPDLA_BST_EX": 8},
 }
