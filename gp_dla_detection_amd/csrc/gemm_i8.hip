@@ -545,9 +545,6 @@ constexpr int kBstMaxKs = 13;                    // 13 x 12 KiB = 156 KiB of LDS
 #ifndef GPDLA_BST_EX
 #define GPDLA_BST_EX 2
 #endif
-#ifndef GPDLA_BST_DEPTH
-#define GPDLA_BST_DEPTH 1
-#endif
 constexpr int kBstEX = GPDLA_BST_EX;
 
 __global__ __launch_bounds__(64 * kBstWaves, 1) __attribute__((amdgpu_waves_per_eu(kBstWaves / 4, kBstWaves / 4)))
@@ -658,33 +655,6 @@ void gemm_i8_bst_kernel(GemmI8Args a) {
     // two A register sets in turn, the loop unrolled by two (no copies); each step's loads are waited
     // for after the previous step's MFMAs and handed over through an empty "+v" asm, so the
     // compiler's waitcnt pass never drains the prefetch in flight (as gemm_i8_kernel's land())
-#if GPDLA_BST_DEPTH == 2
-    // three A register sets, two K steps in flight: a step's 6 loads are waited for with the next
-    // step's 6 still outstanding (vector loads return in order), vmcnt(0) only at the tile's end
-    v4i Ar3[3][2][ND];
-    auto hand = [&](v4i (&Ar)[2][ND], bool more) {
-      if (more) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-      for (int rt = 0; rt < 2; ++rt)
-#pragma unroll
-        for (int p = 0; p < ND; ++p) asm volatile("" : "+v"(Ar[rt][p]));
-    };
-    load_a(At, 0, Ar3[0]);
-    if (nks > 1) load_a(At, 1, Ar3[1]);
-    for (int ks = 0; ks < nks; ks += 3) {
-#pragma unroll
-      for (int u = 0; u < 3; ++u) {
-        if (ks + u < nks) {
-          hand(Ar3[u], ks + u + 1 < nks);
-          if (ks + u + 2 < nks) load_a(At, ks + u + 2, Ar3[(u + 2) % 3]);
-          __builtin_amdgcn_sched_barrier(0);
-          compute(Ar3[u], ks + u);
-          __builtin_amdgcn_sched_barrier(0);
-        }
-      }
-    }
-#else
     v4i A0r[2][ND], A1r[2][ND];
     auto land = [&](v4i (&Ar)[2][ND]) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -706,7 +676,6 @@ void gemm_i8_bst_kernel(GemmI8Args a) {
       if (m1) compute(A1r, ks + 1);
       land(A0r);
     }
-#endif
     epilogue(st * kGTileS);
   }
 }

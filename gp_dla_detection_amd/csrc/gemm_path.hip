@@ -157,6 +157,14 @@ template <typename GT> __device__ inline const GT* gram_of(const LdlArgs& a);
 template <> __device__ inline const double* gram_of<double>(const LdlArgs& a) { return a.G; }
 template <> __device__ inline const float* gram_of<float>(const LdlArgs& a) { return a.G32; }
 
+// 1 / D_p for the pivots: v_rcp_f64 and two Newton steps (within an ulp) for the fp64 Gram, one step
+// (~2^-50) for the fp32 Gram of the 24-bit path, whose entries carry 2^-24 already
+template <typename GT>
+__device__ inline double pivot_rcp(double d) {
+  if constexpr (std::is_same<GT, float>::value) return rcp_sweep(d);
+  else return rcp_nr(d);
+}
+
 template <int NT, typename GT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT <= 13 ? 2 : 1))) void ldl_mfma_kernel(LdlArgs a) {
   constexpr int NTT = NT * (NT + 1) / 2;
@@ -258,7 +266,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT <= 13 ? 
     return dj < w ? (double)g + done : (dj == w ? (di < w ? u : q1) : done);
   };
   double T[NTT];
-  double inv_p[NT];  // this lane's element of S_PP^-1 per finished block row P
+  double inv_p[NT];  // this lane's element of -S_PP^-1 per finished block row P (negated once, not per MFMA)
   double pb = 1.0;  // prod_{p<k} D_p = pb 2^eb
   int eb = 0;
   double quad = 0.0;
@@ -274,7 +282,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT <= 13 ? 
 #pragma unroll
     for (int P = 0; P < J; ++P) {
       const int pp = P * NT - P * (P - 1) / 2;
-      const double x = -__builtin_amdgcn_mfma_f64_4x4x4f64(inv_p[P], T[pp + (J - P)], 0.0, 0, 0, 0);
+      const double x = __builtin_amdgcn_mfma_f64_4x4x4f64(inv_p[P], T[pp + (J - P)], 0.0, 0, 0, 0);
 #pragma unroll
       for (int I = J; I < NT; ++I) {
         double& t = T[jj + (I - J)];
@@ -293,22 +301,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT <= 13 ? 
     double a00 = m[0], a01 = m[1], a02 = m[2], a03 = m[3];
     double a11 = m[5], a12 = m[6], a13 = m[7];
     double a22 = m[10], a23 = m[11], a33 = m[15];
-    const double D0 = a00, i0 = rcp_nr(D0);
+    const double D0 = a00, i0 = pivot_rcp<GT>(D0);
     const double l10 = a01 * i0, l20 = a02 * i0, l30 = a03 * i0;
     a11 = fma(-l10, a01, a11); a12 = fma(-l10, a02, a12); a13 = fma(-l10, a03, a13);
     a22 = fma(-l20, a02, a22); a23 = fma(-l20, a03, a23); a33 = fma(-l30, a03, a33);
-    const double D1 = a11, i1 = rcp_nr(D1);
+    const double D1 = a11, i1 = pivot_rcp<GT>(D1);
     const double l21 = a12 * i1, l31 = a13 * i1;
     a22 = fma(-l21, a12, a22); a23 = fma(-l21, a13, a23); a33 = fma(-l31, a13, a33);
-    const double D2 = a22, i2 = rcp_nr(D2);
+    const double D2 = a22, i2 = pivot_rcp<GT>(D2);
     const double l32 = a23 * i2;
     a33 = fma(-l32, a23, a33);
-    const double D3 = a33, i3 = rcp_nr(D3);
+    const double D3 = a33, i3 = pivot_rcp<GT>(D3);
     const double Dp[4] = {D0, D1, D2, D3};
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       const int p = 4 * J + t;
-      if (p < K) {
+      if (J < NT - 1 || p < K) {  // every row of a whole tile row is a Gram row (4 (NT - 1) <= k)
         bad |= !(Dp[t] > 0.0) || !(Dp[t] < INFINITY);
         pb *= Dp[t];
       } else if (p == K) {
@@ -328,7 +336,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT <= 13 ? 
                  y3 = fma(-l32, y2, fma(-l31, y1, fma(-l30, y0, e3)));
     const double x3 = y3 * i3, x2 = fma(-l32, x3, y2 * i2), x1 = fma(-l31, x3, fma(-l21, x2, y1 * i1)),
                  x0 = fma(-l30, x3, fma(-l20, x2, fma(-l10, x1, y0 * i0)));
-    inv_p[J] = tj == 0 ? x0 : (tj == 1 ? x1 : (tj == 2 ? x2 : x3));
+    inv_p[J] = -(tj == 0 ? x0 : (tj == 1 ? x1 : (tj == 2 ? x2 : x3)));
   }
   const double logdet_b = log(pb) + eb * kLn2;
   double ll = -0.5 * (quad + (logdet_d + logdet_b) + inf.n * kLog2Pi);  // log_mvnpdf_low_rank.m:30-32

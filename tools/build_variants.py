@@ -16,8 +16,6 @@ VARIANTS: dict = {
     "ch25k": {"GPDLA_MAX_CHUNK": 25001},
     "ch16k": {"GPDLA_MAX_CHUNK": 16667},
     "bst8": {"GPDLA_BST_WAVES": 8},
-    "bst8p2": {"GPDLA_BST_WAVES": 8, "GPDLA_BST_DEPTH": 2},
-    "bst12p2": {"GPDLA_BST_DEPTH": 2},
     "bst_ex2": {"GPDLA_BST_EX": 2},
     "bst_ex8": {"GPDLA_BST_EX": 8},
 }
