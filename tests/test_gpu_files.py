@@ -69,16 +69,19 @@ def _rank_worker(rank, world, port, base, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.timeout(300)
-def test_run_process_qsos_two_ranks(tmp_path):
+@pytest.mark.timeout(400)
+@pytest.mark.parametrize("world,Q", [(2, 6), (4, 36)])
+def test_run_process_qsos_ranks(tmp_path, world, Q):
     """One process per GPU (ranks share the device on a one-GPU box): the sharded run writes the
-    same processed_qsos file as the single-process run."""
+    same processed_qsos file as the single-process run -- 2 ranks on 6 spectra (one chunk block:
+    rank 1 gets an empty shard) and 4 ranks on 36 (5 blocks of <= 8 rows over the ranks, each writing
+    its own chunks)."""
     import socket
 
     import torch.multiprocessing as mp
     single, multi = tmp_path / "single", tmp_path / "multi"
     for d in (single, multi):
-        write_reference_tree(d, Q=6, S=48, k=8)
+        write_reference_tree(d, Q=Q, S=48, k=8)
     args = ("dr12q", "dr9q_minus_concordance", "dr9q_concordance",
             " prior_catalog.in_dr9 & prior_catalog.los_inds(dla_catalog_name)", "dr12q", "dr12q",
             "(catalog.filter_flags == 0)")
@@ -88,10 +91,10 @@ def test_run_process_qsos_two_ranks(tmp_path):
         port = s.getsockname()[1]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_rank_worker, args=(r, 2, port, str(multi), q)) for r in range(2)]
+    procs = [ctx.Process(target=_rank_worker, args=(r, world, port, str(multi), q)) for r in range(world)]
     for pr in procs:
         pr.start()
-    assert sorted(q.get(timeout=240) for _ in range(2)) == [0, 1]
+    assert sorted(q.get(timeout=300) for _ in range(world)) == list(range(world))
     for pr in procs:
         pr.join(timeout=60)
         assert pr.exitcode == 0
