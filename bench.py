@@ -202,7 +202,7 @@ WORKLOADS = {
                label="configs[3]: full DR12Q count split over the ranks (spectrum shards), k=20, fp64"),
     "c5": dict(spectra=128, samples=100000, k=50, dr12q=False, scaling="weak", default_path="panel_gemm_i8_24",
                label="configs[4]: 128 spectra/GPU x 10^5 DLA samples, k=50 (quoted in fp32; run on the int8 "
-                     "panel-GEMM path with the 24-bit Gram contraction, ~2e-7 from fp64; --path panel_gemm_i8 "
+                     "panel-GEMM path with the 24-bit Gram contraction and fp32 raw profiles, ~2.5e-7 from fp64; --path panel_gemm_i8 "
                      "for the 32-bit one, ~4e-9; --path panel_gemm for the fp64 GEMMs)"),
 }
 
@@ -725,8 +725,9 @@ def main():
         "scaling": wl["scaling"],
         "vs_baseline": None,
         "dtype": {"fused": "f64", "panel-GEMM": "f64",
-                  "panel-GEMM-int8-24": "f64+i8 (Gram contraction exact in int8/int32 over 24-bit-quantised "
-                                        "operands, u over 32-bit, fp64 elsewhere; fp32-class, ~2e-7 from fp64)"}.get(
+                  "panel-GEMM-int8-24": "f64+i8+f32 (Gram contraction exact in int8/int32 over 24-bit-quantised "
+                                        "operands, u over 32-bit, raw Voigt profiles in fp32, fp64 elsewhere; "
+                                        "fp32-class, ~2.5e-7 from fp64)"}.get(
                      path, "f64+i8 (Gram/u contraction exact in int8/int32 over 32-bit-quantised operands, fp64 elsewhere)"),
         "data": "synthetic (seeded; SURVEY.md 8d model/spectra, unscrambled Halton samples)"
                 + ("; DR12Q-shaped pool of 4096 spectra tiled to the count" if wl["dr12q"] else ""),
