@@ -179,8 +179,8 @@ __device__ inline f2v raw_profile3_pair_f32(double lam0, double lam1, const doub
 // in packed fp32, raw_profile3_pair_f32); everything from the broadened absorption on in fp64.
 // --------------------------------------------------------------------------------------------
 template <bool kF32>
-__device__ inline void weights_i8_task(const WeightsI8Args& a, const SpecInfo& inf, int blk, int g, int h,
-                                       int lane, const double* __restrict__ core,
+__device__ inline void weights_i8_task(const WeightsI8Args& a, const double* __restrict__ srow, const SpecInfo& inf,
+                                       int blk, int g, int h, int lane, const double* __restrict__ core,
                                        const double* __restrict__ wing_lds, const double* __restrict__ exp_lds) {
   using W = typename std::conditional<kF32, float, double>::type;
   constexpr int kB = kF32 ? 2 : kWB;              // raw profiles per batch
@@ -248,7 +248,7 @@ __device__ inline void weights_i8_task(const WeightsI8Args& a, const SpecInfo& i
 #pragma unroll
       for (int b = 0; b < kB; ++b) {
         const int t = tg + kB * qb + b;
-        lam[b] = t < L ? a.srow[((int64_t)g * Ls + t) * 8] : a.lam_pad[(int64_t)g * L + t + 2 * kWidth];
+        lam[b] = t < L ? srow[((int64_t)g * Ls + t) * 8] : a.lam_pad[(int64_t)g * L + t + 2 * kWidth];
       }
       if constexpr (kF32) {
         const f2v p = raw_profile3_pair_f32(lam[0], lam[1], afac, nl2e, oc, core, wing_lds);
@@ -263,7 +263,7 @@ __device__ inline void weights_i8_task(const WeightsI8Args& a, const SpecInfo& i
         const int t = tg + e;
         double y = 0.0, noise = 1.0, mu = 0.0, om2 = 0.0, su = kI8ScaleU, sg = kI8ScaleG;
         if (t < L) {
-          const double* sr = a.srow + ((int64_t)g * Ls + t) * 8;
+          const double* sr = srow + ((int64_t)g * Ls + t) * 8;
           y = sr[1]; noise = sr[2]; mu = sr[3]; om2 = sr[4]; su = sr[6]; sg = sr[7];
         }
         const W w6 = w6v[b];
@@ -313,8 +313,10 @@ __device__ inline void weights_i8_task(const WeightsI8Args& a, const SpecInfo& i
 constexpr int kWingLds = 4 * ((3 * kWingStride + 3) / 4);
 
 // grid (ceil(sc / 64), 4 quarters), 4 waves = the 4 segments of one task column
+// srow separately and __restrict__: the kernel never writes the slot scalars, so their wave-uniform
+// loads can be scalar (s_load into SGPRs) instead of 64-lane vector loads into VGPRs
 template <bool kF32>
-__global__ __launch_bounds__(256) void weights_i8_kernel(WeightsI8Args a) {
+__global__ __launch_bounds__(256) void weights_i8_kernel(WeightsI8Args a, const double* __restrict__ srow) {
   __shared__ __attribute__((aligned(16))) double tables[3 * kCoreTable + kWingLds + 64];
   const SpecInfo inf = a.info[a.q];
   if (inf.J == 0) return;  // the LDL kernel writes NaN
@@ -325,7 +327,7 @@ __global__ __launch_bounds__(256) void weights_i8_kernel(WeightsI8Args a) {
   if (threadIdx.x < 64) exp_lds[threadIdx.x] = a.lines.buf[kLineBufExp2 + threadIdx.x];
   if (threadIdx.x < 3 * kWingStride) wing_lds[threadIdx.x] = a.lines.buf[kLineBufWing + threadIdx.x];
   __syncthreads();
-  weights_i8_task<kF32>(a, inf, blockIdx.x, __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), blockIdx.y,
+  weights_i8_task<kF32>(a, srow, inf, blockIdx.x, __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), blockIdx.y,
                         threadIdx.x & 63, core_lds, wing_lds, exp_lds);
 }
 
@@ -695,9 +697,9 @@ hipError_t launch_weights_i8(const WeightsI8Args& a, hipStream_t s) {
   // the 24-bit path (3 Gram digit planes) takes the fp32 raw profiles
   const dim3 grid((unsigned)((a.sc + 63) / 64), kWeightQuarters);
   if (a.nd == 3)
-    hipLaunchKernelGGL(weights_i8_kernel<true>, grid, dim3(256), 0, s, a);
+    hipLaunchKernelGGL(weights_i8_kernel<true>, grid, dim3(256), 0, s, a, a.srow);
   else
-    hipLaunchKernelGGL(weights_i8_kernel<false>, grid, dim3(256), 0, s, a);
+    hipLaunchKernelGGL(weights_i8_kernel<false>, grid, dim3(256), 0, s, a, a.srow);
   return hipGetLastError();
 }
 
