@@ -296,7 +296,7 @@ PROFILE_SUMMARY = ROOT / "profiles" / "r5s_c2_summary.json"     # configs[1], fu
 PROFILE_SUMMARY_C5 = {
     "panel-GEMM-int8": (ROOT / "profiles" / "r2a_c5_summary.json",
                         ("gpdla::gemm_i8_kernel(gpdla::GemmI8Args)",)),
-    "panel-GEMM-int8-24": (ROOT / "profiles" / "r8f_c5_summary.json",
+    "panel-GEMM-int8-24": (ROOT / "profiles" / "r9z_c5_summary.json",
                            ("gpdla::gemm_i8_bst_kernel(gpdla::GemmI8Args)",
                             "void gpdla::gemm_i8_kernel<4>(gpdla::GemmI8Args)")),
     "panel-GEMM": (ROOT / "profiles" / "r5f_c5f64_summary.json", ("gpdla::gemm_f64_kernel(gpdla::GemmF64Args)",)),
