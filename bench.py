@@ -208,6 +208,21 @@ WORKLOADS = {
 
 
 def run_e2e(args, world: int, rank: int, local_rank: int, dist) -> None:
+    """--workload e2e: e2e_record's line on rank 0."""
+    from gp_dla_detection_amd import _lib as L
+    dev, err = assign_device(world, local_rank, L.load().gpdla_device_count(), args.rehearsal)
+    if err:
+        refuse(err, rank)
+    rec = e2e_record(args.spectra or 162861, args.samples or 10000, args.k or 20, args.e2e_dir, args.e2e_keep,
+                     world, rank, dist, dev)
+    if rank == 0:
+        if world > 1 and args.rehearsal and rec["e2e"]["devices_used"] < world:
+            rec["rehearsal"] = {"value_if_counted": rec["value"], "note": "ranks shared GPUs: not an N-GPU point"}
+            rec["value"] = None
+        print(json.dumps(rec), flush=True)
+
+
+def e2e_record(Q: int, S: int, k: int, e2e_dir, keep: bool, world: int, rank: int, dist, dev: int):
     """configs[2] end to end: the whole process_qsos script on files --
     catalog.mat, learned_qso_model_*.mat, dla_samples.mat and preloaded_qsos.mat in (written
     beforehand, untimed, as the reference's processed/ tree of 162,861 DR12Q-shaped spectra),
@@ -219,10 +234,8 @@ def run_e2e(args, world: int, rank: int, local_rank: int, dist) -> None:
     from gp_dla_detection_amd import _lib as L
     from gp_dla_detection_amd import process as PR
     from gp_dla_detection_amd import synthetic as syn
-    Q = args.spectra or 162861
-    S = args.samples or 10000
-    base = args.e2e_dir or f"/tmp/gpdla_e2e_{Q}_{S}"
-    model = syn.make_model(k=args.k or 20)
+    base = e2e_dir or f"/tmp/gpdla_e2e_{Q}_{S}"
+    model = syn.make_model(k=k)
     samples = syn.make_samples(S)
     t0 = time.perf_counter()
     if rank == 0:
@@ -236,7 +249,6 @@ def run_e2e(args, world: int, rank: int, local_rank: int, dist) -> None:
         dist.broadcast_object_list(box, src=0)
         names = box[0]
         dist.barrier()
-    dev = local_rank % max(1, L.load().gpdla_device_count())
     tm = {}
     t0 = time.perf_counter()
     PR.run_process_qsos(base, names["training_release"], names["training_set_name"], names["dla_catalog_name"],
@@ -262,13 +274,13 @@ def run_e2e(args, world: int, rank: int, local_rank: int, dist) -> None:
         # ranks sharing one leased GPU each wait for the whole job), the write as measured
         ndev = max(1, min(world, L.load().gpdla_device_count()))
         proj8 = load_s * world / 8 + compute_s * ndev / 8
-        print(json.dumps({
+        rec = {
             "metric": "(spectrum x DLA-sample) log-evidence evals/sec", "value": evals / total, "unit": "evals/s",
             "n_gpus": world, "steps": 1, "warmup": 0, "ms_per_step": total * 1e3, "higher_is_better": True,
             "scaling": "strong", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic (seeded; DR12Q-shaped pool of 4096 spectra tiled to the count), written as the "
                     "reference's processed/ tree before the timed region",
-            "config": {"workload": f"configs[2] end to end: process_qsos on files, {Q} spectra x {S} samples, k=20, "
+            "config": {"workload": f"configs[2] end to end: process_qsos on files, {Q} spectra x {S} samples, k={k}, "
                                    f"fp64 -> processed_qsos v7.3 ({out_bytes / 1e9:.1f} GB)",
                        "spectra": Q, "num_samples": S, "parallelism": f"spectrum-shard x{world}"},
             "e2e": {"total_s": total, "load_s": load_s, "compute_s": compute_s, "write_s": write_s,
@@ -280,12 +292,14 @@ def run_e2e(args, world: int, rank: int, local_rank: int, dist) -> None:
                         "note": "ideal-scaling estimate, not a measurement: load x world/8 + compute x "
                                 "devices_used/8 (linear speed-up from the devices used to 8 assumed) + write "
                                 "as measured"},
+                    "devices_used": ndev,
                     "note": "load = catalogues, model, samples and this rank's preloaded_qsos cells "
                             "(process_qsos.m:1-63); compute = the engine incl. its creation (:88-212); "
-                            "write = priors/posteriors and the v7.3 file (:222-249), page cache, no fsync"}}),
-              flush=True)
-        if not args.e2e_keep:
+                            "write = priors/posteriors and the v7.3 file (:222-249), page cache, no fsync"}}
+        if not keep:
             shutil.rmtree(base, ignore_errors=True)
+        return rec
+    return None
 
 
 # rocprofv3 summaries of the bench workloads (tools/profile.sh + tools/summarize_profile.py), committed
@@ -294,8 +308,9 @@ PROFILE_SUMMARY = ROOT / "profiles" / "r5s_c2_summary.json"     # configs[1], fu
 # kernel's launches (the GEMM launches of one spectrum and sample chunk; per-batch conversion kernels
 # such as convert_gemm_i8_kernel are not part of it)
 PROFILE_SUMMARY_C5 = {
-    "panel-GEMM-int8": (ROOT / "profiles" / "r2a_c5_summary.json",
-                        ("gpdla::gemm_i8_kernel(gpdla::GemmI8Args)",)),
+    # the 32-bit path's Gram + u launch is gemm_i8_kernel<4> (round-2 profiles predate the template)
+    "panel-GEMM-int8": (ROOT / "profiles" / "r10_c5i8_summary.json",
+                        ("void gpdla::gemm_i8_kernel<4>(gpdla::GemmI8Args)",)),
     "panel-GEMM-int8-24": (ROOT / "profiles" / "r9z_c5_summary.json",
                            ("gpdla::gemm_i8_bst_kernel(gpdla::GemmI8Args)",
                             "void gpdla::gemm_i8_kernel<4>(gpdla::GemmI8Args)")),
@@ -331,9 +346,44 @@ def profiled_traffic(Q: int, S: int, k: int, path: str = "fused"):
     return None, None
 
 
-def timed_steps(step, synchronize, steps: int, dist=None) -> float:
+E2E_DISK_BYTES = 48e9   # alternatives.e2e: the 13 GB output, the ~5 GB processed/ tree, and headroom
+
+
+def dram_record(traffic, ms, src, path: str) -> dict:
+    """The roofline kernel's DRAM side, recomputable from the committed profile: its PMC bytes per
+    launch (2 x FETCH_SIZE + WRITE_SIZE, MI355X_MICROARCH.md) over its measured launch time, as a
+    fraction of the 8 TB/s HBM peak."""
+    note = ("configs[1]'s fused kernel is FP64-pipe-bound (roofline.bound): the north star's >= 40% "
+            "HBM-roofline target is not a statement about this kernel, whose DRAM use is this small fraction"
+            if path in ("fused", "fused-int8") else
+            "the roofline kernel's PMC bytes per launch over its HIP-event launch time")
+    if traffic is None or not ms:
+        return {"bytes_per_launch": None, "gbs": None, "frac": None, "peak": HBM_PEAK_GBS,
+                "note": "no committed PMC profile for this workload and path"}
+    gbs = traffic / (ms * 1e-3) / 1e9
+    return {"bytes_per_launch": traffic, "gbs": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": gbs / HBM_PEAK_GBS, "source": src, "note": note}
+
+
+def chain_dram(path: str) -> dict | None:
+    """configs[4]'s whole kernel chain from its committed profile: every kernel's PMC HBM bytes over
+    every kernel's time, per engine batch (tools/summarize_profile.py per_batch)."""
+    if path not in PROFILE_SUMMARY_C5 or not PROFILE_SUMMARY_C5[path][0].exists():
+        return None
+    f = PROFILE_SUMMARY_C5[path][0]
+    pb = json.loads(f.read_text()).get("per_batch")
+    if not pb:
+        return None
+    gbs = pb["hbm_bytes_per_batch"] / (pb["kernel_ms_per_batch"] * 1e-3) / 1e9
+    return {"bytes_per_batch": pb["hbm_bytes_per_batch"], "kernel_ms_per_batch": pb["kernel_ms_per_batch"],
+            "gbs": gbs, "peak": HBM_PEAK_GBS, "frac": gbs / HBM_PEAK_GBS, "source": str(f.relative_to(ROOT)),
+            "note": "all kernels of the chain (weights, Gram and u GEMMs, LDL^T, per-batch prep/convert/reduce)"}
+
+
+def timed_steps(step, synchronize, steps: int, dist=None, local: list | None = None) -> float:
     """The bench contract's timed region: barrier + device sync on both sides of exactly ``steps``
-    steps, elapsed time max-reduced over the ranks (gloo, host-side)."""
+    steps, elapsed time max-reduced over the ranks (gloo, host-side).  ``local`` (if given) receives
+    this rank's own elapsed time."""
     synchronize()
     if dist is not None:
         dist.barrier()
@@ -344,6 +394,8 @@ def timed_steps(step, synchronize, steps: int, dist=None) -> float:
     if dist is not None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    if local is not None:
+        local.append(elapsed)
     if dist is not None:
         import torch
         tt = torch.tensor([elapsed], dtype=torch.float64)
@@ -440,19 +492,46 @@ def gather(obj, world: int, dist):
     return out
 
 
-def plan_only(wl: dict, world: int, rank: int, local_rank: int, dist) -> None:
+REFUSAL_EXIT = 3
+
+
+def assign_device(world: int, local_rank: int, ndev: int, rehearsal: bool):
+    """(device, error): one GPU per rank, ``local_rank`` -> device ``local_rank``.  With fewer devices
+    than ranks the ranks would share GPUs and an N-rank line would not be an N-GPU point: that is
+    refused (error set) unless ``rehearsal``, where ranks share devices round-robin."""
+    if ndev < 1:
+        return None, "no HIP device"
+    if world > ndev and not rehearsal:
+        return None, (f"{world} ranks but only {ndev} device(s): ranks would share GPUs, so the line would "
+                      f"not be a {world}-GPU measurement; refusing (pass --rehearsal to run anyway: value null)")
+    return local_rank % ndev, None
+
+
+def refuse(msg: str, rank: int) -> None:
+    print(f"bench.py (rank {rank}): {msg}", file=sys.stderr, flush=True)
+    sys.exit(REFUSAL_EXIT)
+
+
+def plan_only(wl: dict, world: int, rank: int, local_rank: int, dist, ndev: int | None = None,
+              rehearsal: bool = False) -> None:
     """--plan-only: the multi-rank layout (which spectra each rank evaluates and on which device)
-    through the same launcher and process group as a measured run, without any GPU call."""
+    through the same launcher and process group as a measured run, without any GPU call.  ``ndev``
+    is the device count planned against (default one per rank); the device-sharing refusal of a
+    measured run applies."""
+    dev, err = assign_device(world, local_rank, world if ndev is None else ndev, rehearsal)
+    if err:
+        refuse(err, rank)
     pool_pixels = None
     if wl["dr12q"]:
         from gp_dla_detection_amd import synthetic as syn
         pool_pixels = [p["wavelengths"].size for p in dr12q_pool(syn.make_model(k=wl["k"]))]
     ids = rank_spectrum_ids(wl, rank, world, pool_pixels)
-    allr = gather({"rank": rank, "local_rank": local_rank, "device": local_rank, "ids": ids}, world, dist)
+    allr = gather({"rank": rank, "local_rank": local_rank, "device": dev, "ids": ids}, world, dist)
     if rank == 0:
         cat = np.concatenate([r["ids"] for r in allr])
         print(json.dumps({
-            "plan_only": True, "n_gpus": world,
+            "plan_only": True, "n_gpus": world, "rehearsal": bool(rehearsal and len({r["device"] for r in allr}) < world),
+            "distinct_devices": len({r["device"] for r in allr}),
             "world_size": dist.get_world_size() if dist is not None else 1,
             "workload": wl["label"],
             "ranks": [{"rank": r["rank"], "local_rank": r["local_rank"], "device": r["device"],
@@ -510,6 +589,8 @@ def configs4_alternative(dev: int, steps: int) -> dict:
     roof = i8_roofline(st, n_mean, k, Q, S, steps, path)
     traffic, src = profiled_traffic(Q, S, k, path)
     roof.update({"kernel": ROOFLINE_KERNEL[path], "traffic": traffic, "traffic_source": src})
+    dram = dram_record(traffic, roof["avg_launch_ms"], src, path)
+    dram["chain"] = chain_dram(path)
     for a in (*t.values(), o_null, o_dla, o_s, o_n):
         a.free()
     return {"value": Q * S * steps / el, "unit": "evals/s", "ms_per_step": el / steps * 1e3, "steps": steps,
@@ -520,15 +601,97 @@ def configs4_alternative(dev: int, steps: int) -> dict:
                           "gemm_per_chunk": st["contraction_ms"] / max(st["contraction_launches"], 1),
                           "batch": st["likelihood_ms"] / max(st["likelihood_launches"], 1),
                           "reduce": st["reduce_ms"] / max(st["reduce_launches"], 1)},
-            "roofline": roof,
+            "roofline": roof, "dram": dram,
             "max_rel_err_vs_fp64_panel": errs, "parity_subset": f"first {sub} of {Q} spectra, all {S} samples",
             "checks_ok": bool(np.all(np.isfinite(sll)) and errs["sample_log_likelihoods_dla"] < 5e-7
                               and np.max(np.abs(inv - 1)) < 1e-10)}
 
 
+def invariant_all_rows(o_s, o_dla, S: int, threads: int = 8, rows_per_task: int = 4096) -> dict:
+    """The calc_cddf.py:246 invariant sum_s exp(l_s - l_DLA - log S) = 1 and finiteness on EVERY row of
+    a device-resident Q x S sample array (D2H in row blocks on a thread pool; ctypes and numpy release
+    the GIL)."""
+    from concurrent.futures import ThreadPoolExecutor
+    lld = o_dla.numpy()
+    Q = lld.size
+
+    def block(r0):
+        sll = o_s.numpy(rows=rows_per_task, start=r0)
+        inv = np.exp(sll - (lld[r0:r0 + sll.shape[0], None] + np.log(S))).sum(axis=1)
+        return float(np.max(np.abs(inv - 1))), bool(np.all(np.isfinite(sll)))
+
+    with ThreadPoolExecutor(max_workers=threads) as ex:
+        res = list(ex.map(block, range(0, Q, rows_per_task)))
+    return {"rows": int(Q), "max_abs_dev": max(r[0] for r in res),
+            "finite": all(r[1] for r in res) and bool(np.all(np.isfinite(lld)))}
+
+
+def configs2_alternative(dev: int) -> dict:
+    """BASELINE configs[2] beside the headline (the north star's "full DR12Q"): 162,861 DR12Q-shaped
+    spectra x 10^4 DLA samples, k = 20, fp64 fused path, all on this GPU, inputs resident and the 13 GB
+    of sample log-likelihoods left in HBM.  One untimed warm-up call on the first 1,024 spectra, then
+    ONE timed call over all of them (process_qsos.m:88-212 over the whole catalogue); the invariant
+    calc_cddf.py:246 is checked on every spectrum afterwards."""
+    from gp_dla_detection_amd import _lib as L
+    from gp_dla_detection_amd import synthetic as syn
+    from gp_dla_detection_amd.engine import Engine
+    from gp_dla_detection_amd.parameters import set_parameters
+    wl = WORKLOADS["c3"]
+    Q, S, k = wl["spectra"], wl["samples"], wl["k"]
+    t0 = time.perf_counter()
+    model = syn.make_model(k=k)
+    samples = syn.make_samples(S)
+    pool = dr12q_pool(model)
+    packed = syn.pack_spectra([pool[i % len(pool)] for i in range(Q)])
+    del pool
+    t = {key: L.DeviceArray.from_numpy(packed[key], device=dev)
+         for key in ("wavelengths", "flux", "noise_variance", "pixel_mask", "z_qsos")}
+    o_null, o_dla = L.DeviceArray(dev, Q, np.float64), L.DeviceArray(dev, Q, np.float64)
+    o_s, o_n = L.DeviceArray(dev, (Q, S), np.float64), L.DeviceArray(dev, Q, np.int32)
+    setup_s = time.perf_counter() - t0
+    offs = packed["offsets"]
+    with Engine(model, samples, set_parameters(k=k), device=dev) as eng:
+        def call(off):
+            eng.process_device(off, t["wavelengths"].ptr, t["flux"].ptr, t["noise_variance"].ptr,
+                               t["pixel_mask"].ptr, t["z_qsos"].ptr, o_null.ptr, o_dla.ptr, o_s.ptr, S,
+                               npix_ptr=o_n.ptr)
+        call(offs[:1025])
+        eng.synchronize()
+        eng.reset_stats()
+        t0 = time.perf_counter()
+        call(offs)
+        eng.synchronize()
+        el = time.perf_counter() - t0
+        st = eng.stats()
+    t0 = time.perf_counter()
+    inv = invariant_all_rows(o_s, o_dla, S)
+    check_s = time.perf_counter() - t0
+    npix = o_n.numpy()
+    n_mean = float(np.mean(npix))
+    lk_ms = st["likelihood_ms"]
+    flops = float(np.sum(algorithmic_flops_per_eval(npix.astype(np.float64), k))) * (S + 1)
+    for a in (*t.values(), o_null, o_dla, o_s, o_n):
+        a.free()
+    return {"value": Q * S / el, "unit": "evals/s", "wall_s": el, "ms_per_step": el * 1e3, "steps": 1,
+            "warmup": "one call on the first 1,024 spectra",
+            "north_star_under_60s": bool(el < 60.0),
+            "config": {"workload": wl["label"] + "; inputs resident in HBM, outputs (13 GB) left in HBM",
+                       "spectra": Q, "num_samples": S, "k": k, "n_pixels_mean": n_mean, "likelihood_path": "fused"},
+            "kernel_ms": {"prep_total": st["prep_ms"], "likelihood_total": lk_ms, "reduce_total": st["reduce_ms"],
+                          "likelihood_launches": st["likelihood_launches"]},
+            "roofline": {"bound": "mfma", "unit": "TFLOP/s", "peak": FP64_PEAK_TFLOPS,
+                         "achieved": flops / (lk_ms * 1e-3) / 1e12, "frac": flops / (lk_ms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS,
+                         "kernel": "likelihood_kernel<20> (all launches of the call)",
+                         "flops": flops, "note": "SURVEY 8d F_eval summed over every spectrum's own n, incl. the "
+                                                 "null model; over the summed HIP-event times of the likelihood launches"},
+            "invariant_calc_cddf_246": inv, "invariant_check_s": check_s, "setup_untimed_s": setup_s,
+            "checks_ok": bool(inv["finite"] and inv["max_abs_dev"] < 1e-10)}
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs = ranks (default: WORLD_SIZE under a launcher, else 1)")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--e2e-dir", default=None, help="e2e: directory for the processed/ tree (default /tmp/...)")
@@ -548,14 +711,25 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU-baseline work (0 = skip)")
     ap.add_argument("--plan-only", action="store_true",
                     help="print the rank/spectrum/device layout through the launcher, no GPU call")
+    ap.add_argument("--plan-devices", type=int, default=None,
+                    help="--plan-only: the device count to plan against (default: one per rank)")
+    ap.add_argument("--rehearsal", action="store_true",
+                    help="allow N ranks on fewer than N devices (ranks share GPUs); the line then carries "
+                         "value null and is labelled a rehearsal, never an N-GPU point")
+    ap.add_argument("--no-configs2", action="store_true",
+                    help="skip alternatives.configs2 (full DR12Q count on this GPU) in the default line")
+    ap.add_argument("--no-e2e", action="store_true",
+                    help="skip alternatives.e2e (configs[2] end to end on files) in the default line")
     args = ap.parse_args()
 
-    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+    if "WORLD_SIZE" not in os.environ and (args.gpus or 1) > 1:
         # no launcher: start the N ranks as children (nothing has touched the GPU yet)
         sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus is None:          # under torch.distributed.run without --gpus: the launcher's count
+        args.gpus = world
     if world != args.gpus:
         print(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks", file=sys.stderr)
         sys.exit(2)
@@ -578,7 +752,7 @@ def main():
         if getattr(args, key) is not None:
             wl[key] = getattr(args, key)
     if args.plan_only:
-        plan_only(wl, world, rank, local_rank, dist if world > 1 else None)
+        plan_only(wl, world, rank, local_rank, dist if world > 1 else None, args.plan_devices, args.rehearsal)
         if world > 1:
             with _stdout_to_stderr():
                 dist.destroy_process_group()
@@ -607,8 +781,10 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and args.cpu_budget > 0:
         cpu = cpu_baseline(model, samples, spectra, args.cpu_budget, args.k)
-    # one GPU per local rank; on a box with fewer GPUs than ranks (rehearsal) ranks share devices
-    dev = local_rank % max(1, L.load().gpdla_device_count())
+    # one GPU per local rank; fewer devices than ranks is refused unless --rehearsal (ranks share devices)
+    dev, err = assign_device(world, local_rank, L.load().gpdla_device_count(), args.rehearsal)
+    if err:
+        refuse(err, rank)
     D = lambda a: L.DeviceArray.from_numpy(a, device=dev)
     t = {key: D(packed[key]) for key in ("wavelengths", "flux", "noise_variance", "pixel_mask", "z_qsos")}
     S = args.samples
@@ -621,6 +797,10 @@ def main():
     ranks = gather({"rank": rank, "local_rank": local_rank, "device": dev, "pci_bus_id": L.pci_bus_id(dev),
                     "spectra": int(Q), "first_spectrum": int(ids[0]), "last_spectrum": int(ids[-1])},
                    world, dist if world > 1 else None)
+    distinct = len({r["pci_bus_id"] for r in ranks})
+    if distinct < world and not args.rehearsal:
+        refuse(f"{world} ranks drive only {distinct} distinct GPU(s) (PCI ids "
+               f"{sorted({r['pci_bus_id'] for r in ranks})}): not a {world}-GPU measurement", rank)
 
     if args.path == "auto" and "default_path" in wl:
         args.path = wl["default_path"]
@@ -645,12 +825,28 @@ def main():
         step()
     eng.synchronize()
     eng.reset_stats()
-    elapsed = timed_steps(step, eng.synchronize, args.steps, dist if world > 1 else None)
+    local = []
+    elapsed = timed_steps(step, eng.synchronize, args.steps, dist if world > 1 else None, local)
     st = eng.stats()
+    npix = o_n.numpy()
+    n_mean = float(np.mean(npix))
 
-    # alternative path on the same resident inputs (1 GPU, configs[1]): the int8 Ozaki contraction
-    # next to the fp64 line, with its measured deviation from the fp64 outputs.  Not `value`: the
-    # headline stays on the path that computes the contraction in fp64.
+    # per-rank load balance: each rank's own kernel time and wall time over the timed steps
+    per_rank = gather({"rank": rank, "spectra": int(Q), "pixels": int(np.sum(npix)),
+                       "likelihood_ms_per_step": st["likelihood_ms"] / args.steps,
+                       "kernel_ms_per_step": (st["prep_ms"] + st["likelihood_ms"] + st["reduce_ms"]) / args.steps,
+                       "elapsed_ms_per_step": local[0] / args.steps * 1e3}, world, dist if world > 1 else None)
+    for r, pr in zip(ranks, per_rank):
+        r.update({k: v for k, v in pr.items() if k != "rank"})
+    km = np.array([r["kernel_ms_per_step"] for r in per_rank])
+    em = np.array([r["elapsed_ms_per_step"] for r in per_rank])
+    imbalance = {"kernel_ms_max_over_mean": float(km.max() / km.mean()) if km.mean() > 0 else None,
+                 "elapsed_max_over_mean": float(em.max() / em.mean()) if em.mean() > 0 else None,
+                 "note": "per-rank HIP-event kernel time and rank-local wall time of the timed steps; the "
+                         "line's ms_per_step is the max over ranks"}
+
+    # alternative paths / configs on the same GPU (1 GPU, configs[1] default line).  None is `value`:
+    # the headline stays on configs[1] on the path that computes the contraction in fp64.
     alt = None
     if world == 1 and not args.no_alt and not wl["dr12q"] and args.k == 20 and args.path == "auto":
         o_s2 = L.DeviceArray(dev, (Q, S), np.float64)
@@ -675,23 +871,35 @@ def main():
         alt = {"fused_i8": {
             "value": Q * S * args.steps / el2, "unit": "evals/s", "ms_per_step": el2 / args.steps * 1e3,
             "kernel_ms": {"prep+convert": st2["prep_ms"] / max(st2["prep_launches"], 1), "likelihood": l2},
-            "fp64_equivalent_tflops": algorithmic_flops_per_eval(float(np.mean(o_n.numpy())), args.k)
-                                      * Q * (S + 1) / (l2 * 1e-3) / 1e12,
+            "fp64_equivalent_tflops": algorithmic_flops_per_eval(n_mean, args.k) * Q * (S + 1) / (l2 * 1e-3) / 1e12,
             "max_rel_err_vs_fp64": {"sample_log_likelihoods_dla(256 spectra)": rel, "log_likelihoods_dla": rel_dla},
             "note": "likelihood_i8_kernel<20>: Gram/u contraction exact on v_mfma_i32_16x16x64_i8 over "
                     "32-bit-quantised weights/panel (4 digits, levels <= 3), fp64 everywhere else; "
                     "within the 1e-6 contract, not bitwise-fp64 (DESIGN.md section 4)"}}
-        del o_s2, o_null2, o_dla2
+        for a in (o_s2, o_null2, o_dla2):
+            a.free()
         # BASELINE configs[4] (k = 50, 10^5 samples) on the int8 panel-GEMM path, driver-timed
         alt["configs4"] = configs4_alternative(dev, args.steps)
 
-    # sanity: finite outputs and the calc_cddf.py:246 normalisation invariant
-    sll = o_s.numpy(rows=2048)  # the check covers the leading spectra (c3/c4 outputs are 13 GB)
-    lld = o_dla.numpy()[: sll.shape[0]]
-    npix = o_n.numpy()
-    ok = bool(np.all(np.isfinite(sll)) and np.all(np.isfinite(lld)))
-    inv = np.exp(sll - (lld[:, None] + np.log(S))).sum(axis=1)
-    ok = ok and bool(np.max(np.abs(inv - 1)) < 1e-10)
+    # sanity: finite outputs and the calc_cddf.py:246 normalisation invariant on every spectrum
+    inv = invariant_all_rows(o_s, o_dla, S)
+    ok = bool(inv["finite"] and inv["max_abs_dev"] < 1e-10)
+    for a in (*t.values(), o_null, o_dla, o_s, o_n):
+        a.free()
+
+    if alt is not None and not args.no_configs2:
+        # BASELINE configs[2]: the full DR12Q count on this GPU, driver-timed (north star "< 60 s")
+        alt["configs2"] = configs2_alternative(dev)
+    if alt is not None and not args.no_e2e:
+        import shutil
+        base = args.e2e_dir or "/tmp/gpdla_e2e_alt"
+        Path(base).parent.mkdir(parents=True, exist_ok=True)
+        free = shutil.disk_usage(Path(base).parent).free
+        if free >= E2E_DISK_BYTES:
+            alt["e2e"] = e2e_record(162861, 10000, 20, base, False, 1, 0, None, dev)
+        else:
+            alt["e2e"] = {"skipped": f"{free / 1e9:.0f} GB free under {Path(base).parent}, "
+                                     f"{E2E_DISK_BYTES / 1e9:.0f} GB needed (13 GB output + the processed/ tree)"}
 
     q_total = Q
     if world > 1:  # spectra over all ranks (LPT shards of configs[3] differ in size)
@@ -701,7 +909,6 @@ def main():
         q_total = int(qt.item())
     evals_total = q_total * S * args.steps
     value = evals_total / elapsed
-    n_mean = float(np.mean(npix))
     launches = max(st["likelihood_launches"], 1)
     avg_ms = st["likelihood_ms"] / launches
     evals_per_launch = Q * (S + 1) * args.steps / launches  # incl. the null-model evaluation
@@ -710,14 +917,27 @@ def main():
     eff_gbs = effective_bytes_per_eval(n_mean, args.k) * evals_per_launch / (avg_ms * 1e-3) / 1e9
 
     traffic, traffic_src = profiled_traffic(Q, S, args.k, path)
+    roof = {"bound": "mfma", "achieved": achieved_tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": achieved_tf / FP64_PEAK_TFLOPS, "traffic": traffic,
+            "traffic_source": traffic_src,
+            "kernel": ROOFLINE_KERNEL.get(path, path).format(k=args.k),
+            "avg_launch_ms": avg_ms,
+            "flops_per_eval": algorithmic_flops_per_eval(n_mean, args.k),
+            "evals_per_launch": evals_per_launch,
+            # int8 panel paths: the int8 GEMM kernel's own roofline (overrides the fields above)
+            **(i8_roofline(st, n_mean, args.k, Q, S, args.steps, path) if path.startswith("panel-GEMM-int8")
+               else f64_gemm_roofline(st, n_mean, args.k, Q, S, args.steps) if path == "panel-GEMM"
+               else {})}
+    rehearsal = world > 1 and distinct < world
     result = {
         "metric": "(spectrum x DLA-sample) log-evidence evals/sec",
-        "value": value,
+        "value": None if rehearsal else value,
         "unit": "evals/s",
         "n_gpus": world,
         "world_size": dist.get_world_size() if world > 1 else 1,
         "ranks": ranks,
-        "distinct_devices": len({r["pci_bus_id"] for r in ranks}),
+        "distinct_devices": distinct,
+        "imbalance": imbalance,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
@@ -734,25 +954,21 @@ def main():
         "config": {"workload": f"{wl['label']}; this rank: {Q} spectra, mean n={n_mean:.0f}, 3 Lyman lines",
                    "spectra_per_gpu": Q, "num_samples": S, "k": args.k, "n_pixels": n_mean,
                    "likelihood_path": path, "parallelism": f"spectrum-shard x{world}"},
-        "roofline": {"bound": "mfma", "achieved": achieved_tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": achieved_tf / FP64_PEAK_TFLOPS, "traffic": traffic,
-                     "traffic_source": traffic_src,
-                     "kernel": ROOFLINE_KERNEL.get(path, path).format(k=args.k),
-                     "avg_launch_ms": avg_ms,
-                     "flops_per_eval": algorithmic_flops_per_eval(n_mean, args.k),
-                     "evals_per_launch": evals_per_launch,
-                     # int8 panel paths: the int8 GEMM kernel's own roofline (overrides the fields above)
-                     **(i8_roofline(st, n_mean, args.k, Q, S, args.steps, path) if path.startswith("panel-GEMM-int8")
-                        else f64_gemm_roofline(st, n_mean, args.k, Q, S, args.steps) if path == "panel-GEMM"
-                        else {})},
-        "hbm_effective": {"achieved": eff_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                          "frac": eff_gbs / HBM_PEAK_GBS,
-                          "bytes_per_eval": effective_bytes_per_eval(n_mean, args.k),
-                          "note": "north-star streamed-panel accounting (SURVEY.md 8d); compulsory DRAM bytes are ~24 B/eval"},
+        "roofline": roof,
+        "dram": dram_record(traffic, roof["avg_launch_ms"], traffic_src, path),
+        "streamed_panel_equiv": {"gbs": eff_gbs, "bytes_per_eval": effective_bytes_per_eval(n_mean, args.k),
+                                 "note": "SURVEY.md 8d's streamed-panel accounting (B_eval bytes per evaluation / "
+                                         "kernel time): what a kernel re-reading the n x (k+5) panel per sample would "
+                                         "move.  Not DRAM traffic and not a roofline fraction: this fused kernel reads "
+                                         "each panel once per 64 samples (see dram)."},
         "kernel_ms": {"prep": st["prep_ms"] / max(st["prep_launches"], 1), "likelihood": avg_ms,
                       "reduce": st["reduce_ms"] / max(st["reduce_launches"], 1)},
+        "invariant_calc_cddf_246": inv,
         "checks_ok": ok,
     }
+    if rehearsal:
+        result["rehearsal"] = {"value_if_counted": value, "distinct_devices": distinct,
+                               "note": f"--rehearsal: {world} ranks shared {distinct} GPU(s); not a {world}-GPU point"}
     if cpu is not None:
         result["cpu_baseline"] = cpu
     if alt is not None:

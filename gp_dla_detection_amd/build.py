@@ -33,25 +33,31 @@ def build(verbose: bool = False, force: bool = False, out: Path | None = None,
         return OUT_
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     dflags = [f"-D{k}={v}" for k, v in sorted((defines or {}).items())]
-    objdir = OBJ_DIR / (hashlib.sha1(" ".join(dflags).encode()).hexdigest()[:12] if dflags else "head")
+    cflags = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-c", "-Wno-unused-result", *dflags]
+    # the object cache is keyed on everything that shapes an object besides its sources: the compiler
+    # (path and mtime), the full flag list and this file (a changed recipe invalidates old objects)
+    hipcc_path = Path(hipcc).resolve() if Path(hipcc).exists() else Path(hipcc)
+    key = "\n".join([str(hipcc_path), str(hipcc_path.stat().st_mtime if hipcc_path.exists() else 0),
+                     " ".join(cflags), str(Path(__file__).stat().st_mtime)])
+    objdir = OBJ_DIR / hashlib.sha1(key.encode()).hexdigest()[:16]
     objdir.mkdir(parents=True, exist_ok=True)
     hdr_mtime = max(h.stat().st_mtime for h in headers)
+    tmp_tag = f".{os.getpid()}.tmp"      # per-process temporaries: concurrent builds never share one
 
     def compile_one(src: Path) -> Path:
         obj = objdir / (src.name + ".o")
         if not force and obj.exists() and obj.stat().st_mtime >= max(src.stat().st_mtime, hdr_mtime):
             return obj
-        cmd = [hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-c", "-Wno-unused-result",
-               *dflags, "-o", str(obj) + ".tmp", str(src)]
+        cmd = [hipcc, *cflags, "-o", str(obj) + tmp_tag, str(src)]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         subprocess.run(cmd, check=True, cwd=CSRC)
-        Path(str(obj) + ".tmp").replace(obj)
+        Path(str(obj) + tmp_tag).replace(obj)
         return obj
 
     with ThreadPoolExecutor(max_workers=jobs or min(len(srcs), os.cpu_count() or 4)) as ex:
         objs = list(ex.map(compile_one, srcs))
-    tmp = OUT_.with_suffix(".so.tmp")
+    tmp = OUT_.with_name(OUT_.name + tmp_tag)
     cmd = [hipcc, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", str(tmp), *map(str, objs)]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)

@@ -551,9 +551,6 @@ int gpdla_engine_process(gpdla_engine* e, const gpdla_spectra* sp, const gpdla_r
   // Infinity Cache (GEMM -10%) but cost more in the weights and LDL^T launches.  The chunk is also
   // capped per batch by a workspace budget (panel_chunk below): per sample, the A digits (8 B per
   // slot) or the fp64 weights (16 B per slot), plus the Gram and u (8 (k(k+1)/2 + k) B).
-#ifndef GPDLA_MAX_CHUNK
-#define GPDLA_MAX_CHUNK 131072
-#endif
   constexpr int64_t kMaxChunk = GPDLA_MAX_CHUNK;
   const int64_t blocks_x = (e->S + 1 + kSamplesPerBlock - 1) / kSamplesPerBlock;
 

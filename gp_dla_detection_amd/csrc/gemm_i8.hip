@@ -539,14 +539,8 @@ __global__ __launch_bounds__(256, ND == 3 ? 3 : 2) void gemm_i8_kernel(GemmI8Arg
 // of group gi covers sample tiles s0 + 3 (r G + gi) .. + 2 (one per 4 waves), so all of an XCD's
 // blocks sweep the same 3 G sample tiles together and their A lines stay in its L2.
 // --------------------------------------------------------------------------------------------
-#ifndef GPDLA_BST_WAVES
-#define GPDLA_BST_WAVES 12
-#endif
 constexpr int kBstWaves = GPDLA_BST_WAVES;
 constexpr int kBstMaxKs = 13;                    // 13 x 12 KiB = 156 KiB of LDS: spectra up to 832 slots
-#ifndef GPDLA_BST_EX
-#define GPDLA_BST_EX 2
-#endif
 constexpr int kBstEX = GPDLA_BST_EX;
 
 __global__ __launch_bounds__(64 * kBstWaves, 1) __attribute__((amdgpu_waves_per_eu(kBstWaves / 4, kBstWaves / 4)))

@@ -6,6 +6,7 @@
 
 #include "line_profile.h"
 #include "lyman_series.h"
+#include "tuning.h"
 
 // HIP call -> C-ABI status (GPDLA_ENOMEM / GPDLA_EDEVICE with a message), in functions returning int
 #define HIP_TRY(expr)                                                                       \
@@ -190,9 +191,6 @@ __host__ __device__ inline int64_t quad_index(int64_t s, int64_t e, int64_t n) {
 // fp64 Gram / u GEMM of the panel path (gemm_f64.hip).  The weights are stored per 32-sample tile
 // as [tile][slot (cap16)][32], sample 4 g + i of the tile at position 8 i + g (weights_kernel), for
 // whole 128-sample blocks (sc rounded up to kGemmF64TileS)
-#ifndef GPDLA_F64_WAVES
-#define GPDLA_F64_WAVES 4
-#endif
 constexpr int kGemmF64Waves = GPDLA_F64_WAVES;     // waves per block, 32 samples each
 constexpr int kGemmF64TileS = 32 * kGemmF64Waves;
 __host__ __device__ inline int64_t gemm_f64_cap16(int64_t cap) { return (cap + 15) / 16 * 16; }

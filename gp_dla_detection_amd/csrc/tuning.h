@@ -1,0 +1,27 @@
+// tuning.h -- the launch-shape constants chosen by measurement, in one place.
+//
+// Each value below was picked by an A/B on the MI355X (records under profiles/, DESIGN.md section
+// 4); the alternatives lost and their code paths were deleted.  These are the only compile-time
+// knobs in the product sources: tools/build_variants.py may override one with -D to rebuild a
+// variant library for a new A/B, the product build never does.
+#pragma once
+
+// gemm_f64_kernel (fp64 panel path): waves per block, 32 samples each (profiles/r4f, r4g)
+#ifndef GPDLA_F64_WAVES
+#define GPDLA_F64_WAVES 4
+#endif
+
+// gemm_i8_bst_kernel (24-bit Gram GEMM): waves per B-stationary block (8 measured -2%, profiles/r7*)
+#ifndef GPDLA_BST_WAVES
+#define GPDLA_BST_WAVES 12
+#endif
+
+// gemm_i8_bst_kernel: XCDs sharing a sample tile's A digits (4 / 8 measured -1.3% / -5%, profiles/r5j)
+#ifndef GPDLA_BST_EX
+#define GPDLA_BST_EX 2
+#endif
+
+// panel paths: largest sample chunk per spectrum (2 / 4 / 6 equal chunks lost 2-15%, profiles/r2/c5_ab, r7e)
+#ifndef GPDLA_MAX_CHUNK
+#define GPDLA_MAX_CHUNK 131072
+#endif

@@ -12,6 +12,12 @@
 #include "gpdla.h"
 #include "mex_widen.h"
 
+static double ref_scalar(const mxArray* a, const char* name) {
+  if (mxIsCell(a) || mxIsChar(a) || mxGetNumberOfElements(a) == 0)
+    mexErrMsgIdAndTxt("gpdla:voigt", "%s must be a numeric scalar", name);
+  return mxGetScalar(a);
+}
+
 void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
   (void)nlhs;
   if (nrhs < 3 || nrhs > 4) mexErrMsgIdAndTxt("gpdla:voigt", "usage: voigt(lambdas, z, N[, num_lines])");
@@ -21,8 +27,10 @@ void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
   const double* lambdas = widen(prhs[0], "lambdas", 0);
   const int64_t n = (int64_t)mxGetNumberOfElements(prhs[0]);
   if (n <= 6) mexErrMsgIdAndTxt("gpdla:voigt", "need more than 6 wavelengths (2 width)");
-  const double z = widen_scalar(prhs[1], "z"), N = widen_scalar(prhs[2], "N");
-  const int32_t num_lines = nrhs > 3 ? (int32_t)widen_scalar(prhs[3], "num_lines") : 31;
+  /* z, N and num_lines are read like voigt.c:263-266 does, with mxGetScalar: any numeric or logical
+   * class, the first element (voigt(lam, z, N, int32(3)) works as with the original) */
+  const double z = ref_scalar(prhs[1], "z"), N = ref_scalar(prhs[2], "N");
+  const int32_t num_lines = nrhs > 3 ? (int32_t)ref_scalar(prhs[3], "num_lines") : 31;
   mxArray* out = mxCreateDoubleMatrix((size_t)(n - 6), 1, mxREAL);
   const int rc = gpdla_voigt_f64(lambdas, n, z, N, num_lines, mxGetDoubles(out));
   widen_release();

@@ -27,6 +27,7 @@ static size_t elsize(mxClassID c) {
   switch (c) {
     case mxDOUBLE_CLASS: case mxINT64_CLASS: case mxUINT64_CLASS: return 8;
     case mxINT32_CLASS: case mxUINT32_CLASS: case mxSINGLE_CLASS: return 4;
+    case mxINT16_CLASS: case mxUINT16_CLASS: return 2;
     default: return 1;
   }
 }
@@ -47,7 +48,24 @@ float* mxGetSingles(const mxArray* a) { return a->cls == mxSINGLE_CLASS ? (float
 uint64_t* mxGetUint64s(const mxArray* a) { return a->cls == mxUINT64_CLASS ? (uint64_t*)a->data : NULL; }
 int32_t* mxGetInt32s(const mxArray* a) { return a->cls == mxINT32_CLASS ? (int32_t*)a->data : NULL; }
 mxLogical* mxGetLogicals(const mxArray* a) { return a->cls == mxLOGICAL_CLASS ? (mxLogical*)a->data : NULL; }
-double mxGetScalar(const mxArray* a) { return (a->cls == mxDOUBLE_CLASS && a->m * a->n > 0) ? *(double*)a->data : 0.0; }
+/* MATLAB's mxGetScalar: the first element of any numeric, logical or char array as a double (0 if
+ * empty); extra elements are ignored */
+double mxGetScalar(const mxArray* a) {
+  if (a->m * a->n == 0 || a->cls == mxCELL_CLASS) return 0.0;
+  switch (a->cls) {
+    case mxDOUBLE_CLASS: return *(const double*)a->data;
+    case mxSINGLE_CLASS: return (double)*(const float*)a->data;
+    case mxINT8_CLASS: return (double)*(const int8_t*)a->data;
+    case mxUINT8_CLASS: case mxLOGICAL_CLASS: case mxCHAR_CLASS: return (double)*(const uint8_t*)a->data;
+    case mxINT16_CLASS: return (double)*(const int16_t*)a->data;
+    case mxUINT16_CLASS: return (double)*(const uint16_t*)a->data;
+    case mxINT32_CLASS: return (double)*(const int32_t*)a->data;
+    case mxUINT32_CLASS: return (double)*(const uint32_t*)a->data;
+    case mxINT64_CLASS: return (double)*(const int64_t*)a->data;
+    case mxUINT64_CLASS: return (double)*(const uint64_t*)a->data;
+    default: return 0.0;
+  }
+}
 size_t mxGetM(const mxArray* a) { return a->m; }
 size_t mxGetN(const mxArray* a) { return a->n; }
 size_t mxGetNumberOfElements(const mxArray* a) { return a->m * a->n; }

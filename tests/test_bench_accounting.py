@@ -53,6 +53,9 @@ def test_profiled_traffic_lookup(bench):
     assert t is not None and t > 0 and t == want[0] and bench.PROFILE_SUMMARY.name in src
     for path, (f, names) in bench.PROFILE_SUMMARY_C5.items():
         tp, srcp = bench.profiled_traffic(128, 100000, 50, path)
+        if not f.exists():          # not profiled on the current tree: no number is claimed
+            assert (tp, srcp) == (None, None)
+            continue
         rows = json.loads(f.read_text())["kernels"]
         # exact names: per-batch kernels whose names contain the GEMM's (convert_gemm_i8_kernel) excluded
         assert tp == sum(e["hbm_bytes_per_launch"] for e in rows if e["kernel"] in names) and tp > 0

@@ -122,3 +122,48 @@ def test_profiled_traffic_matches_exact_kernel_names():
     got, src = bench.profiled_traffic(128, 100000, 50, "panel-GEMM-int8-24")
     assert got == want and "convert" not in src
     assert all(any(e["kernel"] == n for e in d["kernels"]) for n in names)
+
+
+@pytest.mark.timeout(300)
+def test_launcher_refuses_shared_devices():
+    """2 ranks planned against 1 device would share a GPU: refused (non-zero) unless --rehearsal, which
+    labels the layout and is never an N-GPU point."""
+    r = _run_bench("--gpus", "2", "--plan-only", "--plan-devices", "1")
+    assert r.returncode != 0
+    assert "refusing" in r.stderr and "--rehearsal" in r.stderr
+    assert not [ln for ln in r.stdout.splitlines() if ln.strip().startswith("{")]
+    r = _run_bench("--gpus", "2", "--plan-only", "--plan-devices", "1", "--rehearsal")
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.strip()][-1])
+    assert d["rehearsal"] is True and d["distinct_devices"] == 1
+    assert {x["device"] for x in d["ranks"]} == {0}
+    r = _run_bench("--gpus", "2", "--plan-only", "--plan-devices", "2")
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.strip()][-1])
+    assert d["rehearsal"] is False and d["distinct_devices"] == 2
+
+
+def test_assign_device_rule():
+    bench = _bench()
+    assert bench.assign_device(1, 0, 1, False) == (0, None)
+    assert bench.assign_device(8, 5, 8, False) == (5, None)
+    dev, err = bench.assign_device(8, 5, 1, False)
+    assert dev is None and "refusing" in err
+    assert bench.assign_device(8, 5, 2, True) == (1, None)
+    assert bench.assign_device(1, 0, 0, True)[0] is None
+
+
+@pytest.mark.timeout(300)
+def test_torchrun_without_gpus_flag_takes_the_launcher_world():
+    """DESIGN.md section 5's launch (torch.distributed.run --nproc-per-node N bench.py, no --gpus)
+    takes N from WORLD_SIZE instead of failing in every rank."""
+    import subprocess
+    import sys
+    e = dict(os.environ)
+    e.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), str(ROOT / "bench.py"),
+                        "--plan-only"], capture_output=True, text=True, timeout=240, env=e)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.strip().startswith("{")][-1])
+    assert d["n_gpus"] == 2 and d["world_size"] == 2

@@ -22,6 +22,19 @@ MOCK = Path(__file__).parent / "support" / "mex_api"
 DOUBLE, SINGLE, LOGICAL, CHAR, CELL, UINT64, INT32 = 6, 7, 3, 4, 1, 15, 12
 
 
+IN_TREE_LIB = str((Path(L.__file__).parent / "libgpdla.so").resolve())   # what the mocks' rpath names
+
+
+def _mapped_libgpdla() -> set:
+    """Paths of every libgpdla.so mapped into this process (/proc/self/maps)."""
+    out = set()
+    for line in Path("/proc/self/maps").read_text().splitlines():
+        parts = line.split(maxsplit=5)
+        if len(parts) == 6 and Path(parts[5]).name == "libgpdla.so":
+            out.add(str(Path(parts[5]).resolve()))
+    return out
+
+
 class Gateway:
     """One gateway linked with the mock MEX runtime; Python values <-> mxArrays."""
 
@@ -31,6 +44,13 @@ class Gateway:
         if not path.exists():
             pytest.skip(f"{path.name} not built (gp_dla_detection_amd.build.build_mex_mocks)")
         lib = C.CDLL(str(path))
+        # The mock resolves libgpdla through its rpath (the in-tree build); L.load() honours GPDLA_LIB.
+        # A "bitwise equal to the Python engine" check is only meaningful when both are one file.
+        maps = _mapped_libgpdla()
+        assert IN_TREE_LIB in maps, (IN_TREE_LIB, maps)
+        if L.LIB_PATH.resolve() != Path(IN_TREE_LIB):
+            pytest.skip(f"GPDLA_LIB={L.LIB_PATH} is not the in-tree {IN_TREE_LIB} the gateway links: "
+                        "the two would run different builds")
         vp = C.c_void_p
         for fn, res, args in (("mock_numeric", vp, [C.c_int, C.c_size_t, C.c_size_t, vp]),
                               ("mock_string", vp, [C.c_char_p]), ("mock_cell", vp, [C.c_size_t, C.POINTER(vp)]),
@@ -297,3 +317,31 @@ def test_voigt_and_mvn_gateways_single_inputs():
     M = (syn.make_model(k=k)["M"][:n] * 3).astype(np.float32)
     (got,) = Gateway("log_mvnpdf_low_rank_mex")(1, y, mu, M, d)
     assert got[0, 0] == log_mvnpdf_low_rank(*(a.astype(np.float64) for a in (y, mu, M, d)))
+
+
+@pytest.mark.gpu
+def test_voigt_gateway_integer_class_scalars():
+    """voigt.c:263-266 reads z, N and num_lines with mxGetScalar, so voigt(lam, z, N, int32(3)) and a
+    logical or int32 N work with the original; the drop-in reads them the same way."""
+    from gp_dla_detection_amd.engine import voigt
+    lam = np.linspace(3700.0, 3900.0, 406)
+    g = Gateway("voigt_mex")
+    (got,) = g(1, lam, 2.1, 10 ** 20.5, np.array([3], np.int32))
+    np.testing.assert_array_equal(got[:, 0], voigt(lam, 2.1, 10 ** 20.5, 3))
+    (got,) = g(1, lam, np.float32(2.5), np.array([10 ** 9], np.int32), np.array([True]))
+    np.testing.assert_array_equal(got[:, 0], voigt(lam, float(np.float32(2.5)), 1e9, 1))
+
+
+def test_voigt_gateway_scalar_classes_without_device():
+    """CPU: integer-class scalars pass the gateway's argument reading (mxGetScalar, as voigt.c:263-266)
+    and reach the engine, which reports that there is no device; empty or cell scalars are refused."""
+    if L.load().gpdla_device_count() > 0:
+        pytest.skip("a HIP device is present")
+    lam = np.linspace(3700.0, 3900.0, 406)
+    g = Gateway("voigt_mex")
+    with pytest.raises(RuntimeError, match="no HIP device"):
+        g(1, lam, 2.1, 1e20, np.array([3], np.int32))
+    with pytest.raises(RuntimeError, match="num_lines must be a numeric scalar"):
+        g(1, lam, 2.1, 1e20, np.zeros(0))
+    with pytest.raises(RuntimeError, match="z must be a numeric scalar"):
+        g(1, lam, [np.zeros(1)], 1e20)
