@@ -422,21 +422,22 @@ static int run_panel_gemm(gpdla_engine* e, bool i8, int64_t nq, const int64_t* h
       const int32_t sc = (int32_t)std::min<int64_t>(sc_max, e->S + 1 - s0);
       if (i8) {  // int8 Ozaki contraction (gemm_i8.hip): weights digits -> exact GEMM -> Gram, u
         const int64_t ks = i8_gemm_kstride(h_cap[q]);
+        const int nd = i8_spectrum_nd(e->i8_nd, h_cap[q]);  // short spectra: 32-bit digits (internal.h)
         uint8_t* adig = e->d_ai8;
         WeightsI8Args wi{};
         wi.info = e->d_info; wi.q = (int32_t)q;
         wi.srow = e->d_srow + h_sb[q] * 8; wi.lam_pad = e->d_lam + h_lb[q]; wi.kstride = ks;
         wi.offsets = e->d_off; wi.nhi = e->d_nhi; wi.S = e->S; wi.s0 = s0; wi.sc = sc; wi.rows = rows;
-        wi.lines = make_line_args(e->d_lines); wi.nd = e->i8_nd; wi.adig = adig; wi.q1p = q1p; wi.ldp = ldp;
+        wi.lines = make_line_args(e->d_lines); wi.nd = nd; wi.adig = adig; wi.q1p = q1p; wi.ldp = ldp;
         HIP_TRY(launch_weights_i8(wi, st));
         GemmI8Args gi{};
-        gi.info = e->d_info; gi.q = (int32_t)q; gi.k = K; gi.kstride = ks; gi.rows = rows; gi.sc = sc; gi.nd = e->i8_nd;
+        gi.info = e->d_info; gi.q = (int32_t)q; gi.k = K; gi.kstride = ks; gi.rows = rows; gi.sc = sc; gi.nd = nd;
         gi.adig = adig; gi.bdig = e->d_pi8 + h_cb[q];
         gi.ent = e->d_pent + q * 2 * (int64_t)i8_gemm_entries(K); gi.G = G; gi.U = U;
         // the 24-bit path stores the Gram in fp32 (half the GEMM -> LDL^T round trip; adds ~1e-8
         // to its ~2e-7 from fp64, tests/support/emulate_i8.py), in the same workspace
-        gi.G32 = e->i8_nd == 3 ? reinterpret_cast<float*>(G) : nullptr;
-        gi.ks_bound = (int32_t)(((h_cap[q] - 16) / 4 + 15) / 16);  // slot_cap = 4 ceil(lpix / 4) + 16
+        gi.G32 = nd == 3 ? reinterpret_cast<float*>(G) : nullptr;
+        gi.ks_bound = i8_ks_bound(h_cap[q]);  // slot_cap = 4 ceil(lpix / 4) + 16
         TimedLaunch tg{};
         int rc;
         if ((rc = record_start(e, &tg, 3))) return rc;
@@ -468,7 +469,7 @@ static int run_panel_gemm(gpdla_engine* e, bool i8, int64_t nq, const int64_t* h
       LdlArgs da{};
       da.info = e->d_info; da.q = (int32_t)q; da.k = K;
       da.G = G; da.U = U; da.q1p = q1p; da.ldp = ldp;
-      da.G32 = (i8 && e->i8_nd == 3) ? reinterpret_cast<const float*>(G) : nullptr;
+      da.G32 = (i8 && i8_spectrum_nd(e->i8_nd, h_cap[q]) == 3) ? reinterpret_cast<const float*>(G) : nullptr;
       da.S = e->S; da.s0 = s0; da.sc = sc; da.perm = e->d_perm;
       da.sample_ll = o_sll ? o_sll + q * ld : nullptr; da.ll_null = o_null + q; da.status = e->d_status;
       HIP_TRY(launch_ldl_batch(da, st));

@@ -48,6 +48,7 @@ __global__ __launch_bounds__(256) void convert_gemm_i8_kernel(ConvertGemmI8Args 
   const int Ls16 = 16 * ((L + 15) / 16);
   const int64_t sb = a.slot_base[q];
   const int64_t kstride = i8_gemm_kstride(a.slot_cap[q]);
+  const int nd = i8_spectrum_nd(a.nd, a.slot_cap[q]);  // short spectra: 4 planes on the 24-bit path too
   auto value = [&](int t) -> double {
     if (!valid || t >= L) return 0.0;
     const int64_t row = sb + (int64_t)g * Ls + t;
@@ -93,7 +94,7 @@ __global__ __launch_bounds__(256) void convert_gemm_i8_kernel(ConvertGemmI8Args 
     uint8_t* dst = tbase + (int64_t)ks * 4 * 4096 + 16 * ((gr + rsw) & 3);
 #pragma unroll
     for (int j = 0; j < 4; ++j)
-      if (j < (is_u ? 4 : a.nd))  // u entries keep 4 digits (launch_gemm_i8)
+      if (j < (is_u ? 4 : nd))  // u entries keep 4 digits (launch_gemm_i8)
         *reinterpret_cast<uint4*>(dst + j * 4096) = make_uint4(pl[j][0], pl[j][1], pl[j][2], pl[j][3]);
   }
   s_cs[g][le] = colsum;

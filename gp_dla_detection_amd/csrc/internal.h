@@ -317,6 +317,17 @@ __host__ __device__ inline int gram_tile_index(int r, int c, int k) {
   return base2 + L * 4 * w + (L == NT - 1 ? i * w - i * (i - 1) / 2 + (j - i) : i * w + j);
 }
 
+// The 24-bit path's error is absolute, ~2^-24 of the Gram's scale: relative to max(|ll|, 1) it grows
+// where |ll| is small, which short spectra make likely (n = 3: 5.05e-7 against the fp64 panel,
+// profiles/round5/r10b).  Spectra of at most kI8NarrowKs 64-slot K steps (<= 128 pixels) therefore
+// take the 32-bit digits (4 planes, ~1e-9) on that path; they cost next to nothing.  Decided on the
+// slot capacity (host and device agree without a sync): ks_bound = ceil(ceil(lpix / 4) / 16).
+constexpr int kI8NarrowKs = 2;
+__host__ __device__ inline int i8_ks_bound(int64_t slot_cap) { return (int)(((slot_cap - 16) / 4 + 15) / 16); }
+__host__ __device__ inline int i8_spectrum_nd(int nd, int64_t slot_cap) {
+  return (nd == 3 && i8_ks_bound(slot_cap) <= kI8NarrowKs) ? 4 : nd;
+}
+
 __host__ __device__ inline int i8_gemm_entries(int k) {
   return 64 * ((k * (k + 1) / 2 + 63) / 64) + 64 * ((k + 63) / 64);
 }

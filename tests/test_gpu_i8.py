@@ -218,3 +218,28 @@ def test_panel_gemm_i8_edge_cases(path, tol):
         assert np.all(np.isnan(out[key][-1])), (path, key)
     np.testing.assert_array_equal(out["num_pixels"], ref["num_pixels"])
     print(f"{path} edge cases vs fp64:", {kk: _rel_err(out[kk][:-1], ref[kk][:-1]) for kk in KEYS})
+
+
+def test_panel_gemm_i8_24_short_spectra_take_32_bit_digits():
+    """The 24-bit path's error is absolute (~2^-24 of the Gram's scale), so relative to max(|ll|, 1) it
+    is largest where |ll| is small -- short spectra (n = 3: 5.05e-7, profiles/round5/r10b).  Spectra of
+    <= 128 pixels (kI8NarrowKs = 2 K steps, internal.h) take the 32-bit digits on that path: bitwise the
+    panel_gemm_i8 results, in a batch mixed with longer spectra that keep the 24-bit scheme."""
+    model = syn.make_model(k=50, seed=4)
+    samples = syn.make_samples(300)
+    base = syn.make_spectrum(model, 2, z_qso=2.8, n_target=None, mask_fraction=0.0)
+    spectra = []
+    for npx in (2, 64, 128, 129, 400):
+        sl = slice(50, 50 + npx)
+        s = {kk: (v[sl] if isinstance(v, np.ndarray) else v) for kk, v in base.items()}
+        s["pixel_mask"] = np.zeros(npx, dtype=bool)
+        spectra.append(s)
+    packed = syn.pack_spectra(spectra)
+    o32 = _run(model, samples, packed, "panel_gemm_i8")
+    o24 = _run(model, samples, packed, "panel_gemm_i8_24")
+    ref = _run(model, samples, packed, "panel_gemm")
+    short = np.array([n <= 128 for n in (2, 64, 128, 129, 400)])
+    for key in KEYS:
+        np.testing.assert_array_equal(o24[key][short], o32[key][short])
+        assert not np.array_equal(o24[key][~short], o32[key][~short]), key   # 24-bit digits there
+        assert _rel_err(o24[key], ref[key]) < I8_24_TOL, (key, _rel_err(o24[key], ref[key]))

@@ -9,6 +9,7 @@
 #   tests[=<pytest -k expr>]     the -m gpu suite (or the tests matching the expression)
 #   testfile=<path>              one test file (-m gpu)
 #   smoke                        __graft_entry__.smoke()
+#   py=<script>[=<args>]         python <script> <args>            -> <script name>.log
 #   bench=<name>[=<args>]        python bench.py <args>            -> <name>.json
 #   dist=<N>=<name>[=<args>]     torchrun, N ranks sharing the leased GPU -> <name>.json
 #   prof=<name>[=<args>]         tools/profile.sh <tag>_<name> <args> (trace, FETCH, WRITE, SQ)
@@ -50,6 +51,9 @@ for step in "$@"; do
     testfile)
       run 1100 "$O/$(basename "$a" .py).log" python -u -m pytest "$a" -m gpu -v -s --timeout 900 --timeout-method thread
       tail -1 "$O/$(basename "$a" .py).log" ;;
+    py)
+      run 600 "$O/$(basename "$a" .py).log" python "$a" ${b:-}
+      tail -40 "$O/$(basename "$a" .py).log" ;;
     smoke)
       run 300 "$O/smoke.log" python -c "import __graft_entry__ as g; g.smoke()"
       tail -1 "$O/smoke.log" ;;
