@@ -95,6 +95,7 @@ SIGNATURES = {
                                           C.c_double, dp, dp, dp, dp, dp, dp]),
     "gpdla_diag_faddeeva_w": (C.c_int, [C.c_double, C.c_double, dp, dp]),
     "gpdla_diag_line_table_error": (C.c_int, [C.c_int32, dp]),
+    "gpdla_diag_raw_profile3": (C.c_int, [dp, C.c_int64, C.c_double, C.c_double, C.c_int32, dp]),
     "gpdla_device_malloc": (C.c_int, [C.c_int32, C.c_int64, C.POINTER(C.c_void_p)]),
     "gpdla_device_free": (C.c_int, [C.c_int32, C.c_void_p]),
     "gpdla_memcpy_htod": (C.c_int, [C.c_int32, C.c_void_p, C.c_void_p, C.c_int64]),

@@ -1036,6 +1036,30 @@ int gpdla_voigt_batch_f64(const double* lambdas, int64_t n_padded, const double*
   return GPDLA_OK;
 }
 
+int gpdla_diag_raw_profile3(const double* lambdas, int64_t n, double z, double N, int32_t f32, double* out) {
+  if (!lambdas || !out) return set_error(GPDLA_EINVAL, "null argument");
+  if (n < 1) return GPDLA_OK;
+  int rc = check_device(0);
+  if (rc) return rc;
+  double* d_lines = nullptr;
+  if ((rc = lines_on_device(&d_lines))) return rc;
+  int dev = 0;
+  HIP_TRY(hipGetDevice(&dev));
+  StandaloneBufs& sb = standalone_bufs(dev);
+  std::lock_guard<std::mutex> lock(sb.mu);
+  hipError_t err = standalone_reserve(sb, (size_t)n * 16, (size_t)n * 8);
+  if (err != hipSuccess) return set_error(GPDLA_EDEVICE, "raw profile: %s", hipGetErrorString(err));
+  double* d_lam = (double*)sb.buf;
+  double* d_out = d_lam + n;
+  std::memcpy(sb.host, lambdas, (size_t)n * 8);
+  err = hipMemcpyAsync(d_lam, sb.host, (size_t)n * 8, hipMemcpyHostToDevice, sb.stream);
+  if (err == hipSuccess) err = launch_diag_raw_profile(d_lam, n, z, N, f32 ? 1 : 0, make_line_args(d_lines), d_out, sb.stream);
+  if (err == hipSuccess) err = hipMemcpyAsync(out, d_out, (size_t)n * 8, hipMemcpyDeviceToHost, sb.stream);
+  if (err == hipSuccess) err = hipStreamSynchronize(sb.stream);
+  if (err != hipSuccess) return set_error(GPDLA_EDEVICE, "raw profile: %s", hipGetErrorString(err));
+  return GPDLA_OK;
+}
+
 int gpdla_voigt_f64(const double* lambdas, int64_t n_padded, double z, double N, int32_t num_lines,
                     double* out) {
   return gpdla_voigt_batch_f64(lambdas, n_padded, &z, &N, 1, num_lines, out);

@@ -332,6 +332,50 @@ __global__ __launch_bounds__(256) void weights_i8_kernel(WeightsI8Args a, const 
                         threadIdx.x & 63, core_lds, wing_lds, exp_lds);
 }
 
+// --------------------------------------------------------------------------------------------
+// Diagnostic (gpdla_diag_raw_profile3): the weights kernels' raw 3-line profiles exp(-N sum_j
+// lc_j V_j) at given wavelengths, through the SAME device functions and LDS tables as
+// weights_i8_kernel -- the packed-fp32 pair path of the 24-bit panel path (f32 = 1) or the fp64
+// raw_profile3_t3 of the 32-bit one (f32 = 0).  Test infrastructure for the fp32 profile's error
+// against the fp64 one (tests/test_gpu_i8.py); one thread per pair of wavelengths.
+// --------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void diag_raw_profile_kernel(const double* __restrict__ lam, int64_t n, double z,
+                                                               double N, int32_t f32, LineArgs lines,
+                                                               double* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) double tables[3 * kCoreTable + kWingLds + 64];
+  double* core_lds = tables;
+  double* wing_lds = tables + 3 * kCoreTable;
+  double* exp_lds = wing_lds + kWingLds;
+  for (int i = threadIdx.x; i < 3 * kCoreTable; i += 256) core_lds[i] = lines.buf[i];
+  if (threadIdx.x < 64) exp_lds[threadIdx.x] = lines.buf[kLineBufExp2 + threadIdx.x];
+  if (threadIdx.x < 3 * kWingStride) wing_lds[threadIdx.x] = lines.buf[kLineBufWing + threadIdx.x];
+  __syncthreads();
+  const int64_t i0 = 2 * ((int64_t)blockIdx.x * 256 + threadIdx.x);
+  if (i0 >= n) return;
+  const int64_t i1 = i0 + 1 < n ? i0 + 1 : i0;
+  const double zfac = 1.0 / (1 + z);
+  double afac[3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) afac[j] = lines.buf[kLineBufFac + j] * zfac;
+  double v0, v1;
+  if (f32) {
+    float oc[3][kOuterDeg + 1];
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+#pragma unroll
+      for (int m = 0; m <= kOuterDeg; ++m) oc[j][m] = (float)wing_lds[j * kWingStride + kOuterOff + m];
+    const f2v p = raw_profile3_pair_f32(lam[i0], lam[i1], afac, (float)(N * 1.4426950408889634), oc, core_lds,
+                                        wing_lds);
+    v0 = p.x;
+    v1 = p.y;
+  } else {
+    v0 = raw_profile3_t3(lam[i0], afac, N, core_lds, wing_lds, exp_lds);
+    v1 = raw_profile3_t3(lam[i1], afac, N, core_lds, wing_lds, exp_lds);
+  }
+  out[i0] = v0;
+  if (i0 + 1 < n) out[i0 + 1] = v1;
+}
+
 constexpr int kGTileS = 128, kGTileE = 64;
 
 // --------------------------------------------------------------------------------------------
@@ -677,6 +721,188 @@ void gemm_i8_bst_kernel(GemmI8Args a) {
   }
 }
 
+// --------------------------------------------------------------------------------------------
+// B-stationary Gram GEMM, software-pipelined at 2 waves per SIMD (8-wave blocks, 256 VGPRs): the
+// same tiles, MFMAs and per-accumulator order as gemm_i8_bst_kernel (bitwise its results), but each
+// wave walks ALL its sample tiles as one stream of K steps with its A digits loaded TWO steps ahead
+// (three register sets in turn) and every column tile's B operands read from LDS one column tile
+// ahead (two register sets), so neither the L2/HBM latency of A nor the LDS latency of B sits in
+// front of the MFMAs; the next tile's first A loads are in flight during the epilogue.  No inline
+// waits: after the prologue there is no DMA, so the compiler's waitcnt pass counts every load.
+// --------------------------------------------------------------------------------------------
+constexpr int kBst8Waves = 8;
+
+__global__ __launch_bounds__(64 * kBst8Waves, 1) __attribute__((amdgpu_waves_per_eu(2, 2)))
+void gemm_i8_bst8_kernel(GemmI8Args a) {
+  constexpr int ND = 3;
+  constexpr int kStepBytes = ND * kGTileE * 64;  // 12 KiB: one K step of one entry tile, 3 planes
+  constexpr int kTiles = kBst8Waves / 4;         // 128-sample tiles per block round
+  __shared__ __attribute__((aligned(16))) uint8_t Bs[kBstMaxKs * kStepBytes];
+  __shared__ double s_ent[2][kGTileE];           // the block's column scales and offsets (epilogue)
+  const SpecInfo inf = a.info[a.q];
+  if (inf.J == 0) return;
+  const int K = a.k;
+  const int E = K * (K + 1) / 2;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wave_s = __builtin_amdgcn_readfirstlane(wave);
+  const int ny = a.ny, nst = (a.sc + kGTileS - 1) / kGTileS;
+  const int EX = kBstEX, SX = 8 / EX;
+  const int per = gridDim.x / 8;
+  const int x = blockIdx.x % 8;
+  const int ex = x % EX, sx = x / EX;
+  const int e0 = ny * ex / EX, e1 = ny * (ex + 1) / EX;
+  const int s0 = nst * sx / SX, s1 = nst * (sx + 1) / SX;
+  const int nye = e1 - e0;
+  const int G = per / nye;
+  const int j = blockIdx.x / 8;
+  if (nye <= 0 || G <= 0 || j >= nye * G) return;
+  const int e_tile = (a.e_tile0 + e0 + j % nye) * kGTileE;
+  const int gi = j / nye;
+  const int nks = (16 * ((inf.L + 15) / 16)) / 16;
+  if (nks > kBstMaxKs) return;                   // never: the launch checks the bound (LDS safety)
+  const int64_t nksmax = a.kstride / 64;
+  const uint32_t bs_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)&Bs[0];
+  {
+    const uint8_t* B0 = a.bdig + (int64_t)(e_tile >> 6) * nksmax * 4 * 4096;
+    const int npieces = nks * (kStepBytes / 1024);
+    for (int pc = wave_s; pc < npieces; pc += kBst8Waves) {
+      const int ks = pc / (kStepBytes / 1024), w = pc - ks * (kStepBytes / 1024);
+      dma_piece(B0 + (int64_t)ks * 4 * 4096 + w * 1024, (uint32_t)(lane * 16), bs_base + (uint32_t)(pc * 1024));
+    }
+    // the epilogue's per-column scale and offset from LDS: a global load there would make the
+    // waitcnt pass drain the A prefetches in flight at every tile's end
+    if (threadIdx.x < 2 * kGTileE) {
+      const int c = threadIdx.x & (kGTileE - 1), col = e_tile + c;
+      s_ent[threadIdx.x >> 6][c] = col < E ? a.ent[(threadIdx.x >> 6) * i8_gemm_entries(K) + col] : 0.0;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  const int g = lane >> 4;
+  const int wt = wave_s & 3;                     // the wave's 32 rows of its 128-sample tile
+  const int64_t a_lane = ((int64_t)g * 128 + 32 * wt + (lane & 15)) * 16;
+  // this wave's sample tiles: st_i = s0 + kTiles gi + (wave >> 2) + i span, i = 0 .. nt - 1
+  const int span = kTiles * G;
+  const int st0 = s0 + kTiles * gi + (wave_s >> 2);
+  const int nt = st0 < s1 ? (s1 - st0 + span - 1) / span : 0;
+  const int total = nt * nks;                    // the wave's K steps over all its tiles
+  if (total == 0) return;                        // (after the block's only barrier)
+  v4i acc[ND][2][4];
+  auto zero_acc = [&]() {
+#pragma unroll
+    for (int l = 0; l < ND; ++l)
+#pragma unroll
+      for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+        for (int ct = 0; ct < 4; ++ct) acc[l][rt][ct] = (v4i){0, 0, 0, 0};
+  };
+  // global step gs -> (tile i, step ks); the A digits of that step into r.  Issued from inline asm,
+  // invisible to the compiler's waitcnt pass (which, around the guarded steps and the tile-end
+  // stores, merged its queue model conservatively and drained the prefetch two steps ahead); land()
+  // waits for them explicitly and hands the registers over through an empty "+v" asm.
+  auto load_a = [&](int gs, v4i (&r)[2][ND]) {
+    const int i = gs / nks, ks = gs - i * nks;
+    const uint8_t* A0 = a.adig + ((int64_t)(st0 + i * span) * nksmax + ks) * 16 * 2048 + a_lane;
+#pragma unroll
+    for (int p = 0; p < ND; ++p) {
+      const uint8_t* ap = A0 + p * 8192;
+      asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(r[0][p]) : "v"(ap) : "memory");
+      asm volatile("global_load_dwordx4 %0, %1, off offset:256" : "=v"(r[1][p]) : "v"(ap) : "memory");
+    }
+  };
+  // A(g) has landed once at most the 12 newer loads of A(g + 1), A(g + 2) are outstanding (vmcnt is
+  // in order; a tile-end epilogue's 8 stores in between make this wait longer, never too short)
+  auto land = [&](v4i (&r)[2][ND]) {
+    asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+      for (int p = 0; p < ND; ++p) asm volatile("" : "+v"(r[rt][p]));
+  };
+  auto read_b = [&](int ks, int ct, v4i (&Bd)[ND]) {
+    const uint8_t* Bc = Bs + ks * kStepBytes;
+    const int row = 16 * ct + (lane & 15);
+#pragma unroll
+    for (int p = 0; p < ND; ++p)
+      Bd[p] = *reinterpret_cast<const v4i*>(Bc + p * (kGTileE * 64) + row * 64 + 16 * ((g + 2 * ((row >> 2) & 3)) & 3));
+  };
+  auto mfmas = [&](const v4i (&Ar)[2][ND], const v4i (&Bd)[ND], int ct) {
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+      for (int l = 0; l < ND; ++l)
+#pragma unroll
+        for (int i = 0; i <= l; ++i) acc[l][rt][ct] = MFMA_I8(Ar[rt][i], Bd[l - i], acc[l][rt][ct]);
+  };
+  auto epilogue = [&](int s_tile) {
+#pragma unroll
+    for (int ct = 0; ct < 4; ++ct) {
+      const int col = e_tile + 16 * ct + (lane & 15);
+      if (col >= E) continue;
+      const double sc = s_ent[0][16 * ct + (lane & 15)], off0 = s_ent[1][16 * ct + (lane & 15)];
+#pragma unroll
+      for (int rt = 0; rt < 2; ++rt) {
+        const int s4 = s_tile + 32 * wt + 16 * rt + 4 * (lane >> 4);
+        double v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          double val = (double)acc[ND - 1][rt][ct][r] * __builtin_ldexp(1.0, 48 - 8 * (ND - 1));
+#pragma unroll
+          for (int l = ND - 2; l >= 0; --l) val = fma((double)acc[l][rt][ct][r], __builtin_ldexp(1.0, 48 - 8 * l), val);
+          v[r] = (val + off0) * sc;
+        }
+        typedef float f4v __attribute__((ext_vector_type(4)));
+        __builtin_nontemporal_store((f4v){(float)v[0], (float)v[1], (float)v[2], (float)v[3]},
+                                    reinterpret_cast<f4v*>(a.G32 + quad_index(s4, col, E)));
+      }
+    }
+  };
+  // one K step: B of (ks, ct = 0) is in B0 on entry; B of the next step's ct = 0 is in B0 on exit
+  v4i B0[ND], B1[ND];
+  int ks = 0, tile = 0;
+  auto step = [&](v4i (&Ar)[2][ND]) {
+    const int ksn = ks + 1 == nks ? 0 : ks + 1;
+    land(Ar);
+    __builtin_amdgcn_sched_barrier(0);
+    read_b(ks, 1, B1);
+    mfmas(Ar, B0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    read_b(ks, 2, B0);
+    mfmas(Ar, B1, 1);
+    __builtin_amdgcn_sched_barrier(0);
+    read_b(ks, 3, B1);
+    mfmas(Ar, B0, 2);
+    __builtin_amdgcn_sched_barrier(0);
+    read_b(ksn, 0, B0);
+    mfmas(Ar, B1, 3);
+    __builtin_amdgcn_sched_barrier(0);
+    if (ksn == 0) {
+      epilogue((st0 + tile * span) * kGTileS);
+      zero_acc();
+      ++tile;
+    }
+    ks = ksn;
+  };
+  zero_acc();
+  v4i A0r[2][ND], A1r[2][ND], A2r[2][ND];
+  // The prefetches are unconditional (past the last step they reload it, unused), so exactly 12 loads
+  // are newer than the step's own at every land().  The steps are guarded, not broken out of (early
+  // exits from the unrolled body spilled ~70 VGPRs).
+  const int last = total - 1;
+  load_a(0, A0r);
+  load_a(min(1, last), A1r);
+  read_b(0, 0, B0);
+  for (int gs = 0; gs < total; gs += 3) {
+    load_a(min(gs + 2, last), A2r);
+    step(A0r);
+    load_a(min(gs + 3, last), A0r);
+    if (gs + 1 < total) step(A1r);
+    load_a(min(gs + 4, last), A1r);
+    if (gs + 2 < total) step(A2r);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the tail's redundant prefetches
+}
+
 #undef MFMA_I8
 
 }  // namespace
@@ -685,6 +911,14 @@ hipError_t launch_convert_gemm_i8(const ConvertGemmI8Args& a, int32_t q_count, h
   if (a.k < 1 || a.k > kGemmMaxK) return hipErrorInvalidValue;
   hipLaunchKernelGGL(convert_gemm_i8_kernel, dim3((unsigned)(i8_gemm_entries(a.k) / 64), (unsigned)q_count),
                      dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_diag_raw_profile(const double* lam, int64_t n, double z, double N, int32_t f32,
+                                   const LineArgs& lines, double* out, hipStream_t s) {
+  if (n < 1) return hipSuccess;
+  const unsigned blocks = (unsigned)(((n + 1) / 2 + 255) / 256);
+  hipLaunchKernelGGL(diag_raw_profile_kernel, dim3(blocks), dim3(256), 0, s, lam, n, z, N, f32, lines, out);
   return hipGetLastError();
 }
 
@@ -723,7 +957,10 @@ hipError_t launch_gemm_i8(const GemmI8Args& a0, hipStream_t s) {
     a.e_tile0 = 0; a.ny = ng;
     // B-stationary when the spectrum's K steps fit the block's LDS
     if (a0.ks_bound > 0 && a0.ks_bound <= kBstMaxKs && ng >= kBstEX && a0.G32) {
-      hipLaunchKernelGGL(gemm_i8_bst_kernel, dim3((unsigned)ncu), dim3(64 * kBstWaves), 0, s, a);
+      if (GPDLA_BST_PIPE)
+        hipLaunchKernelGGL(gemm_i8_bst8_kernel, dim3((unsigned)ncu), dim3(64 * kBst8Waves), 0, s, a);
+      else
+        hipLaunchKernelGGL(gemm_i8_bst_kernel, dim3((unsigned)ncu), dim3(64 * kBstWaves), 0, s, a);
     } else {
       hipLaunchKernelGGL(gemm_i8_kernel<3>, grid(a.ny, 3), dim3(256), 0, s, a);
     }

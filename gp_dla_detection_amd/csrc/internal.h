@@ -384,6 +384,8 @@ struct GemmI8Args {
 
 hipError_t launch_convert_gemm_i8(const ConvertGemmI8Args& a, int32_t q_count, hipStream_t s);
 hipError_t launch_weights_i8(const WeightsI8Args& a, hipStream_t s);
+hipError_t launch_diag_raw_profile(const double* lam, int64_t n, double z, double N, int32_t f32,
+                                   const LineArgs& lines, double* out, hipStream_t s);
 hipError_t launch_gemm_i8(const GemmI8Args& a, hipStream_t s);
 
 bool i8_supported(int K);

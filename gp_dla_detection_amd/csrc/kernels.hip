@@ -678,22 +678,65 @@ __global__ __launch_bounds__(256, (K <= 20 ? 2 : 1)) void likelihood_kernel(Like
 // ---------------------------------------------------------------------------------------------
 // log-mean-exp over samples, process_qsos.m:202-209
 // ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void reduce_kernel(ReduceArgs a) {
-  __shared__ double s_d4[4];
+// log-mean-exp per spectrum (process_qsos.m:202-209): one 1,024-thread block per spectrum, each
+// thread with kReduceUnroll independent loads in flight per pass (a 256-thread block with one load
+// per iteration was load-latency bound: 0.29 ms for 64 spectra x 10^5 samples, profiles/r9z)
+constexpr int kReduceThreads = 1024, kReduceUnroll = 4;
+
+template <bool kMax>
+__device__ inline double block_reduce_1024(double v, double* lds) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const double o = __shfl_xor(v, off);
+    v = kMax ? fmax(v, o) : v + o;
+  }
+  if (lane == 0) lds[wave] = v;
+  __syncthreads();
+  double r = lds[0];
+#pragma unroll
+  for (int w = 1; w < kReduceThreads / 64; ++w) r = kMax ? fmax(r, lds[w]) : r + lds[w];
+  __syncthreads();
+  return r;
+}
+
+__global__ __launch_bounds__(kReduceThreads) void reduce_kernel(ReduceArgs a) {
+  __shared__ double s_w[kReduceThreads / 64];
   const int q = blockIdx.x;
   const double* ll = a.sample_ll + q * a.ld;
+  const int64_t S = a.S;
+  constexpr int kStride = kReduceThreads * kReduceUnroll;
   double mx = -INFINITY;
   bool nan = false;
-  for (int64_t s = threadIdx.x; s < a.S; s += 256) {
-    const double v = ll[s];
+  int64_t s = threadIdx.x;
+  for (; s + (kReduceUnroll - 1) * kReduceThreads < S; s += kStride) {
+    double v[kReduceUnroll];
+#pragma unroll
+    for (int u = 0; u < kReduceUnroll; ++u) v[u] = ll[s + u * kReduceThreads];
+#pragma unroll
+    for (int u = 0; u < kReduceUnroll; ++u) {
+      nan |= (v[u] != v[u]);
+      mx = fmax(mx, v[u]);
+    }
+  }
+  for (int64_t t = s; t < S; t += kReduceThreads) {
+    const double v = ll[t];
     nan |= (v != v);
     mx = fmax(mx, v);
   }
-  mx = block_reduce_max(mx, s_d4);
+  mx = block_reduce_1024<true>(mx, s_w);
   double sum = 0.0;
-  for (int64_t s = threadIdx.x; s < a.S; s += 256) sum += exp(ll[s] - mx);
-  sum = block_reduce_sum(sum, s_d4);
-  const double anynan = block_reduce_max(nan ? 1.0 : 0.0, s_d4);
+  s = threadIdx.x;
+  for (; s + (kReduceUnroll - 1) * kReduceThreads < S; s += kStride) {
+    double v[kReduceUnroll];
+#pragma unroll
+    for (int u = 0; u < kReduceUnroll; ++u) v[u] = ll[s + u * kReduceThreads];
+#pragma unroll
+    for (int u = 0; u < kReduceUnroll; ++u) sum += exp(v[u] - mx);
+  }
+  for (int64_t t = s; t < S; t += kReduceThreads) sum += exp(ll[t] - mx);
+  sum = block_reduce_1024<false>(sum, s_w);
+  const double anynan = block_reduce_1024<true>(nan ? 1.0 : 0.0, s_w);
   if (threadIdx.x == 0) {
     const SpecInfo inf = a.info[q];
     double r = mx + log(sum / (double)a.S);
@@ -981,7 +1024,7 @@ hipError_t launch_likelihood(int K, const LikelihoodArgs& a, hipStream_t s) {
 }
 
 hipError_t launch_reduce(const ReduceArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(reduce_kernel, dim3(a.q_count), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(reduce_kernel, dim3(a.q_count), dim3(kReduceThreads), 0, s, a);
   return hipGetLastError();
 }
 

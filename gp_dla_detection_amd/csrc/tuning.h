@@ -25,3 +25,9 @@
 #ifndef GPDLA_MAX_CHUNK
 #define GPDLA_MAX_CHUNK 131072
 #endif
+
+// gemm_i8_bst kernel choice (A/B in progress): 0 = 12 waves, A one step ahead; 1 = 8 waves, A two
+// steps ahead and B one column tile ahead
+#ifndef GPDLA_BST_PIPE
+#define GPDLA_BST_PIPE 0
+#endif

@@ -202,6 +202,10 @@ int gpdla_spectrum_loss_f64(const double* y, const double* lya_1pz, const double
 int gpdla_diag_faddeeva_w(double x, double y, double* re, double* im);
 /* Max relative error of the fitted profile table of `line` against its long-double source. */
 int gpdla_diag_line_table_error(int32_t line, double* max_rel_err);
+/* The panel-GEMM weights kernels' raw 3-line absorption exp(-N sum_j lc_j V_j) (before the
+ * instrument broadening) at n wavelengths, on the device: f32 = 1 the 24-bit path's packed-fp32
+ * profile, f32 = 0 the fp64 one (gemm_i8.hip).  GPDLA_EDEVICE without a device. */
+int gpdla_diag_raw_profile3(const double* lambdas, int64_t n, double z, double N, int32_t f32, double* out);
 
 /* Device buffers for callers without a GPU array library (the benchmark, tests, C callers).
  * Callers that already hold device memory (e.g. PyTorch tensors) pass those pointers instead. */

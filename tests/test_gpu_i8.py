@@ -243,3 +243,48 @@ def test_panel_gemm_i8_24_short_spectra_take_32_bit_digits():
         np.testing.assert_array_equal(o24[key][short], o32[key][short])
         assert not np.array_equal(o24[key][~short], o32[key][~short]), key   # 24-bit digits there
         assert _rel_err(o24[key], ref[key]) < I8_24_TOL, (key, _rel_err(o24[key], ref[key]))
+
+
+def _raw_profile(lam, z, N, f32):
+    import ctypes as C
+    lam = np.ascontiguousarray(lam, dtype=np.float64)
+    out = np.empty_like(lam)
+    L.check(L.load().gpdla_diag_raw_profile3(L.ptr(lam), lam.size, z, N, 1 if f32 else 0, L.ptr(out)))
+    return out
+
+
+def test_weights_fp32_raw_profile_against_fp64():
+    """The 24-bit path's packed-fp32 raw profile (gemm_i8.hip raw_profile3_pair_f32: x_j in fp64, T_j
+    from one fp32 reciprocal, the outer wing polynomial on fp32 coefficients, exp2f) against the fp64
+    profile of the 32-bit path and the oracle (scipy's Faddeeva), through the kernels' own device
+    functions (gpdla_diag_raw_profile3), over z, N and velocity sweeps that cross every line's core,
+    inner-wing and outer-wing zones -- densely at the |x| = kOuterX = 32 switch (411 km/s), where the
+    fp32 lanes hand over to the fp64 fix-up (emulate_f32_profile rounds only the results)."""
+    import sys
+    from pathlib import Path
+    sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+    from oracle import gpdla_oracle as O
+    kms = 1e5
+    x32 = 32 * O.SIGMA * np.sqrt(2)          # |x| = 32 in cm/s
+    vels = np.concatenate([np.arange(-3000, 3000, 0.5) * kms,
+                           x32 + np.linspace(-2, 2, 4001) * kms, -x32 + np.linspace(-2, 2, 4001) * kms])
+    worst = {"abs": 0.0, "rel": 0.0, "oracle64": 0.0}
+    for z in (2.2, 3.0, 4.5):
+        for N in (1e19, 10 ** 20.3, 1e21, 1e22):
+            for j in range(3):
+                lam = (O.C_CGS + vels) * O.TRANSITION_WAVELENGTHS[j] * (1 + z) * 1e8 / O.C_CGS
+                a32 = _raw_profile(lam, z, N, True)
+                a64 = _raw_profile(lam, z, N, False)
+                mult = O.C_CGS / (O.TRANSITION_WAVELENGTHS[:3] * (1 + z)) / 1e8
+                tot = sum(O.LEADING_CONSTANTS[i] * O.libcerf_voigt(lam * mult[i] - O.C_CGS, O.SIGMA, O.LORENTZ_GAMMAS[i])
+                          for i in range(3))
+                ref = np.exp(-N * tot)
+                assert np.all(np.isfinite(a32)) and np.all((a32 >= 0) & (a32 <= 1))
+                worst["oracle64"] = max(worst["oracle64"], float(np.max(np.abs(a64 - ref))))
+                worst["abs"] = max(worst["abs"], float(np.max(np.abs(a32 - a64))))
+                big = a64 > 1e-4
+                worst["rel"] = max(worst["rel"], float(np.max(np.abs(a32 - a64)[big] / a64[big])))
+    print("raw profile fp32 vs fp64:", worst)
+    assert worst["oracle64"] < 1e-12, worst          # the fp64 profile is the oracle's to ~1e-15
+    assert worst["abs"] < 1e-6, worst                 # fp32: an absorption in [0, 1] to ~2^-20
+    assert worst["rel"] < 1e-5, worst                 # and relative where it is not negligible

@@ -56,6 +56,8 @@ def test_no_cpu_fallback_without_device():
     out = np.zeros(14)
     rc = lib.gpdla_voigt_f64(L.ptr(lam), 20, 2.0, 1e20, 3, L.ptr(out))
     assert rc == L.GPDLA_EDEVICE
+    raw = np.zeros(20)
+    assert lib.gpdla_diag_raw_profile3(L.ptr(lam), 20, 2.0, 1e20, 1, L.ptr(raw)) == L.GPDLA_EDEVICE
     with pytest.raises(L.GpdlaError):
         L.pci_bus_id(0)
     assert b"no HIP device" in lib.gpdla_last_error()

@@ -18,6 +18,7 @@ VARIANTS: dict = {
     "bst8": {"GPDLA_BST_WAVES": 8},
     "bst_ex2": {"GPDLA_BST_EX": 2},
     "bst_ex8": {"GPDLA_BST_EX": 8},
+    "bst8p": {"GPDLA_BST_PIPE": 1},
 }
 if __name__ == "__main__":
     names = sys.argv[1:] or list(VARIANTS)
