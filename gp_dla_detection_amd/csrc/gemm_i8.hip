@@ -571,172 +571,35 @@ __global__ __launch_bounds__(256, ND == 3 ? 3 : 2) void gemm_i8_kernel(GemmI8Arg
 }
 
 // --------------------------------------------------------------------------------------------
-// B-stationary Gram GEMM (24-bit path, ND = 3): one 12-wave block per CU keeps the WHOLE K range of
+// B-stationary Gram GEMM (24-bit path, ND = 3): one 8-wave block per CU keeps the WHOLE K range of
 // one 64-entry tile's panel digits in LDS (nks x 12 KiB, nks <= kBstMaxKs) and streams sample tiles
 // past it.  gemm_i8_kernel re-reads an entry tile's B digits from L2 for every 128-sample tile (a
 // third of its L2 -> CU bytes); here each block reads them once, and after the prologue there is no
-// barrier at all: each wave walks its own 32 samples x 64 entries, K step by K step, with its A
-// digits prefetched one step ahead into the other of two register sets (same MFMAs, same per-
-// accumulator order, so the int32 sums and the epilogue are bit for bit gemm_i8_kernel<3>'s).
+// barrier at all: each wave walks its own 32 samples x 64 entries of ALL its sample tiles as one
+// stream of K steps (same MFMAs, same per-accumulator order as gemm_i8_kernel<3>: bit for bit its
+// int32 sums and epilogue).  Software pipeline (round 5, +2.3% configs[4] over the round-3/4 kernel
+// of 12 waves with A one step ahead, bitwise equal; profiles/round5/r10e): the A digits are loaded
+// TWO K steps ahead into three register sets in turn (three steps ahead measured equal), every column
+// tile's B operands are read from LDS one column tile ahead (two register sets), the next tile's
+// first A loads are in flight during the epilogue, and the epilogue's column scales come from LDS;
+// 2 waves per SIMD at 203 VGPRs, no spills (the round-4 kernel spilled 52 B per lane).
 // Work: XCD x owns entry tiles x % EX and sample tiles x / EX (EX = 2: each sample tile's A digits
 // are read by the 2 XCDs of its range; EX = 4 / 8 measured -1.3% / -5%, profiles/r5j); its blocks
-// form nye entry-tile columns x G groups (at k = 50: 10 x 3 of an XCD's 32); round r
-// of group gi covers sample tiles s0 + 3 (r G + gi) .. + 2 (one per 4 waves), so all of an XCD's
-// blocks sweep the same 3 G sample tiles together and their A lines stay in its L2.
+// form nye entry-tile columns x G groups (at k = 50: 10 x 3 of an XCD's 32); round r of group gi
+// covers sample tiles s0 + 2 (r G + gi) .. + 1 (one per 4 waves), so all of an XCD's blocks sweep the
+// same 2 G sample tiles together and their A lines stay in its L2.
 // --------------------------------------------------------------------------------------------
-constexpr int kBstWaves = GPDLA_BST_WAVES;
 constexpr int kBstMaxKs = 13;                    // 13 x 12 KiB = 156 KiB of LDS: spectra up to 832 slots
 constexpr int kBstEX = GPDLA_BST_EX;
 
-__global__ __launch_bounds__(64 * kBstWaves, 1) __attribute__((amdgpu_waves_per_eu(kBstWaves / 4, kBstWaves / 4)))
+constexpr int kBstWaves = 8;
+
+__global__ __launch_bounds__(64 * kBstWaves, 1) __attribute__((amdgpu_waves_per_eu(2, 2)))
 void gemm_i8_bst_kernel(GemmI8Args a) {
   constexpr int ND = 3;
+  constexpr int DEPTH = 2;                       // K steps of A digits in flight ahead of the one multiplied
   constexpr int kStepBytes = ND * kGTileE * 64;  // 12 KiB: one K step of one entry tile, 3 planes
-  constexpr int kTiles = kBstWaves / 4;          // 128-sample tiles per block round
-  __shared__ __attribute__((aligned(16))) uint8_t Bs[kBstMaxKs * kStepBytes];
-  const SpecInfo inf = a.info[a.q];
-  if (inf.J == 0) return;
-  const int K = a.k;
-  const int E = K * (K + 1) / 2;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int wave_s = __builtin_amdgcn_readfirstlane(wave);
-  const int ny = a.ny, nst = (a.sc + kGTileS - 1) / kGTileS;
-  const int EX = kBstEX, SX = 8 / EX;
-  const int per = gridDim.x / 8;
-  const int x = blockIdx.x % 8;
-  const int ex = x % EX, sx = x / EX;
-  const int e0 = ny * ex / EX, e1 = ny * (ex + 1) / EX;
-  const int s0 = nst * sx / SX, s1 = nst * (sx + 1) / SX;
-  const int nye = e1 - e0;
-  const int G = per / nye;                       // groups per entry tile (blocks past nye G idle)
-  const int j = blockIdx.x / 8;
-  if (nye <= 0 || G <= 0 || j >= nye * G) return;
-  const int e_tile = (a.e_tile0 + e0 + j % nye) * kGTileE;
-  const int gi = j / nye;
-  const int nks = (16 * ((inf.L + 15) / 16)) / 16;  // 64-slot K steps (<= ks_bound <= kBstMaxKs)
-  if (nks > kBstMaxKs) return;                   // never: the launch checks the bound (LDS safety)
-  const int64_t nksmax = a.kstride / 64;
-  // prologue: the entry tile's B digits for every K step, 1 KiB pieces round-robin over the waves
-  const uint32_t bs_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)&Bs[0];
-  {
-    const uint8_t* B0 = a.bdig + (int64_t)(e_tile >> 6) * nksmax * 4 * 4096;
-    const int npieces = nks * (kStepBytes / 1024);
-    for (int pc = wave_s; pc < npieces; pc += kBstWaves) {
-      const int ks = pc / (kStepBytes / 1024), w = pc - ks * (kStepBytes / 1024);
-      dma_piece(B0 + (int64_t)ks * 4 * 4096 + w * 1024, (uint32_t)(lane * 16), bs_base + (uint32_t)(pc * 1024));
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-  }
-  const int g = lane >> 4;
-  const int wt = wave_s & 3;                     // the wave's 32 rows of its 128-sample tile
-  const int64_t a_lane = ((int64_t)g * 128 + 32 * wt + (lane & 15)) * 16;
-  v4i acc[ND][2][4];
-  auto zero_acc = [&]() {
-#pragma unroll
-    for (int l = 0; l < ND; ++l)
-#pragma unroll
-      for (int rt = 0; rt < 2; ++rt)
-#pragma unroll
-        for (int ct = 0; ct < 4; ++ct) acc[l][rt][ct] = (v4i){0, 0, 0, 0};
-  };
-  auto load_a = [&](const uint8_t* At, int ks, v4i (&r)[2][ND]) {
-    const uint8_t* A0 = At + (int64_t)ks * 16 * 2048 + a_lane;
-#pragma unroll
-    for (int rt = 0; rt < 2; ++rt)
-#pragma unroll
-      for (int p = 0; p < ND; ++p) r[rt][p] = *reinterpret_cast<const v4i*>(A0 + p * 8192 + rt * 256);
-  };
-  auto compute = [&](const v4i (&Ar)[2][ND], int ks) {
-    const uint8_t* Bc = Bs + ks * kStepBytes;
-#pragma unroll
-    for (int ct = 0; ct < 4; ++ct) {
-      const int row = 16 * ct + (lane & 15);
-      v4i Bd[ND];
-#pragma unroll
-      for (int p = 0; p < ND; ++p)
-        Bd[p] = *reinterpret_cast<const v4i*>(Bc + p * (kGTileE * 64) + row * 64 + 16 * ((g + 2 * ((row >> 2) & 3)) & 3));
-#pragma unroll
-      for (int rt = 0; rt < 2; ++rt)
-#pragma unroll
-        for (int l = 0; l < ND; ++l)
-#pragma unroll
-          for (int i = 0; i <= l; ++i) acc[l][rt][ct] = MFMA_I8(Ar[rt][i], Bd[l - i], acc[l][rt][ct]);
-    }
-  };
-  auto epilogue = [&](int s_tile) {
-#pragma unroll
-    for (int ct = 0; ct < 4; ++ct) {
-      const int col = e_tile + 16 * ct + (lane & 15);
-      if (col >= E) continue;
-      const double sc = a.ent[col], off0 = a.ent[i8_gemm_entries(K) + col];
-#pragma unroll
-      for (int rt = 0; rt < 2; ++rt) {
-        const int s4 = s_tile + 32 * wt + 16 * rt + 4 * (lane >> 4);
-        double v[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          double val = (double)acc[ND - 1][rt][ct][r] * __builtin_ldexp(1.0, 48 - 8 * (ND - 1));
-#pragma unroll
-          for (int l = ND - 2; l >= 0; --l) val = fma((double)acc[l][rt][ct][r], __builtin_ldexp(1.0, 48 - 8 * l), val);
-          v[r] = (val + off0) * sc;
-        }
-        typedef float f4v __attribute__((ext_vector_type(4)));
-        __builtin_nontemporal_store((f4v){(float)v[0], (float)v[1], (float)v[2], (float)v[3]},
-                                    reinterpret_cast<f4v*>(a.G32 + quad_index(s4, col, E)));
-      }
-    }
-  };
-  const int span = kTiles * G;                   // sample tiles per round of the XCD's blocks
-  for (int r0 = s0 + kTiles * gi; r0 < s1; r0 += span) {
-    const int st = r0 + (wave_s >> 2);           // this wave's sample tile
-    if (st >= s1) break;                         // wave-uniform (the round's last tiles)
-    const uint8_t* At = a.adig + (int64_t)st * nksmax * 16 * 2048;
-    zero_acc();
-    // two A register sets in turn, the loop unrolled by two (no copies); each step's loads are waited
-    // for after the previous step's MFMAs and handed over through an empty "+v" asm, so the
-    // compiler's waitcnt pass never drains the prefetch in flight (as gemm_i8_kernel's land())
-    v4i A0r[2][ND], A1r[2][ND];
-    auto land = [&](v4i (&Ar)[2][ND]) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-      for (int rt = 0; rt < 2; ++rt)
-#pragma unroll
-        for (int p = 0; p < ND; ++p) asm volatile("" : "+v"(Ar[rt][p]));
-    };
-    load_a(At, 0, A0r);
-    land(A0r);
-    for (int ks = 0; ks < nks; ks += 2) {
-      const bool m1 = ks + 1 < nks, m2 = ks + 2 < nks;
-      if (m1) load_a(At, ks + 1, A1r);
-      __builtin_amdgcn_sched_barrier(0);
-      compute(A0r, ks);
-      land(A1r);
-      if (m2) load_a(At, ks + 2, A0r);
-      __builtin_amdgcn_sched_barrier(0);
-      if (m1) compute(A1r, ks + 1);
-      land(A0r);
-    }
-    epilogue(st * kGTileS);
-  }
-}
-
-// --------------------------------------------------------------------------------------------
-// B-stationary Gram GEMM, software-pipelined at 2 waves per SIMD (8-wave blocks, 256 VGPRs): the
-// same tiles, MFMAs and per-accumulator order as gemm_i8_bst_kernel (bitwise its results), but each
-// wave walks ALL its sample tiles as one stream of K steps with its A digits loaded TWO steps ahead
-// (three register sets in turn) and every column tile's B operands read from LDS one column tile
-// ahead (two register sets), so neither the L2/HBM latency of A nor the LDS latency of B sits in
-// front of the MFMAs; the next tile's first A loads are in flight during the epilogue.  No inline
-// waits: after the prologue there is no DMA, so the compiler's waitcnt pass counts every load.
-// --------------------------------------------------------------------------------------------
-constexpr int kBst8Waves = 8;
-
-__global__ __launch_bounds__(64 * kBst8Waves, 1) __attribute__((amdgpu_waves_per_eu(2, 2)))
-void gemm_i8_bst8_kernel(GemmI8Args a) {
-  constexpr int ND = 3;
-  constexpr int kStepBytes = ND * kGTileE * 64;  // 12 KiB: one K step of one entry tile, 3 planes
-  constexpr int kTiles = kBst8Waves / 4;         // 128-sample tiles per block round
+  constexpr int kTiles = kBstWaves / 4;         // 128-sample tiles per block round
   __shared__ __attribute__((aligned(16))) uint8_t Bs[kBstMaxKs * kStepBytes];
   __shared__ double s_ent[2][kGTileE];           // the block's column scales and offsets (epilogue)
   const SpecInfo inf = a.info[a.q];
@@ -765,7 +628,7 @@ void gemm_i8_bst8_kernel(GemmI8Args a) {
   {
     const uint8_t* B0 = a.bdig + (int64_t)(e_tile >> 6) * nksmax * 4 * 4096;
     const int npieces = nks * (kStepBytes / 1024);
-    for (int pc = wave_s; pc < npieces; pc += kBst8Waves) {
+    for (int pc = wave_s; pc < npieces; pc += kBstWaves) {
       const int ks = pc / (kStepBytes / 1024), w = pc - ks * (kStepBytes / 1024);
       dma_piece(B0 + (int64_t)ks * 4 * 4096 + w * 1024, (uint32_t)(lane * 16), bs_base + (uint32_t)(pc * 1024));
     }
@@ -810,10 +673,10 @@ void gemm_i8_bst8_kernel(GemmI8Args a) {
       asm volatile("global_load_dwordx4 %0, %1, off offset:256" : "=v"(r[1][p]) : "v"(ap) : "memory");
     }
   };
-  // A(g) has landed once at most the 12 newer loads of A(g + 1), A(g + 2) are outstanding (vmcnt is
-  // in order; a tile-end epilogue's 8 stores in between make this wait longer, never too short)
+  // A(g) has landed once at most the 6 DEPTH newer loads of A(g + 1 .. g + DEPTH) are outstanding
+  // (vmcnt is in order; a tile-end epilogue's 8 stores in between make this wait longer, never too short)
   auto land = [&](v4i (&r)[2][ND]) {
-    asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(6 * DEPTH) : "memory");
 #pragma unroll
     for (int rt = 0; rt < 2; ++rt)
 #pragma unroll
@@ -884,21 +747,22 @@ void gemm_i8_bst8_kernel(GemmI8Args a) {
     ks = ksn;
   };
   zero_acc();
-  v4i A0r[2][ND], A1r[2][ND], A2r[2][ND];
-  // The prefetches are unconditional (past the last step they reload it, unused), so exactly 12 loads
+  // DEPTH + 1 A register sets in turn, the loop unrolled by DEPTH + 1 (compile-time set indices).  The
+  // prefetches are unconditional (past the last step they reload it, unused), so exactly 6 DEPTH loads
   // are newer than the step's own at every land().  The steps are guarded, not broken out of (early
   // exits from the unrolled body spilled ~70 VGPRs).
+  constexpr int NS = DEPTH + 1;
+  v4i Ar[NS][2][ND];
   const int last = total - 1;
-  load_a(0, A0r);
-  load_a(min(1, last), A1r);
+#pragma unroll
+  for (int u = 0; u < DEPTH; ++u) load_a(min(u, last), Ar[u]);
   read_b(0, 0, B0);
-  for (int gs = 0; gs < total; gs += 3) {
-    load_a(min(gs + 2, last), A2r);
-    step(A0r);
-    load_a(min(gs + 3, last), A0r);
-    if (gs + 1 < total) step(A1r);
-    load_a(min(gs + 4, last), A1r);
-    if (gs + 2 < total) step(A2r);
+  for (int gs = 0; gs < total; gs += NS) {
+#pragma unroll
+    for (int u = 0; u < NS; ++u) {
+      load_a(min(gs + u + DEPTH, last), Ar[(u + DEPTH) % NS]);
+      if (u == 0 || gs + u < total) step(Ar[u]);
+    }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the tail's redundant prefetches
 }
@@ -957,10 +821,7 @@ hipError_t launch_gemm_i8(const GemmI8Args& a0, hipStream_t s) {
     a.e_tile0 = 0; a.ny = ng;
     // B-stationary when the spectrum's K steps fit the block's LDS
     if (a0.ks_bound > 0 && a0.ks_bound <= kBstMaxKs && ng >= kBstEX && a0.G32) {
-      if (GPDLA_BST_PIPE)
-        hipLaunchKernelGGL(gemm_i8_bst8_kernel, dim3((unsigned)ncu), dim3(64 * kBst8Waves), 0, s, a);
-      else
-        hipLaunchKernelGGL(gemm_i8_bst_kernel, dim3((unsigned)ncu), dim3(64 * kBstWaves), 0, s, a);
+      hipLaunchKernelGGL(gemm_i8_bst_kernel, dim3((unsigned)ncu), dim3(64 * kBstWaves), 0, s, a);
     } else {
       hipLaunchKernelGGL(gemm_i8_kernel<3>, grid(a.ny, 3), dim3(256), 0, s, a);
     }

@@ -11,11 +11,6 @@
 #define GPDLA_F64_WAVES 4
 #endif
 
-// gemm_i8_bst_kernel (24-bit Gram GEMM): waves per B-stationary block (8 measured -2%, profiles/r7*)
-#ifndef GPDLA_BST_WAVES
-#define GPDLA_BST_WAVES 12
-#endif
-
 // gemm_i8_bst_kernel: XCDs sharing a sample tile's A digits (4 / 8 measured -1.3% / -5%, profiles/r5j)
 #ifndef GPDLA_BST_EX
 #define GPDLA_BST_EX 2
@@ -26,8 +21,3 @@
 #define GPDLA_MAX_CHUNK 131072
 #endif
 
-// gemm_i8_bst kernel choice (A/B in progress): 0 = 12 waves, A one step ahead; 1 = 8 waves, A two
-// steps ahead and B one column tile ahead
-#ifndef GPDLA_BST_PIPE
-#define GPDLA_BST_PIPE 0
-#endif

@@ -15,10 +15,8 @@ VARIANTS: dict = {
     "ch50k": {"GPDLA_MAX_CHUNK": 50001},
     "ch25k": {"GPDLA_MAX_CHUNK": 25001},
     "ch16k": {"GPDLA_MAX_CHUNK": 16667},
-    "bst8": {"GPDLA_BST_WAVES": 8},
     "bst_ex2": {"GPDLA_BST_EX": 2},
     "bst_ex8": {"GPDLA_BST_EX": 8},
-    "bst8p": {"GPDLA_BST_PIPE": 1},
 }
 if __name__ == "__main__":
     names = sys.argv[1:] or list(VARIANTS)

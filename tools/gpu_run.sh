@@ -13,6 +13,7 @@
 #   bench=<name>[=<args>]        python bench.py <args>            -> <name>.json
 #   dist=<N>=<name>[=<args>]     torchrun, N ranks sharing the leased GPU -> <name>.json
 #   prof=<name>[=<args>]         tools/profile.sh <tag>_<name> <args> (trace, FETCH, WRITE, SQ)
+#   stall=<name>[=<args>]        tools/profile_stalls.sh <tag>_<name> <args> (issue / wait / MFMA-busy counters)
 #   lib=<variant.so>             GPDLA_LIB for the following steps (A/B variants; "head" = in-tree)
 #   ab=<reps>=<v1,v2,..>[=<args>]  interleaved bench A/B over tools/variants/<v>.so (head = in-tree)
 set -uo pipefail
@@ -68,6 +69,9 @@ for step in "$@"; do
     prof)
       run 1100 "$O/prof_$a.log" bash tools/profile.sh "${TAG}_$a" ${b:-}
       tail -1 "$O/prof_$a.log" ;;
+    stall)
+      run 1100 "$O/stall_$a.log" bash tools/profile_stalls.sh "${TAG}_$a" ${b:-}
+      tail -1 "$O/stall_$a.log" ;;
     lib)
       if [ "$a" = head ]; then unset GPDLA_LIB; else export GPDLA_LIB=$PWD/$a; fi ;;
     ab)
