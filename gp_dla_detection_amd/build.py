@@ -17,8 +17,9 @@ OBJ_DIR = PKG.parent / "build" / "obj"
 
 
 def build(verbose: bool = False, force: bool = False, out: Path | None = None,
-          defines: dict | None = None, jobs: int | None = None) -> Path:
-    """Compile libgpdla.so (or a variant with -D``defines`` into ``out``, for A/B experiments).
+          defines: dict | None = None, jobs: int | None = None, define_only: set | None = None) -> Path:
+    """Compile libgpdla.so (or a variant with -D``defines`` into ``out``, for A/B experiments;
+    ``define_only`` limits the defines to those source files, the others come from the product build).
 
     Each translation unit is compiled to its own object in parallel (no cross-TU device code: every
     kernel is launched from the file that defines it), then linked; objects are reused while they
@@ -44,11 +45,19 @@ def build(verbose: bool = False, force: bool = False, out: Path | None = None,
     hdr_mtime = max(h.stat().st_mtime for h in headers)
     tmp_tag = f".{os.getpid()}.tmp"      # per-process temporaries: concurrent builds never share one
 
+    base_flags = [f for f in cflags if f not in dflags]
+    base_key = "\n".join([str(hipcc_path), str(hipcc_path.stat().st_mtime if hipcc_path.exists() else 0),
+                          " ".join(base_flags), str(Path(__file__).stat().st_mtime)])
+    base_dir = OBJ_DIR / hashlib.sha1(base_key.encode()).hexdigest()[:16]
+
     def compile_one(src: Path) -> Path:
-        obj = objdir / (src.name + ".o")
-        if not force and obj.exists() and obj.stat().st_mtime >= max(src.stat().st_mtime, hdr_mtime):
+        plain = define_only is not None and src.name not in define_only
+        odir, flags = (base_dir, base_flags) if plain else (objdir, cflags)
+        odir.mkdir(parents=True, exist_ok=True)
+        obj = odir / (src.name + ".o")
+        if not (force and not plain) and obj.exists() and obj.stat().st_mtime >= max(src.stat().st_mtime, hdr_mtime):
             return obj
-        cmd = [hipcc, *cflags, "-o", str(obj) + tmp_tag, str(src)]
+        cmd = [hipcc, *flags, "-o", str(obj) + tmp_tag, str(src)]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         subprocess.run(cmd, check=True, cwd=CSRC)

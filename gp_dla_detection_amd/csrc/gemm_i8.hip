@@ -593,21 +593,199 @@ constexpr int kBstMaxKs = 13;                    // 13 x 12 KiB = 156 KiB of LDS
 constexpr int kBstEX = GPDLA_BST_EX;
 
 constexpr int kBstWaves = 8;
+constexpr int kBstLds = kBstMaxKs * 3 * kGTileE * 64;  // the Gram role's B image (the u role uses 2/3)
+constexpr float kBstUSpare = GPDLA_BST_USPARE;           // share of the u tiles the spare blocks take
 
-__global__ __launch_bounds__(64 * kBstWaves, 1) __attribute__((amdgpu_waves_per_eu(2, 2)))
-void gemm_i8_bst_kernel(GemmI8Args a) {
-  constexpr int ND = 3;
+// One role of the B-stationary launch.  A unit is W = 16 NCT consecutive entries starting at global
+// entry ebase, whose B digits (ND planes, the whole K range) sit in Bs; the block's waves walk the
+// sample tiles s_lo + kTiles (gi + r G) + (wave >> 2), r = 0, 1, ... below s_hi.
+//   (ND, NCT) = (3, 4): a Gram entry tile, 6 digit pairs (levels <= 2), fp32 Gram out;
+//   (ND, NCT) = (4, 2): half of the u entry tile, 10 digit pairs (levels <= 3), fp64 u out.
+template <int ND, int NCT>
+__device__ inline void bst_run(const GemmI8Args& a, const SpecInfo& inf, uint8_t* Bs, double (*s_ent)[kGTileE],
+                               int ebase, int s_lo, int s_hi, int gi, int G) {
+  constexpr int W = 16 * NCT;
+  constexpr bool kU = ND == 4;
   constexpr int DEPTH = 2;                       // K steps of A digits in flight ahead of the one multiplied
-  constexpr int kStepBytes = ND * kGTileE * 64;  // 12 KiB: one K step of one entry tile, 3 planes
-  constexpr int kTiles = kBstWaves / 4;         // 128-sample tiles per block round
-  __shared__ __attribute__((aligned(16))) uint8_t Bs[kBstMaxKs * kStepBytes];
-  __shared__ double s_ent[2][kGTileE];           // the block's column scales and offsets (epilogue)
-  const SpecInfo inf = a.info[a.q];
-  if (inf.J == 0) return;
+  constexpr int kStepBytes = ND * W * 64;        // one K step of the unit: ND planes x W rows x 64 B
+  constexpr int kTiles = kBstWaves / 4;          // 128-sample tiles per block round
   const int K = a.k;
   const int E = K * (K + 1) / 2;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int wave_s = __builtin_amdgcn_readfirstlane(wave);
+  const int Ep = 64 * ((E + 63) / 64);
+  const int NE = i8_gemm_entries(K);
+  const int lane = threadIdx.x & 63;
+  const int wave_s = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int nks = (16 * ((inf.L + 15) / 16)) / 16;
+  const int64_t nksmax = a.kstride / 64;
+  const uint32_t bs_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)Bs;
+  auto valid_entry = [&](int e) { return kU ? e - Ep < K : e < E; };
+  {
+    // the unit's B digits for every K step: 1 KiB pieces (16 rows x 64 B of one plane), round-robin
+    // over the waves; the global image is [entry tile][K step][plane 4][row 64][64 B]
+    const uint8_t* B0 = a.bdig + (int64_t)(ebase >> 6) * nksmax * 4 * 4096 + (int64_t)(ebase & 63) * 64;
+    const int npieces = nks * (kStepBytes / 1024);
+    for (int pc = wave_s; pc < npieces; pc += kBstWaves) {
+      const int ks = pc / (kStepBytes / 1024), w = pc - ks * (kStepBytes / 1024);
+      const int p = w / NCT, sub = w - p * NCT;
+      dma_piece(B0 + (int64_t)ks * 4 * 4096 + p * 4096 + sub * 1024, (uint32_t)(lane * 16),
+                bs_base + (uint32_t)(pc * 1024));
+    }
+    // the epilogue's per-entry scale and offset from LDS: a global load there would make the waitcnt
+    // pass drain the A prefetches in flight at every tile's end
+    if (threadIdx.x < 2 * W) {
+      const int c = threadIdx.x % W, kind = threadIdx.x / W, e = ebase + c;
+      s_ent[kind][c] = valid_entry(e) ? a.ent[kind * NE + e] : 0.0;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  const int g = lane >> 4;
+  const int wt = wave_s & 3;                     // the wave's 32 rows of its 128-sample tile
+  const int64_t a_lane = ((int64_t)g * 128 + 32 * wt + (lane & 15)) * 16;
+  const uint8_t* adig = a.adig + (kU ? a.rows * a.kstride * 4 : 0);  // [type (Gram, u)][...]
+  // this wave's sample tiles: st_i = st0 + i span, i = 0 .. nt - 1
+  const int span = kTiles * G;
+  const int st0 = s_lo + kTiles * gi + (wave_s >> 2);
+  const int nt = st0 < s_hi ? (s_hi - st0 + span - 1) / span : 0;
+  const int total = nt * nks;                    // the wave's K steps over all its tiles
+  if (total == 0) return;                        // (after the block's only barrier)
+  const int last = total - 1;
+  v4i acc[ND][2][NCT];
+  auto zero_acc = [&]() {
+#pragma unroll
+    for (int l = 0; l < ND; ++l)
+#pragma unroll
+      for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+        for (int ct = 0; ct < NCT; ++ct) acc[l][rt][ct] = (v4i){0, 0, 0, 0};
+  };
+  // global step gs -> (tile i, step ks); the A digits of that step into r.  Issued from inline asm,
+  // invisible to the compiler's waitcnt pass (which, around the guarded steps and the tile-end
+  // stores, merged its queue model conservatively and drained the prefetch two steps ahead); land()
+  // waits for them explicitly and hands the registers over through an empty "+v" asm.
+  auto load_a = [&](int gs, v4i (&r)[2][ND]) {
+    const int i = gs / nks, ks = gs - i * nks;
+    const uint8_t* A0 = adig + ((int64_t)(st0 + i * span) * nksmax + ks) * 16 * 2048 + a_lane;
+#pragma unroll
+    for (int p = 0; p < ND; ++p) {
+      const uint8_t* ap = A0 + p * 8192;
+      asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(r[0][p]) : "v"(ap) : "memory");
+      asm volatile("global_load_dwordx4 %0, %1, off offset:256" : "=v"(r[1][p]) : "v"(ap) : "memory");
+    }
+  };
+  // A(g) has landed once at most the 2 ND min(DEPTH, last - g) newer loads of A(g + 1 .. g + DEPTH)
+  // are outstanding (vmcnt is in order; a tile-end epilogue's stores in between make this wait longer,
+  // never too short).  Prefetches past the wave's last step are not issued: a load whose value is
+  // never read leaves its registers free for the compiler while the hardware may still write them.
+  auto land = [&](int g, v4i (&r)[2][ND]) {
+    static_assert(DEPTH == 2, "land() spells out the waits for DEPTH = 2");
+    if (last - g >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * ND * 2) : "memory");
+    else if (last - g == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * ND) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+      for (int p = 0; p < ND; ++p) asm volatile("" : "+v"(r[rt][p]));
+  };
+  // B operands of column tile ct (rows 16 ct .. + 15 of the unit): K granule g of a row sits in 16-B
+  // slot (g + 2 ((row >> 2) & 3)) & 3 of its 64 B (convert_gemm_i8_kernel's swizzle; a unit starts at
+  // a multiple of 32 rows of its entry tile, so the local row gives the same slot)
+  auto read_b = [&](int ks, int ct, v4i (&Bd)[ND]) {
+    const uint8_t* Bc = Bs + ks * kStepBytes;
+    const int row = 16 * ct + (lane & 15);
+#pragma unroll
+    for (int p = 0; p < ND; ++p)
+      Bd[p] = *reinterpret_cast<const v4i*>(Bc + p * (W * 64) + row * 64 + 16 * ((g + 2 * ((row >> 2) & 3)) & 3));
+  };
+  auto mfmas = [&](const v4i (&Ar)[2][ND], const v4i (&Bd)[ND], int ct) {
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+      for (int l = 0; l < ND; ++l)
+#pragma unroll
+        for (int i = 0; i <= l; ++i) acc[l][rt][ct] = MFMA_I8(Ar[rt][i], Bd[l - i], acc[l][rt][ct]);
+  };
+  // D lane map of 16x16x64: sample 4 (lane >> 4) + r, entry lane & 15
+  auto epilogue = [&](int s_tile) {
+#pragma unroll
+    for (int ct = 0; ct < NCT; ++ct) {
+      const int c = 16 * ct + (lane & 15), e = ebase + c;
+      if (!valid_entry(e)) continue;
+      const double sc = s_ent[0][c], off0 = s_ent[1][c];
+#pragma unroll
+      for (int rt = 0; rt < 2; ++rt) {
+        const int s4 = s_tile + 32 * wt + 16 * rt + 4 * (lane >> 4);
+        double v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          // sum_l 2^(48 - 8 l) C_l, least significant level first
+          double val = (double)acc[ND - 1][rt][ct][r] * __builtin_ldexp(1.0, 48 - 8 * (ND - 1));
+#pragma unroll
+          for (int l = ND - 2; l >= 0; --l) val = fma((double)acc[l][rt][ct][r], __builtin_ldexp(1.0, 48 - 8 * l), val);
+          v[r] = (val + off0) * sc;
+        }
+        if constexpr (kU) {
+          double2* d = reinterpret_cast<double2*>(a.U + quad_index(s4, e - Ep, K));
+          d[0] = make_double2(v[0], v[1]);
+          d[1] = make_double2(v[2], v[3]);
+        } else {
+          typedef float f4v __attribute__((ext_vector_type(4)));
+          __builtin_nontemporal_store((f4v){(float)v[0], (float)v[1], (float)v[2], (float)v[3]},
+                                      reinterpret_cast<f4v*>(a.G32 + quad_index(s4, e, E)));
+        }
+      }
+    }
+  };
+  // one K step: B of (ks, ct = 0) is in Bb[0] on entry, B of the next step's ct = 0 in Bb[0] on exit
+  // (NCT is even, so the two register sets alternate in step)
+  v4i Bb[2][ND];
+  int ks = 0, tile = 0;
+  auto step = [&](int g, v4i (&Ar)[2][ND]) {
+    const int ksn = ks + 1 == nks ? 0 : ks + 1;
+    land(g, Ar);
+#pragma unroll
+    for (int ct = 0; ct < NCT; ++ct) {
+      __builtin_amdgcn_sched_barrier(0);
+      if (ct + 1 < NCT) read_b(ks, ct + 1, Bb[(ct + 1) & 1]);
+      else read_b(ksn, 0, Bb[0]);
+      mfmas(Ar, Bb[ct & 1], ct);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if (ksn == 0) {
+      epilogue((st0 + tile * span) * kGTileS);
+      zero_acc();
+      ++tile;
+    }
+    ks = ksn;
+  };
+  zero_acc();
+  // DEPTH + 1 A register sets in turn, the loop unrolled by DEPTH + 1 (compile-time set indices), each
+  // step guarded rather than broken out of (early exits from the unrolled body spilled ~70 VGPRs).
+  constexpr int NS = DEPTH + 1;
+  v4i Ar[NS][2][ND];
+#pragma unroll
+  for (int u = 0; u < DEPTH; ++u)
+    if (u <= last) load_a(u, Ar[u]);
+  read_b(0, 0, Bb[0]);
+  for (int gs = 0; gs < total; gs += NS) {
+#pragma unroll
+    for (int u = 0; u < NS; ++u) {
+      if (gs + u + DEPTH <= last) load_a(gs + u + DEPTH, Ar[(u + DEPTH) % NS]);
+      if (u == 0 || gs + u < total) step(gs + u, Ar[u]);
+    }
+  }
+}
+
+// The launch: per XCD, nye entry-tile columns x G groups of Gram blocks; when the u tile is fused
+// (a.u_tile >= 0), the XCD's two spare blocks (32 - nye G = 2 at k = 50) take the two halves of the
+// u tile over the XCD's share of its sample range (the two XCDs of a sample range split it), so the
+// u contraction runs beside the Gram's instead of as a launch of its own.
+__global__ __launch_bounds__(64 * kBstWaves, 1) __attribute__((amdgpu_waves_per_eu(2, 2)))
+void gemm_i8_bst_kernel(GemmI8Args a) {
+  __shared__ __attribute__((aligned(16))) uint8_t Bs[kBstLds];
+  __shared__ double s_ent[2][kGTileE];
+  const SpecInfo inf = a.info[a.q];
+  if (inf.J == 0) return;
   const int ny = a.ny, nst = (a.sc + kGTileS - 1) / kGTileS;
   const int EX = kBstEX, SX = 8 / EX;
   const int per = gridDim.x / 8;
@@ -618,153 +796,25 @@ void gemm_i8_bst_kernel(GemmI8Args a) {
   const int nye = e1 - e0;
   const int G = per / nye;
   const int j = blockIdx.x / 8;
-  if (nye <= 0 || G <= 0 || j >= nye * G) return;
-  const int e_tile = (a.e_tile0 + e0 + j % nye) * kGTileE;
-  const int gi = j / nye;
+  if (nye <= 0 || G <= 0) return;
   const int nks = (16 * ((inf.L + 15) / 16)) / 16;
   if (nks > kBstMaxKs) return;                   // never: the launch checks the bound (LDS safety)
-  const int64_t nksmax = a.kstride / 64;
-  const uint32_t bs_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)&Bs[0];
-  {
-    const uint8_t* B0 = a.bdig + (int64_t)(e_tile >> 6) * nksmax * 4 * 4096;
-    const int npieces = nks * (kStepBytes / 1024);
-    for (int pc = wave_s; pc < npieces; pc += kBstWaves) {
-      const int ks = pc / (kStepBytes / 1024), w = pc - ks * (kStepBytes / 1024);
-      dma_piece(B0 + (int64_t)ks * 4 * 4096 + w * 1024, (uint32_t)(lane * 16), bs_base + (uint32_t)(pc * 1024));
+  // the u work of this XCD: both halves of the u tile over its share [lo, hi) of the sample range; a
+  // spare block per half takes the first ~kBstUSpare of the tiles (it starts at once), the Gram
+  // blocks split the rest per half once their Gram columns are done
+  const int lo = s0 + (s1 - s0) * ex / EX, hi = s0 + (s1 - s0) * (ex + 1) / EX;
+  const int mid = lo + (int)((hi - lo) * kBstUSpare + 0.5f);
+  if (j < nye * G) {
+    bst_run<3, 4>(a, inf, Bs, s_ent, (a.e_tile0 + e0 + j % nye) * kGTileE, s0, s1, j / nye, G);
+    if (a.u_tile >= 0 && nye * G >= 2) {
+      __syncthreads();                           // every wave is done with the Gram B image
+      const int half = j & 1, ngb = nye * G / 2;
+      if (j / 2 < ngb) bst_run<4, 2>(a, inf, Bs, s_ent, a.u_tile * kGTileE + 32 * half, mid, hi, j / 2, ngb);
     }
-    // the epilogue's per-column scale and offset from LDS: a global load there would make the
-    // waitcnt pass drain the A prefetches in flight at every tile's end
-    if (threadIdx.x < 2 * kGTileE) {
-      const int c = threadIdx.x & (kGTileE - 1), col = e_tile + c;
-      s_ent[threadIdx.x >> 6][c] = col < E ? a.ent[(threadIdx.x >> 6) * i8_gemm_entries(K) + col] : 0.0;
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+  } else if (a.u_tile >= 0 && j < nye * G + 2) {
+    const int half = j - nye * G;
+    bst_run<4, 2>(a, inf, Bs, s_ent, a.u_tile * kGTileE + 32 * half, lo, mid, 0, 1);
   }
-  const int g = lane >> 4;
-  const int wt = wave_s & 3;                     // the wave's 32 rows of its 128-sample tile
-  const int64_t a_lane = ((int64_t)g * 128 + 32 * wt + (lane & 15)) * 16;
-  // this wave's sample tiles: st_i = s0 + kTiles gi + (wave >> 2) + i span, i = 0 .. nt - 1
-  const int span = kTiles * G;
-  const int st0 = s0 + kTiles * gi + (wave_s >> 2);
-  const int nt = st0 < s1 ? (s1 - st0 + span - 1) / span : 0;
-  const int total = nt * nks;                    // the wave's K steps over all its tiles
-  if (total == 0) return;                        // (after the block's only barrier)
-  v4i acc[ND][2][4];
-  auto zero_acc = [&]() {
-#pragma unroll
-    for (int l = 0; l < ND; ++l)
-#pragma unroll
-      for (int rt = 0; rt < 2; ++rt)
-#pragma unroll
-        for (int ct = 0; ct < 4; ++ct) acc[l][rt][ct] = (v4i){0, 0, 0, 0};
-  };
-  // global step gs -> (tile i, step ks); the A digits of that step into r.  Issued from inline asm,
-  // invisible to the compiler's waitcnt pass (which, around the guarded steps and the tile-end
-  // stores, merged its queue model conservatively and drained the prefetch two steps ahead); land()
-  // waits for them explicitly and hands the registers over through an empty "+v" asm.
-  auto load_a = [&](int gs, v4i (&r)[2][ND]) {
-    const int i = gs / nks, ks = gs - i * nks;
-    const uint8_t* A0 = a.adig + ((int64_t)(st0 + i * span) * nksmax + ks) * 16 * 2048 + a_lane;
-#pragma unroll
-    for (int p = 0; p < ND; ++p) {
-      const uint8_t* ap = A0 + p * 8192;
-      asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(r[0][p]) : "v"(ap) : "memory");
-      asm volatile("global_load_dwordx4 %0, %1, off offset:256" : "=v"(r[1][p]) : "v"(ap) : "memory");
-    }
-  };
-  // A(g) has landed once at most the 6 DEPTH newer loads of A(g + 1 .. g + DEPTH) are outstanding
-  // (vmcnt is in order; a tile-end epilogue's 8 stores in between make this wait longer, never too short)
-  auto land = [&](v4i (&r)[2][ND]) {
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(6 * DEPTH) : "memory");
-#pragma unroll
-    for (int rt = 0; rt < 2; ++rt)
-#pragma unroll
-      for (int p = 0; p < ND; ++p) asm volatile("" : "+v"(r[rt][p]));
-  };
-  auto read_b = [&](int ks, int ct, v4i (&Bd)[ND]) {
-    const uint8_t* Bc = Bs + ks * kStepBytes;
-    const int row = 16 * ct + (lane & 15);
-#pragma unroll
-    for (int p = 0; p < ND; ++p)
-      Bd[p] = *reinterpret_cast<const v4i*>(Bc + p * (kGTileE * 64) + row * 64 + 16 * ((g + 2 * ((row >> 2) & 3)) & 3));
-  };
-  auto mfmas = [&](const v4i (&Ar)[2][ND], const v4i (&Bd)[ND], int ct) {
-#pragma unroll
-    for (int rt = 0; rt < 2; ++rt)
-#pragma unroll
-      for (int l = 0; l < ND; ++l)
-#pragma unroll
-        for (int i = 0; i <= l; ++i) acc[l][rt][ct] = MFMA_I8(Ar[rt][i], Bd[l - i], acc[l][rt][ct]);
-  };
-  auto epilogue = [&](int s_tile) {
-#pragma unroll
-    for (int ct = 0; ct < 4; ++ct) {
-      const int col = e_tile + 16 * ct + (lane & 15);
-      if (col >= E) continue;
-      const double sc = s_ent[0][16 * ct + (lane & 15)], off0 = s_ent[1][16 * ct + (lane & 15)];
-#pragma unroll
-      for (int rt = 0; rt < 2; ++rt) {
-        const int s4 = s_tile + 32 * wt + 16 * rt + 4 * (lane >> 4);
-        double v[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          double val = (double)acc[ND - 1][rt][ct][r] * __builtin_ldexp(1.0, 48 - 8 * (ND - 1));
-#pragma unroll
-          for (int l = ND - 2; l >= 0; --l) val = fma((double)acc[l][rt][ct][r], __builtin_ldexp(1.0, 48 - 8 * l), val);
-          v[r] = (val + off0) * sc;
-        }
-        typedef float f4v __attribute__((ext_vector_type(4)));
-        __builtin_nontemporal_store((f4v){(float)v[0], (float)v[1], (float)v[2], (float)v[3]},
-                                    reinterpret_cast<f4v*>(a.G32 + quad_index(s4, col, E)));
-      }
-    }
-  };
-  // one K step: B of (ks, ct = 0) is in B0 on entry; B of the next step's ct = 0 is in B0 on exit
-  v4i B0[ND], B1[ND];
-  int ks = 0, tile = 0;
-  auto step = [&](v4i (&Ar)[2][ND]) {
-    const int ksn = ks + 1 == nks ? 0 : ks + 1;
-    land(Ar);
-    __builtin_amdgcn_sched_barrier(0);
-    read_b(ks, 1, B1);
-    mfmas(Ar, B0, 0);
-    __builtin_amdgcn_sched_barrier(0);
-    read_b(ks, 2, B0);
-    mfmas(Ar, B1, 1);
-    __builtin_amdgcn_sched_barrier(0);
-    read_b(ks, 3, B1);
-    mfmas(Ar, B0, 2);
-    __builtin_amdgcn_sched_barrier(0);
-    read_b(ksn, 0, B0);
-    mfmas(Ar, B1, 3);
-    __builtin_amdgcn_sched_barrier(0);
-    if (ksn == 0) {
-      epilogue((st0 + tile * span) * kGTileS);
-      zero_acc();
-      ++tile;
-    }
-    ks = ksn;
-  };
-  zero_acc();
-  // DEPTH + 1 A register sets in turn, the loop unrolled by DEPTH + 1 (compile-time set indices).  The
-  // prefetches are unconditional (past the last step they reload it, unused), so exactly 6 DEPTH loads
-  // are newer than the step's own at every land().  The steps are guarded, not broken out of (early
-  // exits from the unrolled body spilled ~70 VGPRs).
-  constexpr int NS = DEPTH + 1;
-  v4i Ar[NS][2][ND];
-  const int last = total - 1;
-#pragma unroll
-  for (int u = 0; u < DEPTH; ++u) load_a(min(u, last), Ar[u]);
-  read_b(0, 0, B0);
-  for (int gs = 0; gs < total; gs += NS) {
-#pragma unroll
-    for (int u = 0; u < NS; ++u) {
-      load_a(min(gs + u + DEPTH, last), Ar[(u + DEPTH) % NS]);
-      if (u == 0 || gs + u < total) step(Ar[u]);
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the tail's redundant prefetches
 }
 
 #undef MFMA_I8
@@ -820,8 +870,15 @@ hipError_t launch_gemm_i8(const GemmI8Args& a0, hipStream_t s) {
   } else {
     a.e_tile0 = 0; a.ny = ng;
     // B-stationary when the spectrum's K steps fit the block's LDS
-    if (a0.ks_bound > 0 && a0.ks_bound <= kBstMaxKs && ng >= kBstEX && a0.G32) {
+    if (a0.ks_bound > 0 && a0.ks_bound <= kBstMaxKs && ng >= kBstEX && a0.G32 && ncu % 8 == 0) {
+      // the u tile on the two spare blocks per XCD when the Gram columns leave them (k = 50: 10 x 3 of
+      // 32) and there is one u tile (k <= 64)
+      const int per = ncu / 8, nye_max = (ng + kBstEX - 1) / kBstEX, nye_min = ng / kBstEX;
+      const bool fuse_u = GPDLA_BST_FUSE_U && nu == 1 && nye_min > 0 && per - nye_min * (per / nye_min) >= 2 &&
+                          per - nye_max * (per / nye_max) >= 2;
+      a.u_tile = fuse_u ? ng : -1;
       hipLaunchKernelGGL(gemm_i8_bst_kernel, dim3((unsigned)ncu), dim3(64 * kBstWaves), 0, s, a);
+      if (fuse_u) return hipGetLastError();
     } else {
       hipLaunchKernelGGL(gemm_i8_kernel<3>, grid(a.ny, 3), dim3(256), 0, s, a);
     }

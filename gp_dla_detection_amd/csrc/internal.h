@@ -374,6 +374,7 @@ struct GemmI8Args {
   int32_t nd;                    // Gram digit planes per operand: 4 (10 pairs, levels <= 3) or 3 (6 pairs); u: 4
   int32_t e_tile0, ny;           // set by launch_gemm_i8: first 64-entry tile and tile count of a launch
   int32_t ks_bound;              // bound on the spectrum's 64-slot K steps, ceil(ceil(lpix / 4) / 16)
+  int32_t u_tile;                // set by launch_gemm_i8: the u entry tile fused into the Gram launch, or -1
   const uint8_t* adig;
   const uint8_t* bdig;           // this spectrum's B planes
   const double* ent;             // this spectrum's [2][entries]

@@ -21,3 +21,10 @@
 #define GPDLA_MAX_CHUNK 131072
 #endif
 
+// gemm_i8_bst_kernel: share of an XCD's u sample tiles taken by its two spare blocks (A/B in progress)
+#ifndef GPDLA_BST_USPARE
+#define GPDLA_BST_USPARE 0.55f
+#endif
+#ifndef GPDLA_BST_FUSE_U
+#define GPDLA_BST_FUSE_U 1
+#endif

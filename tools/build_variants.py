@@ -17,10 +17,19 @@ VARIANTS: dict = {
     "ch16k": {"GPDLA_MAX_CHUNK": 16667},
     "bst_ex2": {"GPDLA_BST_EX": 2},
     "bst_ex8": {"GPDLA_BST_EX": 8},
+    "cur": {"GPDLA_VARIANT_CUR": 1},
+    "nofuse": {"GPDLA_BST_FUSE_U": 0},
+    "us45": {"GPDLA_BST_USPARE": "0.45f"},
+    "us55": {"GPDLA_BST_USPARE": "0.55f"},
+    "us65": {"GPDLA_BST_USPARE": "0.65f"},     # the working tree as a variant (A/B against the in-tree build)
 }
+# variants whose defines only matter in some sources: the rest is linked from the product objects
+ONLY = {n: {"gemm_i8.hip"} for n in ("cur", "nofuse", "us45", "us55", "us65")}
+
 if __name__ == "__main__":
     names = sys.argv[1:] or list(VARIANTS)
     out = Path(__file__).resolve().parent / "variants"
     out.mkdir(exist_ok=True)
     for n in names:
-        print(n, build(out=out / f"{n}.so", defines=VARIANTS[n] or {"GPDLA_VARIANT_BASE": 1}, force=True))
+        print(n, build(out=out / f"{n}.so", defines=VARIANTS[n] or {"GPDLA_VARIANT_BASE": 1}, force=True,
+                       define_only=ONLY.get(n)))
