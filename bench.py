@@ -67,8 +67,8 @@ def i8_roofline(st: dict, n: float, k: int, Q: int, S: int, steps: int, path: st
                             "achieved_tops": ops * evals_per_batch / (batch_ms * 1e-3) / 1e12,
                             "fp64_equivalent_tflops": algorithmic_flops_per_eval(n, k) * evals_per_batch
                                                       / (batch_ms * 1e-3) / 1e12},
-            "note": "gemm_i8 launches only (one per spectrum and sample chunk; the Gram and u launches of "
-                    "the 24-bit path counted as one); the batch adds the weights and LDL^T kernels"}
+            "note": "the int8 GEMM launch(es) of one spectrum and sample chunk only (the 24-bit path runs its Gram "
+                    "and u contractions in one launch); the batch adds the weights and LDL^T kernels"}
 
 
 def f64_gemm_roofline(st: dict, n: float, k: int, Q: int, S: int, steps: int) -> dict:
@@ -303,23 +303,23 @@ def e2e_record(Q: int, S: int, k: int, e2e_dir, keep: bool, world: int, rank: in
 
 
 # rocprofv3 summaries of the bench workloads (tools/profile.sh + tools/summarize_profile.py), committed
-PROFILE_SUMMARY = ROOT / "profiles" / "r5s_c2_summary.json"     # configs[1], fused fp64 (final round-3 tree)
+PROFILE_SUMMARY = ROOT / "profiles" / "round5" / "r10k_c2_summary.json"   # configs[1], fused fp64 (round-5 tree)
 # configs[4] (128 spectra x 10^5 samples, k = 50): the summary file and the EXACT names of the roofline
 # kernel's launches (the GEMM launches of one spectrum and sample chunk; per-batch conversion kernels
 # such as convert_gemm_i8_kernel are not part of it)
 PROFILE_SUMMARY_C5 = {
-    # the 32-bit path's Gram + u launch is gemm_i8_kernel<4> (round-2 profiles predate the template)
-    "panel-GEMM-int8": (ROOT / "profiles" / "r10_c5i8_summary.json",
+    # the 32-bit path's Gram + u launch is gemm_i8_kernel<4>
+    "panel-GEMM-int8": (ROOT / "profiles" / "round5" / "r10k_c5i8_summary.json",
                         ("void gpdla::gemm_i8_kernel<4>(gpdla::GemmI8Args)",)),
-    "panel-GEMM-int8-24": (ROOT / "profiles" / "r9z_c5_summary.json",
-                           ("gpdla::gemm_i8_bst_kernel(gpdla::GemmI8Args)",
-                            "void gpdla::gemm_i8_kernel<4>(gpdla::GemmI8Args)")),
+    # the 24-bit path: Gram and u contractions in one B-stationary launch (round 5)
+    "panel-GEMM-int8-24": (ROOT / "profiles" / "round5" / "r10k_c5_summary.json",
+                           ("gpdla::gemm_i8_bst_kernel(gpdla::GemmI8Args)",)),
     "panel-GEMM": (ROOT / "profiles" / "r5f_c5f64_summary.json", ("gpdla::gemm_f64_kernel(gpdla::GemmF64Args)",)),
 }
 # the roofline kernel's label per path
 ROOFLINE_KERNEL = {"fused": "likelihood_kernel<{k}>", "fused-int8": "likelihood_i8_kernel<{k}>",
                    "panel-GEMM-int8": "gemm_i8_kernel (Gram + u)",
-                   "panel-GEMM-int8-24": "gemm_i8_bst_kernel (Gram) + gemm_i8_kernel<4> (u)",
+                   "panel-GEMM-int8-24": "gemm_i8_bst_kernel (Gram + u contractions in one launch)",
                    "panel-GEMM": "gemm_f64_kernel (Gram + u)"}
 
 

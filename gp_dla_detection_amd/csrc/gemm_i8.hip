@@ -800,8 +800,11 @@ void gemm_i8_bst_kernel(GemmI8Args a) {
   const int nks = (16 * ((inf.L + 15) / 16)) / 16;
   if (nks > kBstMaxKs) return;                   // never: the launch checks the bound (LDS safety)
   // the u work of this XCD: both halves of the u tile over its share [lo, hi) of the sample range; a
-  // spare block per half takes the first ~kBstUSpare of the tiles (it starts at once), the Gram
-  // blocks split the rest per half once their Gram columns are done
+  // spare block per half takes the first kBstUSpare of the tiles (it starts at once), the Gram blocks
+  // split the rest per half once their Gram columns are done.  A u tile takes a spare block ~2x the
+  // time a Gram tile takes a Gram block (the u role is bound by its A stream: 4 digit planes for 2 x
+  // 10 MFMA pairs), hence the split (tuning.h); the u launch this replaces cost 0.085 ms per
+  // spectrum and 100,001 samples, the fused launch +0.03 ms over the Gram alone (profiles/round5)
   const int lo = s0 + (s1 - s0) * ex / EX, hi = s0 + (s1 - s0) * (ex + 1) / EX;
   const int mid = lo + (int)((hi - lo) * kBstUSpare + 0.5f);
   if (j < nye * G) {
@@ -874,7 +877,7 @@ hipError_t launch_gemm_i8(const GemmI8Args& a0, hipStream_t s) {
       // the u tile on the two spare blocks per XCD when the Gram columns leave them (k = 50: 10 x 3 of
       // 32) and there is one u tile (k <= 64)
       const int per = ncu / 8, nye_max = (ng + kBstEX - 1) / kBstEX, nye_min = ng / kBstEX;
-      const bool fuse_u = GPDLA_BST_FUSE_U && nu == 1 && nye_min > 0 && per - nye_min * (per / nye_min) >= 2 &&
+      const bool fuse_u = nu == 1 && nye_min > 0 && per - nye_min * (per / nye_min) >= 2 &&
                           per - nye_max * (per / nye_max) >= 2;
       a.u_tile = fuse_u ? ng : -1;
       hipLaunchKernelGGL(gemm_i8_bst_kernel, dim3((unsigned)ncu), dim3(64 * kBstWaves), 0, s, a);

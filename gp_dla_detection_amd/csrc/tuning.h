@@ -21,10 +21,9 @@
 #define GPDLA_MAX_CHUNK 131072
 #endif
 
-// gemm_i8_bst_kernel: share of an XCD's u sample tiles taken by its two spare blocks (A/B in progress)
+// gemm_i8_bst_kernel: share of an XCD's u sample tiles taken by its two spare blocks (the Gram
+// blocks take the rest after their columns); configs[4]: 0.15 / 0.25 / 0.35 / 0.40 / 0.45 / 0.50 /
+// 0.55 / 0.65 -> 9.96 / 9.97 / 9.99 / 10.08 / 10.03 / 9.79 / 9.44 / 8.93e7 evals/s (profiles/round5/r10h-j)
 #ifndef GPDLA_BST_USPARE
-#define GPDLA_BST_USPARE 0.55f
-#endif
-#ifndef GPDLA_BST_FUSE_U
-#define GPDLA_BST_FUSE_U 1
+#define GPDLA_BST_USPARE 0.40f
 #endif
