@@ -770,6 +770,9 @@ int gpdla_engine_process(gpdla_engine* e, const gpdla_spectra* sp, const gpdla_r
     pa.om2_hi_e = e->om2_hi_e;
     pa.info = e->d_info; pa.panel = e->d_panel; pa.lam_pad = e->d_lam; pa.slot_pixel = e->d_smap;
     pa.k = e->K; pa.panel_m = e->d_pm; pa.srow = e->d_srow;
+    // the int8 panel paths form the Khatri-Rao entries from the M rows (convert_gemm_i8_kernel): prep
+    // skips the k(k+1)/2 doubles per slot
+    if (batch_gemm_i8) pa.panel = nullptr;
 
     LikelihoodArgs la{};
     la.q_count = (int32_t)nq;
@@ -802,7 +805,7 @@ int gpdla_engine_process(gpdla_engine* e, const gpdla_spectra* sp, const gpdla_r
     if (batch_i8) HIP_TRY(launch_convert_i8(e->K, ca, st));
     if (batch_gemm_i8) {
       ConvertGemmI8Args cg{};
-      cg.k = e->K; cg.info = e->d_info; cg.panel = e->d_panel; cg.panel_m = e->d_pm; cg.srow = e->d_srow;
+      cg.k = e->K; cg.info = e->d_info; cg.panel_m = e->d_pm; cg.srow = e->d_srow;
       cg.slot_base = pa.slot_base; cg.slot_cap = pa.slot_cap; cg.bbase = pa.slot_cap + QB;
       cg.bdig = e->d_pi8; cg.ent = e->d_pent; cg.nd = e->i8_nd;
       HIP_TRY(launch_convert_gemm_i8(cg, (int32_t)nq, st));

@@ -31,6 +31,7 @@ namespace {
 __global__ __launch_bounds__(256) void convert_gemm_i8_kernel(ConvertGemmI8Args a) {
   __shared__ double s_mx[4][64];
   __shared__ long long s_cs[4][64];
+  __shared__ uint16_t s_rc[64];                  // Gram entry -> (r, c) of this block's 64 entries
   const int q = blockIdx.y;
   const SpecInfo inf = a.info[q];
   if (inf.J == 0) return;
@@ -49,13 +50,27 @@ __global__ __launch_bounds__(256) void convert_gemm_i8_kernel(ConvertGemmI8Args 
   const int64_t sb = a.slot_base[q];
   const int64_t kstride = i8_gemm_kstride(a.slot_cap[q]);
   const int nd = i8_spectrum_nd(a.nd, a.slot_cap[q]);  // short spectra: 4 planes on the 24-bit path too
+  // the Gram entry col is the Khatri-Rao product M_r M_c of its (r, c) (gram_tile_index order, as
+  // prep_kernel<0> would store it; formed here from the M rows instead of read as 8 B per entry and
+  // slot: bit for bit the same products)
+  if (threadIdx.x < 64) s_rc[threadIdx.x] = 0;
+  __syncthreads();
+  if (blockIdx.x * 64 < Ep)                      // a Gram entry tile: every (r, c) of it, 256 at a time
+    for (int pr = threadIdx.x; pr < K * K; pr += 256) {
+      const int r = pr / K, c = pr - r * K;
+      const int ee = c >= r ? gram_tile_index(r, c, K) - blockIdx.x * 64 : -1;
+      if (ee >= 0 && ee < 64) s_rc[ee] = (uint16_t)(r | (c << 8));
+    }
+  __syncthreads();
+  const int rc = is_u ? 0 : s_rc[le];
+  const int mr = is_u ? col : (rc & 255), mc = rc >> 8;
   auto value = [&](int t) -> double {
     if (!valid || t >= L) return 0.0;
     const int64_t row = sb + (int64_t)g * Ls + t;
     const double* sr = a.srow + row * 8;
     const double y = sr[1], noise = sr[2], mu = sr[3], om2 = sr[4];
-    return is_u ? a.panel_m[row * gemm_ldm(K) + col] * u_bound(y, mu, noise)
-                : a.panel[row * gemm_ldp(K) + col] / (om2 + noise);
+    const double* m = a.panel_m + row * gemm_ldm(K);
+    return is_u ? m[mr] * u_bound(y, mu, noise) : (m[mr] * m[mc]) / (om2 + noise);
   };
   double mx = 0.0;
   for (int t = 0; t < L; ++t) mx = fmax(mx, fabs(value(t)));
@@ -595,18 +610,18 @@ constexpr int kBstEX = GPDLA_BST_EX;
 constexpr int kBstWaves = 8;
 constexpr int kBstLds = kBstMaxKs * 3 * kGTileE * 64;  // the Gram role's B image (the u role uses 2/3)
 constexpr float kBstUSpare = GPDLA_BST_USPARE;           // share of the u tiles the spare blocks take
+constexpr int kBstUDepth = 2;  // the u role's A prefetch depth (K steps; 3 measured equal, profiles/round5/ab/r10n)
 
 // One role of the B-stationary launch.  A unit is W = 16 NCT consecutive entries starting at global
 // entry ebase, whose B digits (ND planes, the whole K range) sit in Bs; the block's waves walk the
 // sample tiles s_lo + kTiles (gi + r G) + (wave >> 2), r = 0, 1, ... below s_hi.
 //   (ND, NCT) = (3, 4): a Gram entry tile, 6 digit pairs (levels <= 2), fp32 Gram out;
 //   (ND, NCT) = (4, 2): half of the u entry tile, 10 digit pairs (levels <= 3), fp64 u out.
-template <int ND, int NCT>
+template <int ND, int NCT, int DEPTH>  // DEPTH: K steps of A digits in flight ahead of the one multiplied
 __device__ inline void bst_run(const GemmI8Args& a, const SpecInfo& inf, uint8_t* Bs, double (*s_ent)[kGTileE],
                                int ebase, int s_lo, int s_hi, int gi, int G) {
   constexpr int W = 16 * NCT;
   constexpr bool kU = ND == 4;
-  constexpr int DEPTH = 2;                       // K steps of A digits in flight ahead of the one multiplied
   constexpr int kStepBytes = ND * W * 64;        // one K step of the unit: ND planes x W rows x 64 B
   constexpr int kTiles = kBstWaves / 4;          // 128-sample tiles per block round
   const int K = a.k;
@@ -678,8 +693,9 @@ __device__ inline void bst_run(const GemmI8Args& a, const SpecInfo& inf, uint8_t
   // never too short).  Prefetches past the wave's last step are not issued: a load whose value is
   // never read leaves its registers free for the compiler while the hardware may still write them.
   auto land = [&](int g, v4i (&r)[2][ND]) {
-    static_assert(DEPTH == 2, "land() spells out the waits for DEPTH = 2");
-    if (last - g >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * ND * 2) : "memory");
+    static_assert(DEPTH == 2 || DEPTH == 3, "land() spells out the waits for DEPTH 2 and 3");
+    if (last - g >= DEPTH) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * ND * DEPTH) : "memory");
+    else if (DEPTH == 3 && last - g == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * ND * 2) : "memory");
     else if (last - g == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * ND) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
@@ -808,15 +824,15 @@ void gemm_i8_bst_kernel(GemmI8Args a) {
   const int lo = s0 + (s1 - s0) * ex / EX, hi = s0 + (s1 - s0) * (ex + 1) / EX;
   const int mid = lo + (int)((hi - lo) * kBstUSpare + 0.5f);
   if (j < nye * G) {
-    bst_run<3, 4>(a, inf, Bs, s_ent, (a.e_tile0 + e0 + j % nye) * kGTileE, s0, s1, j / nye, G);
+    bst_run<3, 4, 2>(a, inf, Bs, s_ent, (a.e_tile0 + e0 + j % nye) * kGTileE, s0, s1, j / nye, G);
     if (a.u_tile >= 0 && nye * G >= 2) {
       __syncthreads();                           // every wave is done with the Gram B image
       const int half = j & 1, ngb = nye * G / 2;
-      if (j / 2 < ngb) bst_run<4, 2>(a, inf, Bs, s_ent, a.u_tile * kGTileE + 32 * half, mid, hi, j / 2, ngb);
+      if (j / 2 < ngb) bst_run<4, 2, kBstUDepth>(a, inf, Bs, s_ent, a.u_tile * kGTileE + 32 * half, mid, hi, j / 2, ngb);
     }
   } else if (a.u_tile >= 0 && j < nye * G + 2) {
     const int half = j - nye * G;
-    bst_run<4, 2>(a, inf, Bs, s_ent, a.u_tile * kGTileE + 32 * half, lo, mid, 0, 1);
+    bst_run<4, 2, kBstUDepth>(a, inf, Bs, s_ent, a.u_tile * kGTileE + 32 * half, lo, mid, 0, 1);
   }
 }
 

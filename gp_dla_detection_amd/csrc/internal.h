@@ -111,7 +111,8 @@ struct PrepArgs {
   int32_t om2_hi_e;              // binary exponent of the model's largest omega^2 (1 + c_0)^2 (units)
   // outputs
   SpecInfo* info;
-  double* panel;                 // fused layout: [slots][kRow]; GEMM layout: [slots][k(k+1)/2]
+  double* panel;                 // fused layout: [slots][kRow]; GEMM layout: [slots][k(k+1)/2] (nullptr:
+                                 // the int8 panel paths form the Khatri-Rao entries from panel_m themselves)
   double* panel_m;               // GEMM layout only: [slots][k] M rows
   double* srow;                  // GEMM layout only: [slots][8] lam, y, noise, mu, om2, valid
   double* lam_pad;
@@ -335,8 +336,7 @@ __host__ __device__ inline int i8_gemm_entries(int k) {
 struct ConvertGemmI8Args {
   int32_t k;
   const SpecInfo* info;
-  const double* panel;           // PG [slots][E]
-  const double* panel_m;         // [slots][k]
+  const double* panel_m;         // [slots][k] M rows (the Khatri-Rao entries are formed from them)
   const double* srow;            // [slots][8]
   const int64_t* slot_base;      // device [q]
   const int64_t* slot_cap;       // device [q]

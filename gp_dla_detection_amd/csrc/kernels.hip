@@ -283,12 +283,13 @@ __global__ __launch_bounds__(256) void prep_kernel(PrepArgs a) {
       // panel-GEMM layout: Khatri-Rao row (entry (r, c) at gram_tile_index(r, c), internal.h) and M
       // row (the 8 slot scalars come from pass 3a); all zero for masked and padding slots
       const int64_t E = (int64_t)KK * (KK + 1) / 2;
-      double* pg = a.panel + (sb + j) * gemm_ldp(KK);
+      double* pg = a.panel ? a.panel + (sb + j) * gemm_ldp(KK) : nullptr;
       double* pm = a.panel_m + (sb + j) * gemm_ldm(KK);
-      for (int64_t e = lane; e < E; e += 64) {
-        const int rc = s_rc[e];
-        pg[e] = pix >= 0 ? Mi(rc & 255) * Mi(rc >> 8) : 0.0;
-      }
+      if (a.panel)  // (the int8 panel paths form these from the M rows in convert_gemm_i8_kernel)
+        for (int64_t e = lane; e < E; e += 64) {
+          const int rc = s_rc[e];
+          pg[e] = pix >= 0 ? Mi(rc & 255) * Mi(rc >> 8) : 0.0;
+        }
       for (int c = lane; c < KK; c += 64) pm[c] = pix >= 0 ? Mi(c) : 0.0;
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // reads of this slot's row done before
