@@ -25,6 +25,21 @@ namespace {
 
 #define MFMA_I8(A, B, C) __builtin_amdgcn_mfma_i32_16x16x64_i8((A), (B), (C), 0, 0, 0)
 
+// Epilogue of the exact int8 contraction: the ND level sums C_l (digit pairs of level l, weight
+// 2^(48 - 8 l)) are folded as t = sum_l 256^(ND - 1 - l) C_l in fp64 (integer-valued, exact while it
+// stays below 2^53, which covers every configs[4]-sized K), then value = (2^(48 - 8 (ND - 1)) t + off0)
+// sc as ONE fma with the column's constants scl = 2^(48 - 8 (ND - 1)) sc and offl = off0 sc: 7 VALU
+// per output instead of 9 (round 5: the epilogue was 16% of the Gram launch, profiles/round5/r10o)
+template <int ND>
+__device__ inline double i8_level_value(const v4i (&lv)[ND], int r, double scl, double offl) {
+  double t = (double)lv[0][r];
+#pragma unroll
+  for (int l = 1; l < ND; ++l) t = fma(t, 256.0, (double)lv[l][r]);
+  return fma(t, scl, offl);
+}
+template <int ND>
+__host__ __device__ constexpr double i8_level_scale() { return (double)(1ull << (48 - 8 * (ND - 1))); }
+
 // --------------------------------------------------------------------------------------------
 // convert: grid (entries / 64, spectra), 256 threads = 64 entries x 4 segments
 // --------------------------------------------------------------------------------------------
@@ -516,20 +531,18 @@ __global__ __launch_bounds__(256, ND == 3 ? 3 : 2) void gemm_i8_kernel(GemmI8Arg
       const int col = u_tile ? e - Ep : e;
       if (u_tile ? col >= K : col >= E) continue;
       const double sc = a.ent[e], off0 = a.ent[NE + e];
+      const double scl = i8_level_scale<ND>() * sc, offl = off0 * sc;
 #pragma unroll
       for (int rt = 0; rt < 2; ++rt) {
         // the lane's 4 consecutive samples of entry col: one vector store in the quad_index layout
         // (every sample of the rows is stored; those past sc are never read)
         const int s4 = s_tile + 32 * wave + 16 * rt + 4 * (lane >> 4);
+        v4i lv[ND];
+#pragma unroll
+        for (int l = 0; l < ND; ++l) lv[l] = acc[l][rt][ct];
         double v[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          // sum_l 2^(48 - 8 l) C_l, least significant level first
-          double val = (double)acc[ND - 1][rt][ct][r] * __builtin_ldexp(1.0, 48 - 8 * (ND - 1));
-#pragma unroll
-          for (int l = ND - 2; l >= 0; --l) val = fma((double)acc[l][rt][ct][r], __builtin_ldexp(1.0, 48 - 8 * l), val);
-          v[r] = (val + off0) * sc;
-        }
+        for (int r = 0; r < 4; ++r) v[r] = i8_level_value<ND>(lv, r, scl, offl);
         if (u_tile) {
           double2* d = reinterpret_cast<double2*>(a.U + quad_index(s4, col, K));
           d[0] = make_double2(v[0], v[1]);
@@ -647,9 +660,11 @@ __device__ inline void bst_run(const GemmI8Args& a, const SpecInfo& inf, uint8_t
     }
     // the epilogue's per-entry scale and offset from LDS: a global load there would make the waitcnt
     // pass drain the A prefetches in flight at every tile's end
-    if (threadIdx.x < 2 * W) {
-      const int c = threadIdx.x % W, kind = threadIdx.x / W, e = ebase + c;
-      s_ent[kind][c] = valid_entry(e) ? a.ent[kind * NE + e] : 0.0;
+    if (threadIdx.x < W) {  // the column's epilogue constants scl, offl (i8_level_value)
+      const int c = threadIdx.x, e = ebase + c;
+      const double sc = valid_entry(e) ? a.ent[e] : 0.0, off0 = valid_entry(e) ? a.ent[NE + e] : 0.0;
+      s_ent[0][c] = i8_level_scale<ND>() * sc;
+      s_ent[1][c] = off0 * sc;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -727,19 +742,16 @@ __device__ inline void bst_run(const GemmI8Args& a, const SpecInfo& inf, uint8_t
     for (int ct = 0; ct < NCT; ++ct) {
       const int c = 16 * ct + (lane & 15), e = ebase + c;
       if (!valid_entry(e)) continue;
-      const double sc = s_ent[0][c], off0 = s_ent[1][c];
+      const double scl = s_ent[0][c], offl = s_ent[1][c];
 #pragma unroll
       for (int rt = 0; rt < 2; ++rt) {
         const int s4 = s_tile + 32 * wt + 16 * rt + 4 * (lane >> 4);
+        v4i lv[ND];
+#pragma unroll
+        for (int l = 0; l < ND; ++l) lv[l] = acc[l][rt][ct];
         double v[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          // sum_l 2^(48 - 8 l) C_l, least significant level first
-          double val = (double)acc[ND - 1][rt][ct][r] * __builtin_ldexp(1.0, 48 - 8 * (ND - 1));
-#pragma unroll
-          for (int l = ND - 2; l >= 0; --l) val = fma((double)acc[l][rt][ct][r], __builtin_ldexp(1.0, 48 - 8 * l), val);
-          v[r] = (val + off0) * sc;
-        }
+        for (int r = 0; r < 4; ++r) v[r] = i8_level_value<ND>(lv, r, scl, offl);
         if constexpr (kU) {
           double2* d = reinterpret_cast<double2*>(a.U + quad_index(s4, e - Ep, K));
           d[0] = make_double2(v[0], v[1]);

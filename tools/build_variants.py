@@ -28,7 +28,7 @@ VARIANTS: dict = {
     "us65": {"GPDLA_BST_USPARE": "0.65f"},     # the working tree as a variant (A/B against the in-tree build)
 }
 # variants whose defines only matter in some sources: the rest is linked from the product objects
-ONLY = {n: {"gemm_i8.hip"} for n in ("us40", "us50", "us15", "us25", "us35", "us45", "us55", "us65")}
+ONLY = {n: {"gemm_i8.hip"} for n in ("cur", "us40", "us50", "us15", "us25", "us35", "us45", "us55", "us65")}
 
 if __name__ == "__main__":
     names = sys.argv[1:] or list(VARIANTS)
