@@ -71,6 +71,29 @@ def i8_roofline(st: dict, n: float, k: int, Q: int, S: int, steps: int, path: st
                     "and u contractions in one launch); the batch adds the weights and LDL^T kernels"}
 
 
+def i8_single_stream(eng, step, n: float, k: int, Q: int, S: int, path: str, steps: int = 2) -> dict:
+    """The int8 GEMM launch timed with the batch on ONE compute stream, after the timed region (one
+    untimed step, then ``steps`` steps).  In the timed region a batch's spectra alternate over two
+    streams (gpdla_engine_set_panel_streams), so each GEMM launch shares the CUs with the other
+    stream's weights / LDL^T kernels and its HIP-event duration is the overlapped one; this is the
+    kernel's own rate."""
+    eng.set_panel_streams(1)
+    step()
+    eng.synchronize()
+    eng.reset_stats()
+    for _ in range(steps):
+        step()
+    eng.synchronize()
+    st = eng.stats()
+    eng.set_panel_streams(2)
+    r = i8_roofline(st, n, k, Q, S, steps, path)
+    return {"avg_launch_ms": r["avg_launch_ms"], "achieved": r["achieved"], "frac": r["frac"],
+            "whole_batch_ms": r["whole_batch"]["avg_ms"], "steps": steps,
+            "note": "panel streams = 1, measured after the timed region: the GEMM launch without the other "
+                    "stream's kernels beside it (roofline.avg_launch_ms is the overlapped launch of the "
+                    "timed region)"}
+
+
 def f64_gemm_roofline(st: dict, n: float, k: int, Q: int, S: int, steps: int) -> dict:
     """Roofline of the fp64 panel path's dominant kernel, the Gram/u GEMM on the f64 matrix cores
     (gemm_f64.hip): 2 n (k(k+1)/2 + k) algorithmic flops per evaluation (the Gram and u part of
@@ -574,6 +597,8 @@ def configs4_alternative(dev: int, steps: int) -> dict:
         eng.synchronize()
         el = time.perf_counter() - t0
         st = eng.stats()
+        n_mean = float(np.mean(o_n.numpy()))
+        alone = i8_single_stream(eng, step, n_mean, k, Q, S, "panel-GEMM-int8-24")
     sub = 8
     with Engine(model, samples, set_parameters(k=k), device=dev, path="panel_gemm") as e64:
         ref = e64.process(syn.pack_spectra(spectra[:sub]))
@@ -584,12 +609,13 @@ def configs4_alternative(dev: int, steps: int) -> dict:
             "log_likelihoods_dla": rel(lld[:sub], ref["log_likelihoods_dla"]),
             "log_likelihoods_no_dla": rel(lln[:sub], ref["log_likelihoods_no_dla"])}
     inv = np.exp(sll - (lld[:sub, None] + np.log(S))).sum(axis=1)
-    n_mean = float(np.mean(o_n.numpy()))
     path = "panel-GEMM-int8-24"
     roof = i8_roofline(st, n_mean, k, Q, S, steps, path)
     traffic, src = profiled_traffic(Q, S, k, path)
-    roof.update({"kernel": ROOFLINE_KERNEL[path], "traffic": traffic, "traffic_source": src})
-    dram = dram_record(traffic, roof["avg_launch_ms"], src, path)
+    roof.update({"kernel": ROOFLINE_KERNEL[path], "traffic": traffic, "traffic_source": src,
+                 "single_stream": alone})
+    # PMC bytes are per dispatch (the counter passes serialise kernels): over the kernel's own time
+    dram = dram_record(traffic, alone["avg_launch_ms"], src, path)
     dram["chain"] = chain_dram(path)
     for a in (*t.values(), o_null, o_dla, o_s, o_n):
         a.free()
@@ -706,6 +732,8 @@ def main():
     ap.add_argument("--path", choices=["auto", "fused", "fused_i8", "panel_gemm", "panel_gemm_i8", "panel_gemm_i8_24"], default="auto",
                     help="likelihood path (Engine path=): auto = fused fp64 kernel for the compiled ranks, "
                          "fused_i8 = the int8 Ozaki contraction (k=20), panel_gemm = weights + dgemm + LDL^T")
+    ap.add_argument("--panel-streams", type=int, choices=[1, 2], default=2,
+                    help="int8 panel paths: compute streams a batch's spectra alternate over")
     ap.add_argument("--no-alt", action="store_true",
                     help="skip the alternative-path measurement (fused_i8 next to the fp64 line, 1 GPU, c2)")
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU-baseline work (0 = skip)")
@@ -805,6 +833,8 @@ def main():
     if args.path == "auto" and "default_path" in wl:
         args.path = wl["default_path"]
     eng = Engine(model, samples, set_parameters(k=args.k), device=dev, path=args.path)
+    if args.path.startswith("panel_gemm_i8"):
+        eng.set_panel_streams(args.panel_streams)
     if args.path == "fused_i8":
         path = "fused-int8"
     elif args.path == "panel_gemm_i8":
@@ -830,6 +860,8 @@ def main():
     st = eng.stats()
     npix = o_n.numpy()
     n_mean = float(np.mean(npix))
+    alone = (i8_single_stream(eng, step, n_mean, args.k, Q, S, path)
+             if path.startswith("panel-GEMM-int8") and args.panel_streams == 2 else None)
 
     # per-rank load balance: each rank's own kernel time and wall time over the timed steps
     per_rank = gather({"rank": rank, "spectra": int(Q), "pixels": int(np.sum(npix)),
@@ -928,6 +960,8 @@ def main():
             **(i8_roofline(st, n_mean, args.k, Q, S, args.steps, path) if path.startswith("panel-GEMM-int8")
                else f64_gemm_roofline(st, n_mean, args.k, Q, S, args.steps) if path == "panel-GEMM"
                else {})}
+    if alone is not None:
+        roof["single_stream"] = alone
     rehearsal = world > 1 and distinct < world
     result = {
         "metric": "(spectrum x DLA-sample) log-evidence evals/sec",
@@ -955,7 +989,7 @@ def main():
                    "spectra_per_gpu": Q, "num_samples": S, "k": args.k, "n_pixels": n_mean,
                    "likelihood_path": path, "parallelism": f"spectrum-shard x{world}"},
         "roofline": roof,
-        "dram": dram_record(traffic, roof["avg_launch_ms"], traffic_src, path),
+        "dram": dram_record(traffic, (alone or roof)["avg_launch_ms"], traffic_src, path),
         "streamed_panel_equiv": {"gbs": eff_gbs, "bytes_per_eval": effective_bytes_per_eval(n_mean, args.k),
                                  "note": "SURVEY.md 8d's streamed-panel accounting (B_eval bytes per evaluation / "
                                          "kernel time): what a kernel re-reading the n x (k+5) panel per sample would "

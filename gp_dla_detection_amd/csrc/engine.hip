@@ -166,6 +166,12 @@ struct gpdla_engine {
   // copy_stream while batch b + 1 (resp. b) computes; the two stages alternate
   HostStage hs[2];
   hipStream_t copy_stream = nullptr;
+  // the int8 panel path's second compute stream (panel_streams = 2): odd spectra of a batch run on it,
+  // with their own workspace set, so one spectrum's kernels fill the last-round tails of the other's
+  int panel_streams = 2;
+  hipStream_t panel_stream2 = nullptr;
+  hipEvent_t panel_fork = nullptr, panel_join = nullptr;
+  int64_t ws_ai8 = 0, ws_G = 0, ws_U = 0, ws_wp = 0;  // per-set workspace sizes (bytes / doubles)
 
   // pinned host metadata (reused after meta_ready completes)
   int64_t* h_meta = nullptr;
@@ -179,11 +185,11 @@ struct gpdla_engine {
 
 namespace {
 
-int record_start(gpdla_engine* e, TimedLaunch* t, int kind) {
+int record_start(gpdla_engine* e, TimedLaunch* t, int kind, hipStream_t s = nullptr) {
   HIP_TRY(hipEventCreate(&t->start));
   HIP_TRY(hipEventCreate(&t->stop));
   t->kind = kind;
-  HIP_TRY(hipEventRecord(t->start, e->stream));
+  HIP_TRY(hipEventRecord(t->start, s ? s : e->stream));
   return GPDLA_OK;
 }
 
@@ -270,6 +276,12 @@ void gpdla_engine_destroy(gpdla_engine* e) {
       if (ev) (void)hipEventDestroy(ev);
   }
   if (e->copy_stream) (void)hipStreamDestroy(e->copy_stream);
+  if (e->panel_stream2) {
+    (void)hipStreamSynchronize(e->panel_stream2);
+    (void)hipStreamDestroy(e->panel_stream2);
+  }
+  if (e->panel_fork) (void)hipEventDestroy(e->panel_fork);
+  if (e->panel_join) (void)hipEventDestroy(e->panel_join);
   void* bufs[] = {e->d_rest, e->d_mu, e->d_M, e->d_logom, e->d_off, e->d_nhi, e->d_perm, e->d_lines,
                   e->d_status, e->d_meta, e->d_wl, e->d_flux, e->d_noise, e->d_mask, e->d_z,
                   e->d_info, e->d_panel, e->d_lam, e->d_smap, e->d_scratch, e->d_sll,
@@ -404,26 +416,49 @@ int gpdla_engine_set_stream(gpdla_engine* e, void* hip_stream) {
   return GPDLA_OK;
 }
 
+int gpdla_engine_set_panel_streams(gpdla_engine* e, int32_t n) {
+  if (!e) return set_error(GPDLA_EINVAL, "null engine");
+  if (n != 1 && n != 2) return set_error(GPDLA_EINVAL, "panel streams must be 1 or 2 (got %d)", (int)n);
+  e->panel_streams = n;
+  return GPDLA_OK;
+}
+
 // Panel-GEMM path for one batch: per spectrum and chunk of samples, weights -> GEMM on the matrix
 // cores (int8 digits, gemm_i8.hip, or fp64, gemm_f64.hip) -> batched LDL^T (gemm_path.hip), in
 // stream order.
-// (Second streams measured no gain and were removed: the LDL^T beside the next chunk's weights and
-// GEMM +5% with round 1's VALU LDL^T, 0% with the matrix-core one (profiles/r2f); the weights kernel
-// beside the previous chunk's GEMM and LDL^T, double-buffered, +0.5% (round 2, profiles/r2c).)
+// int8 paths: a batch's spectra alternate over two streams (gpdla_engine_set_panel_streams), which
+// fills the last partial round of each spectrum's weights / LDL^T launches with the other spectrum's
+// work: +3.6% on configs[4] (profiles/round5/ab/r11a).  (Earlier second-stream layouts, within one
+// spectrum, measured no gain: the LDL^T beside the next chunk's weights and GEMM, 0% with the
+// matrix-core LDL^T (profiles/r2f); the weights beside the previous chunk's GEMM, +0.5% (profiles/r2c).)
 static int run_panel_gemm(gpdla_engine* e, bool i8, int64_t nq, const int64_t* h_sb, const int64_t* h_lb,
                           const int64_t* h_cap, const int64_t* h_cb, int64_t sc_max, double* o_sll,
                           int64_t ld, double* o_null, hipStream_t st) {
   const int K = e->K;
   const int64_t E = (int64_t)K * (K + 1) / 2;
-  double *G = e->d_G, *U = e->d_U, *q1p = e->d_q1p, *ldp = e->d_ldp;
   const int64_t rows = (sc_max + 127) / 128 * 128;
+  // int8 path with two compute streams: spectrum q on stream q % 2 with workspace set q % 2, forked
+  // from and joined back into st (the batch's prep / convert before, its reduce after)
+  const bool two = i8 && e->panel_streams == 2 && nq > 1;
+  if (two) {
+    if (!e->panel_stream2) HIP_TRY(hipStreamCreateWithFlags(&e->panel_stream2, hipStreamNonBlocking));
+    if (!e->panel_fork) HIP_TRY(hipEventCreateWithFlags(&e->panel_fork, hipEventDisableTiming));
+    if (!e->panel_join) HIP_TRY(hipEventCreateWithFlags(&e->panel_join, hipEventDisableTiming));
+    HIP_TRY(hipEventRecord(e->panel_fork, st));
+    HIP_TRY(hipStreamWaitEvent(e->panel_stream2, e->panel_fork, 0));
+  }
+  const hipStream_t st0 = st;
   for (int64_t q = 0; q < nq; ++q) {
+    const int set = two ? (int)(q & 1) : 0;
+    st = set ? e->panel_stream2 : st0;
+    double *G = e->d_G + set * e->ws_G, *U = e->d_U + set * e->ws_U;
+    double *q1p = e->d_q1p + set * e->ws_wp, *ldp = e->d_ldp + set * e->ws_wp;
     for (int64_t s0 = 0; s0 <= e->S; s0 += sc_max) {
       const int32_t sc = (int32_t)std::min<int64_t>(sc_max, e->S + 1 - s0);
       if (i8) {  // int8 Ozaki contraction (gemm_i8.hip): weights digits -> exact GEMM -> Gram, u
         const int64_t ks = i8_gemm_kstride(h_cap[q]);
         const int nd = i8_spectrum_nd(e->i8_nd, h_cap[q]);  // short spectra: 32-bit digits (internal.h)
-        uint8_t* adig = e->d_ai8;
+        uint8_t* adig = e->d_ai8 + set * e->ws_ai8;
         WeightsI8Args wi{};
         wi.info = e->d_info; wi.q = (int32_t)q;
         wi.srow = e->d_srow + h_sb[q] * 8; wi.lam_pad = e->d_lam + h_lb[q]; wi.kstride = ks;
@@ -440,7 +475,7 @@ static int run_panel_gemm(gpdla_engine* e, bool i8, int64_t nq, const int64_t* h
         gi.ks_bound = i8_ks_bound(h_cap[q]);  // slot_cap = 4 ceil(lpix / 4) + 16
         TimedLaunch tg{};
         int rc;
-        if ((rc = record_start(e, &tg, 3))) return rc;
+        if ((rc = record_start(e, &tg, 3, st))) return rc;
         HIP_TRY(launch_gemm_i8(gi, st));
         HIP_TRY(hipEventRecord(tg.stop, st));
         e->pending.push_back(tg);
@@ -474,6 +509,10 @@ static int run_panel_gemm(gpdla_engine* e, bool i8, int64_t nq, const int64_t* h
       da.sample_ll = o_sll ? o_sll + q * ld : nullptr; da.ll_null = o_null + q; da.status = e->d_status;
       HIP_TRY(launch_ldl_batch(da, st));
     }
+  }
+  if (two) {
+    HIP_TRY(hipEventRecord(e->panel_join, e->panel_stream2));
+    HIP_TRY(hipStreamWaitEvent(st0, e->panel_join, 0));
   }
   return GPDLA_OK;
 }
@@ -662,16 +701,20 @@ int gpdla_engine_process(gpdla_engine* e, const gpdla_spectra* sp, const gpdla_r
       // slack: ldl_mfma_kernel's straight-line tile loads may address one entry past the last
       // sample's Gram when k is a multiple of 4 (the value is discarded)
       const int64_t grows = gemm_f64_rows(sc_max);
-      if ((rc = grow(&e->d_G, &e->cap_G, (size_t)(E * grows + 64)))) return rc;
-      if ((rc = grow(&e->d_U, &e->cap_U, (size_t)(e->K * grows + 64)))) return rc;
-      if ((rc = grow(&e->d_q1p, &e->cap_q1p, (size_t)(kWeightParts * sc_max)))) return rc;
-      if ((rc = grow(&e->d_ldp, &e->cap_ldp, (size_t)(kWeightParts * sc_max)))) return rc;
+      const int64_t sets = batch_gemm_i8 ? e->panel_streams : 1;  // one workspace set per panel stream
+      e->ws_G = E * grows + 64;
+      e->ws_U = e->K * grows + 64;
+      e->ws_wp = kWeightParts * sc_max;
+      if ((rc = grow(&e->d_G, &e->cap_G, (size_t)(sets * e->ws_G)))) return rc;
+      if ((rc = grow(&e->d_U, &e->cap_U, (size_t)(sets * e->ws_U)))) return rc;
+      if ((rc = grow(&e->d_q1p, &e->cap_q1p, (size_t)(sets * e->ws_wp)))) return rc;
+      if ((rc = grow(&e->d_ldp, &e->cap_ldp, (size_t)(sets * e->ws_wp)))) return rc;
     }
     if (batch_gemm_i8) {
       if ((rc = grow(&e->d_pi8, &e->cap_pi8, (size_t)chunks))) return rc;
       if ((rc = grow(&e->d_pent, &e->cap_pent, (size_t)nq * 2 * i8_gemm_entries(e->K)))) return rc;
-      if ((rc = grow(&e->d_ai8, &e->cap_ai8,
-                     (size_t)8 * ((sc_max + 127) / 128 * 128) * i8_gemm_kstride(cap_max + 0)))) return rc;
+      e->ws_ai8 = (int64_t)8 * ((sc_max + 127) / 128 * 128) * i8_gemm_kstride(cap_max + 0);
+      if ((rc = grow(&e->d_ai8, &e->cap_ai8, (size_t)(e->panel_streams * e->ws_ai8)))) return rc;
     }
     if (batch_i8) {  // (the fp64 fused kernel transposes its accumulators in registers: no scratch)
       if ((rc = grow(&e->d_scratch, &e->cap_scr, (size_t)blocks_x * nq * kSamplesPerBlock * es))) return rc;

@@ -154,6 +154,10 @@ class Engine:
     def set_stream(self, stream_handle: int | None) -> None:
         L.check(self.lib.gpdla_engine_set_stream(self._h, C.c_void_p(stream_handle or 0)))
 
+    def set_panel_streams(self, n: int) -> None:
+        """int8 panel paths: spectra of a batch alternate over n (1 or 2) compute streams."""
+        L.check(self.lib.gpdla_engine_set_panel_streams(self._h, int(n)))
+
     def stats(self) -> dict:
         s = L.Stats()
         L.check(self.lib.gpdla_engine_get_stats(self._h, C.byref(s)))

@@ -292,3 +292,28 @@ def test_weights_fp32_raw_profile_against_fp64():
     assert worst["oracle64"] < 1e-10, worst          # fp64 profile vs scipy's Faddeeva (measured 1.6e-11)
     assert worst["abs"] < 1e-6, worst                 # fp32: an absorption in [0, 1] to ~2^-20
     assert worst["rel"] < 1e-5, worst                 # and relative where it is not negligible
+
+
+@pytest.mark.parametrize("path", ["panel_gemm_i8", "panel_gemm_i8_24"])
+@pytest.mark.parametrize("batch", [0, 3])
+def test_panel_gemm_i8_two_streams_bitwise(path, batch):
+    """gpdla_engine_set_panel_streams: a batch's spectra alternating over two compute streams (own
+    workspace per stream, forked from and joined into the engine's stream) give bitwise the one-stream
+    results -- ragged spectra in one batch, or batches of 3 (the last one a single spectrum); 1 and 2
+    are the only accepted values."""
+    model = syn.make_model(k=50, seed=11)
+    samples = syn.make_samples(3001)
+    packed = syn.pack_spectra(syn.make_dr12q_like_spectra(model, 7, seed=11, mask_fraction=0.05))
+    with Engine(model, samples, set_parameters(k=50), max_batch_spectra=batch, path=path) as eng:
+        eng.set_panel_streams(1)
+        one = eng.process(packed)
+        eng.set_panel_streams(2)
+        two = eng.process(packed)
+        again = eng.process(packed)
+        for bad in (0, 3):
+            with pytest.raises(L.GpdlaError):
+                eng.set_panel_streams(bad)
+    for key in KEYS:
+        np.testing.assert_array_equal(two[key], one[key])
+        np.testing.assert_array_equal(again[key], one[key])
+    assert np.all(np.isfinite(two["sample_log_likelihoods_dla"]))

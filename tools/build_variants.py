@@ -17,7 +17,7 @@ VARIANTS: dict = {
     "ch16k": {"GPDLA_MAX_CHUNK": 16667},
     "bst_ex2": {"GPDLA_BST_EX": 2},
     "bst_ex8": {"GPDLA_BST_EX": 8},
-    "cur": {"GPDLA_VARIANT_CUR": 1},
+    "cur": {"GPDLA_VARIANT_CUR": 1},     # the working tree as a variant (A/B against the in-tree build)
     "us45": {"GPDLA_BST_USPARE": "0.45f"},
     "us35": {"GPDLA_BST_USPARE": "0.35f"},
     "us40": {"GPDLA_BST_USPARE": "0.40f"},
@@ -25,7 +25,7 @@ VARIANTS: dict = {
     "us25": {"GPDLA_BST_USPARE": "0.25f"},
     "us15": {"GPDLA_BST_USPARE": "0.15f"},
     "us55": {"GPDLA_BST_USPARE": "0.55f"},
-    "us65": {"GPDLA_BST_USPARE": "0.65f"},     # the working tree as a variant (A/B against the in-tree build)
+    "us65": {"GPDLA_BST_USPARE": "0.65f"},
 }
 # variants whose defines only matter in some sources: the rest is linked from the product objects
 ONLY = {n: {"gemm_i8.hip"} for n in ("cur", "us40", "us50", "us15", "us25", "us35", "us45", "us55", "us65")}
