@@ -71,12 +71,14 @@ def i8_roofline(st: dict, n: float, k: int, Q: int, S: int, steps: int, path: st
                     "and u contractions in one launch); the batch adds the weights and LDL^T kernels"}
 
 
-def i8_single_stream(eng, step, n: float, k: int, Q: int, S: int, path: str, steps: int = 2) -> dict:
+def i8_single_stream(eng, step, n: float, k: int, Q: int, S: int, path: str, streams: int = 2,
+                     steps: int = 2) -> dict:
     """The int8 GEMM launch timed with the batch on ONE compute stream, after the timed region (one
-    untimed step, then ``steps`` steps).  In the timed region a batch's spectra alternate over two
-    streams (gpdla_engine_set_panel_streams), so each GEMM launch shares the CUs with the other
-    stream's weights / LDL^T kernels and its HIP-event duration is the overlapped one; this is the
-    kernel's own rate."""
+    untimed step, then ``steps`` steps): the kernel's own rate.  In the timed region a batch's spectra
+    alternate over two streams (gpdla_engine_set_panel_streams), so a GEMM launch shares the CUs with
+    the other stream's weights / LDL^T kernels, and the HIP events around it also count the time it
+    waits in its queue for them (rocprofv3's kernel trace, which times the kernel from its first
+    wave, reads less: profiles/round5/r11c_c5_summary.md)."""
     eng.set_panel_streams(1)
     step()
     eng.synchronize()
@@ -85,13 +87,21 @@ def i8_single_stream(eng, step, n: float, k: int, Q: int, S: int, path: str, ste
         step()
     eng.synchronize()
     st = eng.stats()
-    eng.set_panel_streams(2)
-    r = i8_roofline(st, n, k, Q, S, steps, path)
-    return {"avg_launch_ms": r["avg_launch_ms"], "achieved": r["achieved"], "frac": r["frac"],
-            "whole_batch_ms": r["whole_batch"]["avg_ms"], "steps": steps,
-            "note": "panel streams = 1, measured after the timed region: the GEMM launch without the other "
-                    "stream's kernels beside it (roofline.avg_launch_ms is the overlapped launch of the "
-                    "timed region)"}
+    eng.set_panel_streams(streams)
+    return i8_roofline(st, n, k, Q, S, steps, path)
+
+
+def i8_roofline_two_streams(timed: dict, alone: dict, streams: int = 2) -> dict:
+    """The int8 panel paths' roofline record: the GEMM kernel's own rate (one stream, after the timed
+    region; agrees with a one-stream rocprofv3 trace) and beside it the timed region's overlapped
+    launches.  The batch figures (whole_batch) are the timed region's."""
+    return {**alone, "whole_batch": timed["whole_batch"],
+            "measured": "GEMM launches with the batch on one compute stream, 2 steps after the timed region",
+            "timed_region": {"panel_streams": streams, "avg_launch_ms": timed["avg_launch_ms"],
+                             "achieved": timed["achieved"], "frac": timed["frac"],
+                             "note": "HIP events around each GEMM launch in the timed region, where a batch's "
+                                     "spectra alternate over panel_streams streams: the launch shares the CUs with, and "
+                                     "queues behind, the other streams' weights / LDL^T kernels"}}
 
 
 def f64_gemm_roofline(st: dict, n: float, k: int, Q: int, S: int, steps: int) -> dict:
@@ -329,13 +339,16 @@ def e2e_record(Q: int, S: int, k: int, e2e_dir, keep: bool, world: int, rank: in
 PROFILE_SUMMARY = ROOT / "profiles" / "round5" / "r10k_c2_summary.json"   # configs[1], fused fp64 (round-5 tree)
 # configs[4] (128 spectra x 10^5 samples, k = 50): the summary file and the EXACT names of the roofline
 # kernel's launches (the GEMM launches of one spectrum and sample chunk; per-batch conversion kernels
-# such as convert_gemm_i8_kernel are not part of it)
+# such as convert_gemm_i8_kernel are not part of it).  The int8 paths' summaries are one-stream runs
+# (--panel-streams 1), whose kernel durations are the roofline's one-stream launch time; the trace of
+# the two-stream timed configuration is profiles/round5/r11c_c5_summary.md (PMC bytes per dispatch
+# are the same: the counter passes serialise the kernels)
 PROFILE_SUMMARY_C5 = {
     # the 32-bit path's Gram + u launch is gemm_i8_kernel<4>
-    "panel-GEMM-int8": (ROOT / "profiles" / "round5" / "r10k_c5i8_summary.json",
+    "panel-GEMM-int8": (ROOT / "profiles" / "round5" / "r11d_c5i8s1_summary.json",
                         ("void gpdla::gemm_i8_kernel<4>(gpdla::GemmI8Args)",)),
     # the 24-bit path: Gram and u contractions in one B-stationary launch (round 5)
-    "panel-GEMM-int8-24": (ROOT / "profiles" / "round5" / "r10k_c5_summary.json",
+    "panel-GEMM-int8-24": (ROOT / "profiles" / "round5" / "r11d_c5s1_summary.json",
                            ("gpdla::gemm_i8_bst_kernel(gpdla::GemmI8Args)",)),
     "panel-GEMM": (ROOT / "profiles" / "r5f_c5f64_summary.json", ("gpdla::gemm_f64_kernel(gpdla::GemmF64Args)",)),
 }
@@ -610,12 +623,11 @@ def configs4_alternative(dev: int, steps: int) -> dict:
             "log_likelihoods_no_dla": rel(lln[:sub], ref["log_likelihoods_no_dla"])}
     inv = np.exp(sll - (lld[:sub, None] + np.log(S))).sum(axis=1)
     path = "panel-GEMM-int8-24"
-    roof = i8_roofline(st, n_mean, k, Q, S, steps, path)
+    roof = i8_roofline_two_streams(i8_roofline(st, n_mean, k, Q, S, steps, path), alone)
     traffic, src = profiled_traffic(Q, S, k, path)
-    roof.update({"kernel": ROOFLINE_KERNEL[path], "traffic": traffic, "traffic_source": src,
-                 "single_stream": alone})
+    roof.update({"kernel": ROOFLINE_KERNEL[path], "traffic": traffic, "traffic_source": src})
     # PMC bytes are per dispatch (the counter passes serialise kernels): over the kernel's own time
-    dram = dram_record(traffic, alone["avg_launch_ms"], src, path)
+    dram = dram_record(traffic, roof["avg_launch_ms"], src, path)
     dram["chain"] = chain_dram(path)
     for a in (*t.values(), o_null, o_dla, o_s, o_n):
         a.free()
@@ -732,7 +744,7 @@ def main():
     ap.add_argument("--path", choices=["auto", "fused", "fused_i8", "panel_gemm", "panel_gemm_i8", "panel_gemm_i8_24"], default="auto",
                     help="likelihood path (Engine path=): auto = fused fp64 kernel for the compiled ranks, "
                          "fused_i8 = the int8 Ozaki contraction (k=20), panel_gemm = weights + dgemm + LDL^T")
-    ap.add_argument("--panel-streams", type=int, choices=[1, 2], default=2,
+    ap.add_argument("--panel-streams", type=int, choices=[1, 2, 3, 4], default=2,
                     help="int8 panel paths: compute streams a batch's spectra alternate over")
     ap.add_argument("--no-alt", action="store_true",
                     help="skip the alternative-path measurement (fused_i8 next to the fp64 line, 1 GPU, c2)")
@@ -860,8 +872,8 @@ def main():
     st = eng.stats()
     npix = o_n.numpy()
     n_mean = float(np.mean(npix))
-    alone = (i8_single_stream(eng, step, n_mean, args.k, Q, S, path)
-             if path.startswith("panel-GEMM-int8") and args.panel_streams == 2 else None)
+    alone = (i8_single_stream(eng, step, n_mean, args.k, Q, S, path, args.panel_streams)
+             if path.startswith("panel-GEMM-int8") and args.panel_streams > 1 else None)
 
     # per-rank load balance: each rank's own kernel time and wall time over the timed steps
     per_rank = gather({"rank": rank, "spectra": int(Q), "pixels": int(np.sum(npix)),
@@ -961,7 +973,7 @@ def main():
                else f64_gemm_roofline(st, n_mean, args.k, Q, S, args.steps) if path == "panel-GEMM"
                else {})}
     if alone is not None:
-        roof["single_stream"] = alone
+        roof.update(i8_roofline_two_streams(roof, alone, args.panel_streams))
     rehearsal = world > 1 and distinct < world
     result = {
         "metric": "(spectrum x DLA-sample) log-evidence evals/sec",
@@ -989,7 +1001,7 @@ def main():
                    "spectra_per_gpu": Q, "num_samples": S, "k": args.k, "n_pixels": n_mean,
                    "likelihood_path": path, "parallelism": f"spectrum-shard x{world}"},
         "roofline": roof,
-        "dram": dram_record(traffic, (alone or roof)["avg_launch_ms"], traffic_src, path),
+        "dram": dram_record(traffic, roof["avg_launch_ms"], traffic_src, path),
         "streamed_panel_equiv": {"gbs": eff_gbs, "bytes_per_eval": effective_bytes_per_eval(n_mean, args.k),
                                  "note": "SURVEY.md 8d's streamed-panel accounting (B_eval bytes per evaluation / "
                                          "kernel time): what a kernel re-reading the n x (k+5) panel per sample would "

@@ -166,11 +166,13 @@ struct gpdla_engine {
   // copy_stream while batch b + 1 (resp. b) computes; the two stages alternate
   HostStage hs[2];
   hipStream_t copy_stream = nullptr;
-  // the int8 panel path's second compute stream (panel_streams = 2): odd spectra of a batch run on it,
-  // with their own workspace set, so one spectrum's kernels fill the last-round tails of the other's
+  // the int8 panel path's extra compute streams (panel_streams > 1): spectrum q of a batch runs on
+  // stream q % panel_streams (0 = the engine's stream) with its own workspace set, so one spectrum's
+  // kernels fill the last-round tails of the others'
+  static constexpr int kMaxPanelStreams = 4;
   int panel_streams = 2;
-  hipStream_t panel_stream2 = nullptr;
-  hipEvent_t panel_fork = nullptr, panel_join = nullptr;
+  hipStream_t panel_stream[kMaxPanelStreams] = {};
+  hipEvent_t panel_fork = nullptr, panel_join[kMaxPanelStreams] = {};
   int64_t ws_ai8 = 0, ws_G = 0, ws_U = 0, ws_wp = 0;  // per-set workspace sizes (bytes / doubles)
 
   // pinned host metadata (reused after meta_ready completes)
@@ -276,12 +278,14 @@ void gpdla_engine_destroy(gpdla_engine* e) {
       if (ev) (void)hipEventDestroy(ev);
   }
   if (e->copy_stream) (void)hipStreamDestroy(e->copy_stream);
-  if (e->panel_stream2) {
-    (void)hipStreamSynchronize(e->panel_stream2);
-    (void)hipStreamDestroy(e->panel_stream2);
+  for (int i = 1; i < gpdla_engine::kMaxPanelStreams; ++i) {
+    if (e->panel_stream[i]) {
+      (void)hipStreamSynchronize(e->panel_stream[i]);
+      (void)hipStreamDestroy(e->panel_stream[i]);
+    }
+    if (e->panel_join[i]) (void)hipEventDestroy(e->panel_join[i]);
   }
   if (e->panel_fork) (void)hipEventDestroy(e->panel_fork);
-  if (e->panel_join) (void)hipEventDestroy(e->panel_join);
   void* bufs[] = {e->d_rest, e->d_mu, e->d_M, e->d_logom, e->d_off, e->d_nhi, e->d_perm, e->d_lines,
                   e->d_status, e->d_meta, e->d_wl, e->d_flux, e->d_noise, e->d_mask, e->d_z,
                   e->d_info, e->d_panel, e->d_lam, e->d_smap, e->d_scratch, e->d_sll,
@@ -418,7 +422,8 @@ int gpdla_engine_set_stream(gpdla_engine* e, void* hip_stream) {
 
 int gpdla_engine_set_panel_streams(gpdla_engine* e, int32_t n) {
   if (!e) return set_error(GPDLA_EINVAL, "null engine");
-  if (n != 1 && n != 2) return set_error(GPDLA_EINVAL, "panel streams must be 1 or 2 (got %d)", (int)n);
+  if (n < 1 || n > gpdla_engine::kMaxPanelStreams)
+    return set_error(GPDLA_EINVAL, "panel streams must be 1..%d (got %d)", gpdla_engine::kMaxPanelStreams, (int)n);
   e->panel_streams = n;
   return GPDLA_OK;
 }
@@ -437,20 +442,22 @@ static int run_panel_gemm(gpdla_engine* e, bool i8, int64_t nq, const int64_t* h
   const int K = e->K;
   const int64_t E = (int64_t)K * (K + 1) / 2;
   const int64_t rows = (sc_max + 127) / 128 * 128;
-  // int8 path with two compute streams: spectrum q on stream q % 2 with workspace set q % 2, forked
+  // int8 path with several compute streams: spectrum q on stream q % ns with workspace set q % ns, forked
   // from and joined back into st (the batch's prep / convert before, its reduce after)
-  const bool two = i8 && e->panel_streams == 2 && nq > 1;
-  if (two) {
-    if (!e->panel_stream2) HIP_TRY(hipStreamCreateWithFlags(&e->panel_stream2, hipStreamNonBlocking));
+  const int ns = i8 ? (int)std::min<int64_t>(e->panel_streams, nq) : 1;
+  if (ns > 1) {
     if (!e->panel_fork) HIP_TRY(hipEventCreateWithFlags(&e->panel_fork, hipEventDisableTiming));
-    if (!e->panel_join) HIP_TRY(hipEventCreateWithFlags(&e->panel_join, hipEventDisableTiming));
     HIP_TRY(hipEventRecord(e->panel_fork, st));
-    HIP_TRY(hipStreamWaitEvent(e->panel_stream2, e->panel_fork, 0));
+    for (int i = 1; i < ns; ++i) {
+      if (!e->panel_stream[i]) HIP_TRY(hipStreamCreateWithFlags(&e->panel_stream[i], hipStreamNonBlocking));
+      if (!e->panel_join[i]) HIP_TRY(hipEventCreateWithFlags(&e->panel_join[i], hipEventDisableTiming));
+      HIP_TRY(hipStreamWaitEvent(e->panel_stream[i], e->panel_fork, 0));
+    }
   }
   const hipStream_t st0 = st;
   for (int64_t q = 0; q < nq; ++q) {
-    const int set = two ? (int)(q & 1) : 0;
-    st = set ? e->panel_stream2 : st0;
+    const int set = (int)(q % ns);
+    st = set ? e->panel_stream[set] : st0;
     double *G = e->d_G + set * e->ws_G, *U = e->d_U + set * e->ws_U;
     double *q1p = e->d_q1p + set * e->ws_wp, *ldp = e->d_ldp + set * e->ws_wp;
     for (int64_t s0 = 0; s0 <= e->S; s0 += sc_max) {
@@ -510,9 +517,9 @@ static int run_panel_gemm(gpdla_engine* e, bool i8, int64_t nq, const int64_t* h
       HIP_TRY(launch_ldl_batch(da, st));
     }
   }
-  if (two) {
-    HIP_TRY(hipEventRecord(e->panel_join, e->panel_stream2));
-    HIP_TRY(hipStreamWaitEvent(st0, e->panel_join, 0));
+  for (int i = 1; i < ns; ++i) {
+    HIP_TRY(hipEventRecord(e->panel_join[i], e->panel_stream[i]));
+    HIP_TRY(hipStreamWaitEvent(st0, e->panel_join[i], 0));
   }
   return GPDLA_OK;
 }

@@ -155,7 +155,7 @@ class Engine:
         L.check(self.lib.gpdla_engine_set_stream(self._h, C.c_void_p(stream_handle or 0)))
 
     def set_panel_streams(self, n: int) -> None:
-        """int8 panel paths: spectra of a batch alternate over n (1 or 2) compute streams."""
+        """int8 panel paths: spectra of a batch alternate over n (1..4) compute streams."""
         L.check(self.lib.gpdla_engine_set_panel_streams(self._h, int(n)))
 
     def stats(self) -> dict:

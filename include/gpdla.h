@@ -159,9 +159,10 @@ int gpdla_engine_synchronize(gpdla_engine* engine);
  * call are ordered on that stream (after the work already on it); the host-buffer copies above run on
  * the engine's copy stream, ordered against it by events. */
 int gpdla_engine_set_stream(gpdla_engine* engine, void* hip_stream);
-/* int8 panel-GEMM paths: the number of compute streams (1 or 2, default 2) a batch's spectra
- * alternate over.  With 2, odd spectra run on an engine-owned second stream with their own
- * workspace, forked from and joined back into the engine's stream; results are bitwise identical. */
+/* int8 panel-GEMM paths: the number of compute streams (1..4, default 2) a batch's spectra
+ * alternate over.  Spectrum q of a batch runs on stream q % n (0 = the engine's stream, the others
+ * engine-owned) with a workspace of its own, forked from and joined back into the engine's stream;
+ * results are bitwise identical for every n. */
 int gpdla_engine_set_panel_streams(gpdla_engine* engine, int32_t n);
 int gpdla_engine_get_stats(gpdla_engine* engine, gpdla_stats* stats);
 /* The same, writing at most stats_bytes bytes (a caller's sizeof(gpdla_stats) from an older header). */

@@ -299,8 +299,8 @@ def test_weights_fp32_raw_profile_against_fp64():
 def test_panel_gemm_i8_two_streams_bitwise(path, batch):
     """gpdla_engine_set_panel_streams: a batch's spectra alternating over two compute streams (own
     workspace per stream, forked from and joined into the engine's stream) give bitwise the one-stream
-    results -- ragged spectra in one batch, or batches of 3 (the last one a single spectrum); 1 and 2
-    are the only accepted values."""
+    results -- ragged spectra in one batch, or batches of 3 (the last one a single spectrum); 3 streams
+    likewise; 1..4 are the accepted values."""
     model = syn.make_model(k=50, seed=11)
     samples = syn.make_samples(3001)
     packed = syn.pack_spectra(syn.make_dr12q_like_spectra(model, 7, seed=11, mask_fraction=0.05))
@@ -310,10 +310,14 @@ def test_panel_gemm_i8_two_streams_bitwise(path, batch):
         eng.set_panel_streams(2)
         two = eng.process(packed)
         again = eng.process(packed)
-        for bad in (0, 3):
+        eng.set_panel_streams(3)
+        three = eng.process(packed)
+        eng.set_panel_streams(2)
+        for bad in (0, 5):
             with pytest.raises(L.GpdlaError):
                 eng.set_panel_streams(bad)
     for key in KEYS:
         np.testing.assert_array_equal(two[key], one[key])
         np.testing.assert_array_equal(again[key], one[key])
+        np.testing.assert_array_equal(three[key], one[key])
     assert np.all(np.isfinite(two["sample_log_likelihoods_dla"]))
