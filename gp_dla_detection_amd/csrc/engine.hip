@@ -455,73 +455,79 @@ static int run_panel_gemm(gpdla_engine* e, bool i8, int64_t nq, const int64_t* h
     }
   }
   const hipStream_t st0 = st;
-  for (int64_t q = 0; q < nq; ++q) {
-    const int set = (int)(q % ns);
-    st = set ? e->panel_stream[set] : st0;
-    double *G = e->d_G + set * e->ws_G, *U = e->d_U + set * e->ws_U;
-    double *q1p = e->d_q1p + set * e->ws_wp, *ldp = e->d_ldp + set * e->ws_wp;
-    for (int64_t s0 = 0; s0 <= e->S; s0 += sc_max) {
-      const int32_t sc = (int32_t)std::min<int64_t>(sc_max, e->S + 1 - s0);
-      if (i8) {  // int8 Ozaki contraction (gemm_i8.hip): weights digits -> exact GEMM -> Gram, u
-        const int64_t ks = i8_gemm_kstride(h_cap[q]);
-        const int nd = i8_spectrum_nd(e->i8_nd, h_cap[q]);  // short spectra: 32-bit digits (internal.h)
-        uint8_t* adig = e->d_ai8 + set * e->ws_ai8;
-        WeightsI8Args wi{};
-        wi.info = e->d_info; wi.q = (int32_t)q;
-        wi.srow = e->d_srow + h_sb[q] * 8; wi.lam_pad = e->d_lam + h_lb[q]; wi.kstride = ks;
-        wi.offsets = e->d_off; wi.nhi = e->d_nhi; wi.S = e->S; wi.s0 = s0; wi.sc = sc; wi.rows = rows;
-        wi.lines = make_line_args(e->d_lines); wi.nd = nd; wi.adig = adig; wi.q1p = q1p; wi.ldp = ldp;
-        HIP_TRY(launch_weights_i8(wi, st));
-        GemmI8Args gi{};
-        gi.info = e->d_info; gi.q = (int32_t)q; gi.k = K; gi.kstride = ks; gi.rows = rows; gi.sc = sc; gi.nd = nd;
-        gi.adig = adig; gi.bdig = e->d_pi8 + h_cb[q];
-        gi.ent = e->d_pent + q * 2 * (int64_t)i8_gemm_entries(K); gi.G = G; gi.U = U;
-        // the 24-bit path stores the Gram in fp32 (half the GEMM -> LDL^T round trip; adds ~1e-8
-        // to its ~2e-7 from fp64, tests/support/emulate_i8.py), in the same workspace
-        gi.G32 = nd == 3 ? reinterpret_cast<float*>(G) : nullptr;
-        gi.ks_bound = i8_ks_bound(h_cap[q]);  // slot_cap = 4 ceil(lpix / 4) + 16
-        TimedLaunch tg{};
-        int rc;
-        if ((rc = record_start(e, &tg, 3, st))) return rc;
-        HIP_TRY(launch_gemm_i8(gi, st));
-        HIP_TRY(hipEventRecord(tg.stop, st));
-        e->pending.push_back(tg);
-      } else {
-        WeightsArgs wa{};
-        wa.info = e->d_info; wa.q = (int32_t)q;
-        wa.srow = e->d_srow + h_sb[q] * 8; wa.lam_pad = e->d_lam + h_lb[q]; wa.cap = h_cap[q];
-        wa.offsets = e->d_off; wa.nhi = e->d_nhi; wa.S = e->S; wa.s0 = s0; wa.sc = sc;
-        wa.num_lines = e->params.num_lines; wa.lines = make_line_args(e->d_lines);
-        wa.wg = e->d_wg; wa.wu = e->d_wu; wa.q1p = q1p; wa.ldp = ldp;
-        HIP_TRY(launch_weights(wa, st));
-        // Gram[s][e] = sum_t Wg[t][s] PG[t][e] (the slot-major Khatri-Rao rows), u[s][i] likewise
-        // over the M rows, on the f64 matrix cores (gemm_f64.hip)
-        GemmF64Args ga{};
-        ga.seg[0] = GemmF64Seg{e->d_wg, e->d_panel + h_sb[q] * gemm_ldp(K), gemm_ldp(K), (int32_t)E, G};
-        ga.seg[1] = GemmF64Seg{e->d_wu, e->d_pm + h_sb[q] * gemm_ldm(K), gemm_ldm(K), K, U};
-        ga.nseg = 2;
-        ga.cap = h_cap[q]; ga.cap16 = gemm_f64_cap16(h_cap[q]); ga.sc = sc;
-        TimedLaunch tg{};
-        int rc;
-        if ((rc = record_start(e, &tg, 3))) return rc;
-        HIP_TRY(launch_gemm_f64(ga, st));
-        HIP_TRY(hipEventRecord(tg.stop, st));
-        e->pending.push_back(tg);
+  auto enqueue = [&]() -> int {
+    for (int64_t q = 0; q < nq; ++q) {
+      const int set = (int)(q % ns);
+      st = set ? e->panel_stream[set] : st0;
+      double *G = e->d_G + set * e->ws_G, *U = e->d_U + set * e->ws_U;
+      double *q1p = e->d_q1p + set * e->ws_wp, *ldp = e->d_ldp + set * e->ws_wp;
+      for (int64_t s0 = 0; s0 <= e->S; s0 += sc_max) {
+        const int32_t sc = (int32_t)std::min<int64_t>(sc_max, e->S + 1 - s0);
+        if (i8) {  // int8 Ozaki contraction (gemm_i8.hip): weights digits -> exact GEMM -> Gram, u
+          const int64_t ks = i8_gemm_kstride(h_cap[q]);
+          const int nd = i8_spectrum_nd(e->i8_nd, h_cap[q]);  // short spectra: 32-bit digits (internal.h)
+          uint8_t* adig = e->d_ai8 + set * e->ws_ai8;
+          WeightsI8Args wi{};
+          wi.info = e->d_info; wi.q = (int32_t)q;
+          wi.srow = e->d_srow + h_sb[q] * 8; wi.lam_pad = e->d_lam + h_lb[q]; wi.kstride = ks;
+          wi.offsets = e->d_off; wi.nhi = e->d_nhi; wi.S = e->S; wi.s0 = s0; wi.sc = sc; wi.rows = rows;
+          wi.lines = make_line_args(e->d_lines); wi.nd = nd; wi.adig = adig; wi.q1p = q1p; wi.ldp = ldp;
+          HIP_TRY(launch_weights_i8(wi, st));
+          GemmI8Args gi{};
+          gi.info = e->d_info; gi.q = (int32_t)q; gi.k = K; gi.kstride = ks; gi.rows = rows; gi.sc = sc; gi.nd = nd;
+          gi.adig = adig; gi.bdig = e->d_pi8 + h_cb[q];
+          gi.ent = e->d_pent + q * 2 * (int64_t)i8_gemm_entries(K); gi.G = G; gi.U = U;
+          // the 24-bit path stores the Gram in fp32 (half the GEMM -> LDL^T round trip; adds ~1e-8
+          // to its ~2e-7 from fp64, tests/support/emulate_i8.py), in the same workspace
+          gi.G32 = nd == 3 ? reinterpret_cast<float*>(G) : nullptr;
+          gi.ks_bound = i8_ks_bound(h_cap[q]);  // slot_cap = 4 ceil(lpix / 4) + 16
+          TimedLaunch tg{};
+          int rc;
+          if ((rc = record_start(e, &tg, 3, st))) return rc;
+          HIP_TRY(launch_gemm_i8(gi, st));
+          HIP_TRY(hipEventRecord(tg.stop, st));
+          e->pending.push_back(tg);
+        } else {
+          WeightsArgs wa{};
+          wa.info = e->d_info; wa.q = (int32_t)q;
+          wa.srow = e->d_srow + h_sb[q] * 8; wa.lam_pad = e->d_lam + h_lb[q]; wa.cap = h_cap[q];
+          wa.offsets = e->d_off; wa.nhi = e->d_nhi; wa.S = e->S; wa.s0 = s0; wa.sc = sc;
+          wa.num_lines = e->params.num_lines; wa.lines = make_line_args(e->d_lines);
+          wa.wg = e->d_wg; wa.wu = e->d_wu; wa.q1p = q1p; wa.ldp = ldp;
+          HIP_TRY(launch_weights(wa, st));
+          // Gram[s][e] = sum_t Wg[t][s] PG[t][e] (the slot-major Khatri-Rao rows), u[s][i] likewise
+          // over the M rows, on the f64 matrix cores (gemm_f64.hip)
+          GemmF64Args ga{};
+          ga.seg[0] = GemmF64Seg{e->d_wg, e->d_panel + h_sb[q] * gemm_ldp(K), gemm_ldp(K), (int32_t)E, G};
+          ga.seg[1] = GemmF64Seg{e->d_wu, e->d_pm + h_sb[q] * gemm_ldm(K), gemm_ldm(K), K, U};
+          ga.nseg = 2;
+          ga.cap = h_cap[q]; ga.cap16 = gemm_f64_cap16(h_cap[q]); ga.sc = sc;
+          TimedLaunch tg{};
+          int rc;
+          if ((rc = record_start(e, &tg, 3))) return rc;
+          HIP_TRY(launch_gemm_f64(ga, st));
+          HIP_TRY(hipEventRecord(tg.stop, st));
+          e->pending.push_back(tg);
+        }
+        LdlArgs da{};
+        da.info = e->d_info; da.q = (int32_t)q; da.k = K;
+        da.G = G; da.U = U; da.q1p = q1p; da.ldp = ldp;
+        da.G32 = (i8 && i8_spectrum_nd(e->i8_nd, h_cap[q]) == 3) ? reinterpret_cast<const float*>(G) : nullptr;
+        da.S = e->S; da.s0 = s0; da.sc = sc; da.perm = e->d_perm;
+        da.sample_ll = o_sll ? o_sll + q * ld : nullptr; da.ll_null = o_null + q; da.status = e->d_status;
+        HIP_TRY(launch_ldl_batch(da, st));
       }
-      LdlArgs da{};
-      da.info = e->d_info; da.q = (int32_t)q; da.k = K;
-      da.G = G; da.U = U; da.q1p = q1p; da.ldp = ldp;
-      da.G32 = (i8 && i8_spectrum_nd(e->i8_nd, h_cap[q]) == 3) ? reinterpret_cast<const float*>(G) : nullptr;
-      da.S = e->S; da.s0 = s0; da.sc = sc; da.perm = e->d_perm;
-      da.sample_ll = o_sll ? o_sll + q * ld : nullptr; da.ll_null = o_null + q; da.status = e->d_status;
-      HIP_TRY(launch_ldl_batch(da, st));
     }
-  }
+    return GPDLA_OK;
+  };
+  const int rc = enqueue();
+  // joined even after a failed enqueue: later work on st0 (the next batch reusing the workspace sets,
+  // the engine's synchronize) stays ordered after everything already on the other streams
   for (int i = 1; i < ns; ++i) {
     HIP_TRY(hipEventRecord(e->panel_join[i], e->panel_stream[i]));
     HIP_TRY(hipStreamWaitEvent(st0, e->panel_join[i], 0));
   }
-  return GPDLA_OK;
+  return rc;
 }
 
 // The host-buffer pipeline's stages, sized for the largest batch of this call (no reallocation
