@@ -71,14 +71,13 @@ def i8_roofline(st: dict, n: float, k: int, Q: int, S: int, steps: int, path: st
                     "and u contractions in one launch); the batch adds the weights and LDL^T kernels"}
 
 
-def i8_single_stream(eng, step, n: float, k: int, Q: int, S: int, path: str, streams: int = 2,
-                     steps: int = 2) -> dict:
-    """The int8 GEMM launch timed with the batch on ONE compute stream, after the timed region (one
-    untimed step, then ``steps`` steps): the kernel's own rate.  In the timed region a batch's spectra
-    alternate over two streams (gpdla_engine_set_panel_streams), so a GEMM launch shares the CUs with
-    the other stream's weights / LDL^T kernels, and the HIP events around it also count the time it
-    waits in its queue for them (rocprofv3's kernel trace, which times the kernel from its first
-    wave, reads less: profiles/round5/r11c_c5_summary.md)."""
+def single_stream_stats(eng, step, streams: int = 2, steps: int = 2) -> dict:
+    """Engine stats of ``steps`` steps with the batch on ONE compute stream, after the timed region (one
+    untimed step first), for the panel paths' GEMM launch at its own rate.  In the timed region a
+    batch's spectra alternate over two streams (gpdla_engine_set_panel_streams), so a GEMM launch
+    shares the CUs with the other stream's weights / LDL^T kernels, and the HIP events around it also
+    count the time it waits in its queue for them (rocprofv3's kernel trace, which times the kernel
+    from its first wave, reads less: profiles/round5/r11c_c5_summary.md)."""
     eng.set_panel_streams(1)
     step()
     eng.synchronize()
@@ -88,14 +87,16 @@ def i8_single_stream(eng, step, n: float, k: int, Q: int, S: int, path: str, str
     eng.synchronize()
     st = eng.stats()
     eng.set_panel_streams(streams)
-    return i8_roofline(st, n, k, Q, S, steps, path)
+    return st
 
 
-def i8_roofline_two_streams(timed: dict, alone: dict, streams: int = 2) -> dict:
-    """The int8 panel paths' roofline record: the GEMM kernel's own rate (one stream, after the timed
+def panel_roofline_streams(timed: dict, alone: dict, streams: int = 2) -> dict:
+    """The panel paths' roofline record: the GEMM kernel's own rate (one stream, after the timed
     region; agrees with a one-stream rocprofv3 trace) and beside it the timed region's overlapped
-    launches.  The batch figures (whole_batch) are the timed region's."""
-    return {**alone, "whole_batch": timed["whole_batch"],
+    launches.  The batch figures (whole_batch, int8 paths) are the timed region's."""
+    if "avg_launch_ms" not in timed or "avg_launch_ms" not in alone:
+        return timed
+    return {**alone, **({"whole_batch": timed["whole_batch"]} if "whole_batch" in timed else {}),
             "measured": "GEMM launches with the batch on one compute stream, 2 steps after the timed region",
             "timed_region": {"panel_streams": streams, "avg_launch_ms": timed["avg_launch_ms"],
                              "achieved": timed["achieved"], "frac": timed["frac"],
@@ -611,7 +612,7 @@ def configs4_alternative(dev: int, steps: int) -> dict:
         el = time.perf_counter() - t0
         st = eng.stats()
         n_mean = float(np.mean(o_n.numpy()))
-        alone = i8_single_stream(eng, step, n_mean, k, Q, S, "panel-GEMM-int8-24")
+        alone = i8_roofline(single_stream_stats(eng, step), n_mean, k, Q, S, 2, "panel-GEMM-int8-24")
     sub = 8
     with Engine(model, samples, set_parameters(k=k), device=dev, path="panel_gemm") as e64:
         ref = e64.process(syn.pack_spectra(spectra[:sub]))
@@ -623,7 +624,7 @@ def configs4_alternative(dev: int, steps: int) -> dict:
             "log_likelihoods_no_dla": rel(lln[:sub], ref["log_likelihoods_no_dla"])}
     inv = np.exp(sll - (lld[:sub, None] + np.log(S))).sum(axis=1)
     path = "panel-GEMM-int8-24"
-    roof = i8_roofline_two_streams(i8_roofline(st, n_mean, k, Q, S, steps, path), alone)
+    roof = panel_roofline_streams(i8_roofline(st, n_mean, k, Q, S, steps, path), alone)
     traffic, src = profiled_traffic(Q, S, k, path)
     roof.update({"kernel": ROOFLINE_KERNEL[path], "traffic": traffic, "traffic_source": src})
     # PMC bytes are per dispatch (the counter passes serialise kernels): over the kernel's own time
@@ -745,7 +746,7 @@ def main():
                     help="likelihood path (Engine path=): auto = fused fp64 kernel for the compiled ranks, "
                          "fused_i8 = the int8 Ozaki contraction (k=20), panel_gemm = weights + dgemm + LDL^T")
     ap.add_argument("--panel-streams", type=int, choices=[1, 2, 3, 4], default=2,
-                    help="int8 panel paths: compute streams a batch's spectra alternate over")
+                    help="panel-GEMM paths: compute streams a batch's spectra alternate over")
     ap.add_argument("--no-alt", action="store_true",
                     help="skip the alternative-path measurement (fused_i8 next to the fp64 line, 1 GPU, c2)")
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU-baseline work (0 = skip)")
@@ -845,8 +846,7 @@ def main():
     if args.path == "auto" and "default_path" in wl:
         args.path = wl["default_path"]
     eng = Engine(model, samples, set_parameters(k=args.k), device=dev, path=args.path)
-    if args.path.startswith("panel_gemm_i8"):
-        eng.set_panel_streams(args.panel_streams)
+    eng.set_panel_streams(args.panel_streams)    # the panel paths' compute streams (others ignore it)
     if args.path == "fused_i8":
         path = "fused-int8"
     elif args.path == "panel_gemm_i8":
@@ -872,8 +872,11 @@ def main():
     st = eng.stats()
     npix = o_n.numpy()
     n_mean = float(np.mean(npix))
-    alone = (i8_single_stream(eng, step, n_mean, args.k, Q, S, path, args.panel_streams)
-             if path.startswith("panel-GEMM-int8") and args.panel_streams > 1 else None)
+    alone = None
+    if path.startswith("panel-GEMM") and args.panel_streams > 1:
+        st1 = single_stream_stats(eng, step, args.panel_streams)
+        alone = (i8_roofline(st1, n_mean, args.k, Q, S, 2, path) if path.startswith("panel-GEMM-int8")
+                 else f64_gemm_roofline(st1, n_mean, args.k, Q, S, 2))
 
     # per-rank load balance: each rank's own kernel time and wall time over the timed steps
     per_rank = gather({"rank": rank, "spectra": int(Q), "pixels": int(np.sum(npix)),
@@ -973,7 +976,7 @@ def main():
                else f64_gemm_roofline(st, n_mean, args.k, Q, S, args.steps) if path == "panel-GEMM"
                else {})}
     if alone is not None:
-        roof.update(i8_roofline_two_streams(roof, alone, args.panel_streams))
+        roof.update(panel_roofline_streams(roof, alone, args.panel_streams))
     rehearsal = world > 1 and distinct < world
     result = {
         "metric": "(spectrum x DLA-sample) log-evidence evals/sec",

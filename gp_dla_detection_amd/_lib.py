@@ -81,6 +81,7 @@ SIGNATURES = {
     "gpdla_engine_synchronize": (C.c_int, [C.c_void_p]),
     "gpdla_engine_set_stream": (C.c_int, [C.c_void_p, C.c_void_p]),
     "gpdla_engine_set_panel_streams": (C.c_int, [C.c_void_p, C.c_int32]),
+    "gpdla_engine_use_null_stream": (C.c_int, [C.c_void_p]),
     "gpdla_engine_get_stats": (C.c_int, [C.c_void_p, C.POINTER(Stats)]),
     "gpdla_engine_get_stats_n": (C.c_int, [C.c_void_p, C.POINTER(Stats), C.c_int64]),
     "gpdla_engine_reset_stats": (C.c_int, [C.c_void_p]),

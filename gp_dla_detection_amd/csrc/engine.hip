@@ -166,14 +166,14 @@ struct gpdla_engine {
   // copy_stream while batch b + 1 (resp. b) computes; the two stages alternate
   HostStage hs[2];
   hipStream_t copy_stream = nullptr;
-  // the int8 panel path's extra compute streams (panel_streams > 1): spectrum q of a batch runs on
+  // the panel-GEMM paths' extra compute streams (panel_streams > 1): spectrum q of a batch runs on
   // stream q % panel_streams (0 = the engine's stream) with its own workspace set, so one spectrum's
   // kernels fill the last-round tails of the others'
   static constexpr int kMaxPanelStreams = 4;
   int panel_streams = 2;
   hipStream_t panel_stream[kMaxPanelStreams] = {};
   hipEvent_t panel_fork = nullptr, panel_join[kMaxPanelStreams] = {};
-  int64_t ws_ai8 = 0, ws_G = 0, ws_U = 0, ws_wp = 0;  // per-set workspace sizes (bytes / doubles)
+  int64_t ws_ai8 = 0, ws_G = 0, ws_U = 0, ws_wp = 0, ws_w = 0;  // per-set workspace sizes (bytes / doubles)
 
   // pinned host metadata (reused after meta_ready completes)
   int64_t* h_meta = nullptr;
@@ -267,7 +267,7 @@ int gpdla_diag_line_table_error(int32_t line, double* max_rel_err) {
 void gpdla_engine_destroy(gpdla_engine* e) {
   if (!e) return;
   (void)hipSetDevice(e->device);
-  if (e->stream) (void)hipStreamSynchronize(e->stream);
+  (void)hipStreamSynchronize(e->stream);  // (the null stream too)
   if (e->copy_stream) (void)hipStreamSynchronize(e->copy_stream);
   for (auto& t : e->pending) { (void)hipEventDestroy(t.start); (void)hipEventDestroy(t.stop); }
   for (HostStage& h : e->hs) {
@@ -420,6 +420,14 @@ int gpdla_engine_set_stream(gpdla_engine* e, void* hip_stream) {
   return GPDLA_OK;
 }
 
+int gpdla_engine_use_null_stream(gpdla_engine* e) {
+  if (!e) return set_error(GPDLA_EINVAL, "null engine");
+  HIP_TRY(hipSetDevice(e->device));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  e->stream = nullptr;  // the null stream (HIP's stream 0)
+  return GPDLA_OK;
+}
+
 int gpdla_engine_set_panel_streams(gpdla_engine* e, int32_t n) {
   if (!e) return set_error(GPDLA_EINVAL, "null engine");
   if (n < 1 || n > gpdla_engine::kMaxPanelStreams)
@@ -431,7 +439,7 @@ int gpdla_engine_set_panel_streams(gpdla_engine* e, int32_t n) {
 // Panel-GEMM path for one batch: per spectrum and chunk of samples, weights -> GEMM on the matrix
 // cores (int8 digits, gemm_i8.hip, or fp64, gemm_f64.hip) -> batched LDL^T (gemm_path.hip), in
 // stream order.
-// int8 paths: a batch's spectra alternate over two streams (gpdla_engine_set_panel_streams), which
+// A batch's spectra alternate over two streams (gpdla_engine_set_panel_streams), which
 // fills the last partial round of each spectrum's weights / LDL^T launches with the other spectrum's
 // work: +3.6% on configs[4] (profiles/round5/ab/r11a).  (Earlier second-stream layouts, within one
 // spectrum, measured no gain: the LDL^T beside the next chunk's weights and GEMM, 0% with the
@@ -442,9 +450,9 @@ static int run_panel_gemm(gpdla_engine* e, bool i8, int64_t nq, const int64_t* h
   const int K = e->K;
   const int64_t E = (int64_t)K * (K + 1) / 2;
   const int64_t rows = (sc_max + 127) / 128 * 128;
-  // int8 path with several compute streams: spectrum q on stream q % ns with workspace set q % ns, forked
+  // several compute streams: spectrum q on stream q % ns with workspace set q % ns, forked
   // from and joined back into st (the batch's prep / convert before, its reduce after)
-  const int ns = i8 ? (int)std::min<int64_t>(e->panel_streams, nq) : 1;
+  const int ns = (int)std::min<int64_t>(e->panel_streams, nq);
   if (ns > 1) {
     if (!e->panel_fork) HIP_TRY(hipEventCreateWithFlags(&e->panel_fork, hipEventDisableTiming));
     HIP_TRY(hipEventRecord(e->panel_fork, st));
@@ -493,18 +501,19 @@ static int run_panel_gemm(gpdla_engine* e, bool i8, int64_t nq, const int64_t* h
           wa.srow = e->d_srow + h_sb[q] * 8; wa.lam_pad = e->d_lam + h_lb[q]; wa.cap = h_cap[q];
           wa.offsets = e->d_off; wa.nhi = e->d_nhi; wa.S = e->S; wa.s0 = s0; wa.sc = sc;
           wa.num_lines = e->params.num_lines; wa.lines = make_line_args(e->d_lines);
-          wa.wg = e->d_wg; wa.wu = e->d_wu; wa.q1p = q1p; wa.ldp = ldp;
+          double *wg = e->d_wg + set * e->ws_w, *wu = e->d_wu + set * e->ws_w;
+          wa.wg = wg; wa.wu = wu; wa.q1p = q1p; wa.ldp = ldp;
           HIP_TRY(launch_weights(wa, st));
           // Gram[s][e] = sum_t Wg[t][s] PG[t][e] (the slot-major Khatri-Rao rows), u[s][i] likewise
           // over the M rows, on the f64 matrix cores (gemm_f64.hip)
           GemmF64Args ga{};
-          ga.seg[0] = GemmF64Seg{e->d_wg, e->d_panel + h_sb[q] * gemm_ldp(K), gemm_ldp(K), (int32_t)E, G};
-          ga.seg[1] = GemmF64Seg{e->d_wu, e->d_pm + h_sb[q] * gemm_ldm(K), gemm_ldm(K), K, U};
+          ga.seg[0] = GemmF64Seg{wg, e->d_panel + h_sb[q] * gemm_ldp(K), gemm_ldp(K), (int32_t)E, G};
+          ga.seg[1] = GemmF64Seg{wu, e->d_pm + h_sb[q] * gemm_ldm(K), gemm_ldm(K), K, U};
           ga.nseg = 2;
           ga.cap = h_cap[q]; ga.cap16 = gemm_f64_cap16(h_cap[q]); ga.sc = sc;
           TimedLaunch tg{};
           int rc;
-          if ((rc = record_start(e, &tg, 3))) return rc;
+          if ((rc = record_start(e, &tg, 3, st))) return rc;
           HIP_TRY(launch_gemm_f64(ga, st));
           HIP_TRY(hipEventRecord(tg.stop, st));
           e->pending.push_back(tg);
@@ -683,8 +692,10 @@ int gpdla_engine_process(gpdla_engine* e, const gpdla_spectra* sp, const gpdla_r
       size_t free_b = 0, total_b = 0;
       HIP_TRY(hipMemGetInfo(&free_b, &total_b));
       const int64_t budget = (int64_t)std::min<size_t>(free_b / 4, (size_t)16 << 30);
-      const int64_t per_sample = (batch_gemm_i8 ? 8 * i8_gemm_kstride(cap_max) : 16 * gemm_f64_cap16(cap_max)) +
-                                 8 * (E + e->K + 2 * kWeightParts);
+      // (one workspace set per panel stream)
+      const int64_t per_sample = e->panel_streams *
+                                 ((batch_gemm_i8 ? 8 * i8_gemm_kstride(cap_max) : 16 * gemm_f64_cap16(cap_max)) +
+                                  8 * (E + e->K + 2 * kWeightParts));
       const int64_t fit = std::max<int64_t>(128, budget / std::max<int64_t>(per_sample, 1) / 128 * 128);
       const int64_t cmax = std::min<int64_t>(kMaxChunk, fit);
       const int64_t nchunk = (e->S + 1 + cmax - 1) / cmax;
@@ -705,16 +716,16 @@ int gpdla_engine_process(gpdla_engine* e, const gpdla_spectra* sp, const gpdla_r
       HIP_TRY(hipMemsetAsync(e->d_panel + slots * row, 0, gemm_panel_slack(row) * 8, st));
       HIP_TRY(hipMemsetAsync(e->d_pm + slots * ldm, 0, gemm_panel_slack(ldm) * 8, st));
       if ((rc = grow(&e->d_srow, &e->cap_srow, (size_t)slots * 8))) return rc;
+      const int64_t sets = e->panel_streams;  // one workspace set per panel stream
       if (!batch_gemm_i8) {  // the fp64 weight tiles: only the fp64 GEMM reads them
-        const size_t wbytes = (size_t)(gemm_f64_cap16(cap_max) * gemm_f64_rows(sc_max));
-        if ((rc = grow(&e->d_wg, &e->cap_wg, wbytes))) return rc;
-        if ((rc = grow(&e->d_wu, &e->cap_wu, wbytes))) return rc;
+        e->ws_w = gemm_f64_cap16(cap_max) * gemm_f64_rows(sc_max);
+        if ((rc = grow(&e->d_wg, &e->cap_wg, (size_t)(sets * e->ws_w)))) return rc;
+        if ((rc = grow(&e->d_wu, &e->cap_wu, (size_t)(sets * e->ws_w)))) return rc;
       }
       // the GEMMs store whole 128-sample tiles (quad_index layout, internal.h); + 64 elements of
       // slack: ldl_mfma_kernel's straight-line tile loads may address one entry past the last
       // sample's Gram when k is a multiple of 4 (the value is discarded)
       const int64_t grows = gemm_f64_rows(sc_max);
-      const int64_t sets = batch_gemm_i8 ? e->panel_streams : 1;  // one workspace set per panel stream
       e->ws_G = E * grows + 64;
       e->ws_U = e->K * grows + 64;
       e->ws_wp = kWeightParts * sc_max;

@@ -152,10 +152,17 @@ class Engine:
         L.check(self.lib.gpdla_engine_synchronize(self._h))
 
     def set_stream(self, stream_handle: int | None) -> None:
-        L.check(self.lib.gpdla_engine_set_stream(self._h, C.c_void_p(stream_handle or 0)))
+        """Order the engine's kernels on an external hipStream_t handle (e.g. torch's
+        ``current_stream().cuda_stream``); None restores the engine's own stream.  Handle 0 is the
+        null stream (torch's default stream): gpdla_engine_use_null_stream, since the C ABI reads a
+        NULL handle as "restore"."""
+        if stream_handle == 0:
+            L.check(self.lib.gpdla_engine_use_null_stream(self._h))
+        else:
+            L.check(self.lib.gpdla_engine_set_stream(self._h, C.c_void_p(stream_handle or 0)))
 
     def set_panel_streams(self, n: int) -> None:
-        """int8 panel paths: spectra of a batch alternate over n (1..4) compute streams."""
+        """Panel-GEMM paths: spectra of a batch alternate over n (1..4) compute streams."""
         L.check(self.lib.gpdla_engine_set_panel_streams(self._h, int(n)))
 
     def stats(self) -> dict:

@@ -155,11 +155,15 @@ int gpdla_engine_process(gpdla_engine* engine, const gpdla_spectra* spectra,
                          const gpdla_results* results);
 /* Wait for enqueued work; returns GPDLA_ENUMERIC if any pivot was non-positive since the last call. */
 int gpdla_engine_synchronize(gpdla_engine* engine);
-/* Use an external hipStream_t (NULL restores the engine's own stream).  All kernels of a process
+/* Use an external hipStream_t (NULL restores the engine's own stream; the null stream itself is
+ * selected by gpdla_engine_use_null_stream).  All kernels of a process
  * call are ordered on that stream (after the work already on it); the host-buffer copies above run on
  * the engine's copy stream, ordered against it by events. */
 int gpdla_engine_set_stream(gpdla_engine* engine, void* hip_stream);
-/* int8 panel-GEMM paths: the number of compute streams (1..4, default 2) a batch's spectra
+/* Order the kernels on the null stream (stream 0, e.g. PyTorch's default stream), as
+ * gpdla_engine_set_stream does for any other stream. */
+int gpdla_engine_use_null_stream(gpdla_engine* engine);
+/* Panel-GEMM paths (fp64 and int8): the number of compute streams (1..4, default 2) a batch's spectra
  * alternate over.  Spectrum q of a batch runs on stream q % n (0 = the engine's stream, the others
  * engine-owned) with a workspace of its own, forked from and joined back into the engine's stream;
  * results are bitwise identical for every n. */

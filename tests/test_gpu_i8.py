@@ -294,9 +294,9 @@ def test_weights_fp32_raw_profile_against_fp64():
     assert worst["rel"] < 1e-5, worst                 # and relative where it is not negligible
 
 
-@pytest.mark.parametrize("path", ["panel_gemm_i8", "panel_gemm_i8_24"])
+@pytest.mark.parametrize("path", ["panel_gemm", "panel_gemm_i8", "panel_gemm_i8_24"])
 @pytest.mark.parametrize("batch", [0, 3])
-def test_panel_gemm_i8_two_streams_bitwise(path, batch):
+def test_panel_gemm_two_streams_bitwise(path, batch):
     """gpdla_engine_set_panel_streams: a batch's spectra alternating over two compute streams (own
     workspace per stream, forked from and joined into the engine's stream) give bitwise the one-stream
     results -- ragged spectra in one batch, or batches of 3 (the last one a single spectrum); 3 streams

@@ -327,15 +327,25 @@ t = {k: torch.from_numpy(np.ascontiguousarray(packed[k])).to(dev)
      for k in ('wavelengths', 'flux', 'noise_variance', 'pixel_mask', 'z_qsos')}
 o_null = torch.empty(3, dtype=torch.float64, device=dev); o_dla = torch.empty_like(o_null)
 o_s = torch.empty((3, 200), dtype=torch.float64, device=dev)
-with Engine(model, samples, set_parameters(k=20)) as eng:
-    host = eng.process(packed)
-    eng.set_stream(torch.cuda.current_stream(dev).cuda_stream)
-    eng.process_device(packed['offsets'], t['wavelengths'].data_ptr(), t['flux'].data_ptr(),
-                       t['noise_variance'].data_ptr(), t['pixel_mask'].data_ptr(), t['z_qsos'].data_ptr(),
-                       o_null.data_ptr(), o_dla.data_ptr(), o_s.data_ptr(), 200)
-    eng.synchronize()
-assert np.array_equal(o_s.cpu().numpy(), host['sample_log_likelihoods_dla'])
-assert np.array_equal(o_dla.cpu().numpy(), host['log_likelihoods_dla'])
+# the fused path, and the int8 panel path whose spectra alternate over two streams forked from and
+# joined into torch's stream; torch's default (null) stream and a side stream.  The torch ops after
+# the call are ordered on torch's stream only and must see every spectrum's results.
+side = torch.cuda.Stream(dev)
+side.wait_stream(torch.cuda.default_stream(dev))   # the inputs above were uploaded on the default stream
+for path in ('auto', 'panel_gemm_i8_24'):
+    for ts in (torch.cuda.default_stream(dev), side):
+        with torch.cuda.stream(ts), Engine(model, samples, set_parameters(k=20), path=path) as eng:
+            host = eng.process(packed)
+            o_s.fill_(7.0)
+            o_dla.fill_(7.0)
+            eng.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+            eng.process_device(packed['offsets'], t['wavelengths'].data_ptr(), t['flux'].data_ptr(),
+                               t['noise_variance'].data_ptr(), t['pixel_mask'].data_ptr(), t['z_qsos'].data_ptr(),
+                               o_null.data_ptr(), o_dla.data_ptr(), o_s.data_ptr(), 200)
+            got_s, got_dla = o_s.cpu().numpy(), o_dla.cpu().numpy()
+            eng.synchronize()
+        assert np.array_equal(got_s, host['sample_log_likelihoods_dla']), (path, ts)
+        assert np.array_equal(got_dla, host['log_likelihoods_dla']), (path, ts)
 libs = {l.split()[-1] for l in open('/proc/self/maps') if 'libamdhip64' in l}
 assert len(libs) == 1, libs
 print('torch interop ok', libs)
@@ -343,7 +353,8 @@ print('torch interop ok', libs)
 
 
 def test_torch_tensor_interop():
-    """PyTorch tensors as engine buffers: torch imported first so the process holds ONE HIP runtime
+    """PyTorch tensors as engine buffers, the engine on torch's stream (fused path, and the int8 panel
+    path with its two compute streams): torch imported first so the process holds ONE HIP runtime
     (torch ships its own libamdhip64 with the same SONAME)."""
     import subprocess
     import sys
