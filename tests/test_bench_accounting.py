@@ -44,6 +44,23 @@ def test_i8_roofline_uses_the_gemm_launches(bench):
     assert r["whole_batch"]["avg_ms"] == 15.0
 
 
+def test_panel_roofline_streams_record(bench):
+    """With two panel streams the roofline is the GEMM's one-stream launch (measured after the timed
+    region) and the timed region's overlapped launches sit beside it; the batch figures stay the timed
+    region's.  A record without launch timing passes through unchanged."""
+    st2 = {"contraction_ms": 32.0, "contraction_launches": 20, "likelihood_ms": 28.0, "likelihood_launches": 2}
+    st1 = {"contraction_ms": 2.0, "contraction_launches": 2, "likelihood_ms": 16.0, "likelihood_launches": 1}
+    timed = bench.i8_roofline(st2, 800, 50, Q=10, S=99, steps=2, path="panel-GEMM-int8-24")
+    alone = bench.i8_roofline(st1, 800, 50, Q=1, S=99, steps=2, path="panel-GEMM-int8-24")
+    r = bench.panel_roofline_streams(timed, alone, 2)
+    assert r["avg_launch_ms"] == 1.0 and r["frac"] == alone["frac"]
+    assert r["timed_region"]["avg_launch_ms"] == 1.6 and r["timed_region"]["panel_streams"] == 2
+    assert r["timed_region"]["frac"] == pytest.approx(timed["frac"]) and r["frac"] > r["timed_region"]["frac"]
+    assert r["whole_batch"] == timed["whole_batch"]
+    f64 = bench.f64_gemm_roofline({**st1, "contraction_launches": 0}, 800, 50, 1, 99, 2)
+    assert bench.panel_roofline_streams(f64, alone) is f64
+
+
 def test_profiled_traffic_lookup(bench):
     """Every bench workload's roofline traffic comes from the committed summary bench.py names, summed
     over that path's roofline-kernel launches; other shapes claim no profiled number."""
