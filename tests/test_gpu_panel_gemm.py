@@ -1,9 +1,9 @@
-"""GPU parity of the panel-GEMM path (weights kernel + rocBLAS dgemm + batched LDL^T), the path
+"""GPU parity of the panel-GEMM path (weights kernel + hand-written fp64 Gram/u GEMM + batched LDL^T), the path
 for ranks the fused kernel is not compiled for -- BASELINE configs[4] (k = 50, 10^5 samples).
 
 Checks: the committed golden fixtures through the forced panel-GEMM path; agreement with the fused
-path on identical inputs; k = 50 against the oracle; sample chunking across the 16384-sample
-chunk boundary; the edge cases of the fused-path suite.  Tolerance as in test_gpu_parity.py:
+path on identical inputs; k = 50 against the oracle; sample chunking across the sample-chunk
+boundary (GPDLA_MAX_CHUNK); the edge cases of the fused-path suite.  Tolerance as in test_gpu_parity.py:
 |got - ref| <= 1e-6 max(|ref|, 1) (contract), and a 1e-9 bar to catch precision regressions."""
 import numpy as np
 import pytest
@@ -93,17 +93,34 @@ def test_high_rank_ldl_buckets_match_oracle(k):
                 assert err < tol, (path, k, key, err)
 
 
+def _max_chunk() -> int:
+    """The panel paths' sample chunk bound, GPDLA_MAX_CHUNK in csrc/tuning.h (the source of the build)."""
+    import re
+    from pathlib import Path
+    txt = (Path(__file__).resolve().parents[1] / "gp_dla_detection_amd" / "csrc" / "tuning.h").read_text()
+    return int(re.search(r"#define GPDLA_MAX_CHUNK (\d+)", txt).group(1))
+
+
 def test_sample_chunk_boundaries():
-    """S + 1 = 16685 spans two sample chunks (<= 16384 each); compare with the fused path (k = 8)."""
+    """S + 1 = 140,001 samples span two sample chunks (at most GPDLA_MAX_CHUNK = 131,072 each, so two
+    of 70,001): the fp64 panel path against the fused path (k = 8), and both int8 panel paths, whose
+    3 spectra alternate over the two panel streams, against the fp64 panel path at their bars."""
+    S = 140000
+    assert _max_chunk() < S + 1 <= 2 * _max_chunk()
     model = syn.make_model(k=8, seed=8)
-    samples = syn.make_samples(16684)
-    packed = syn.pack_spectra(syn.make_dr12q_like_spectra(model, 2, seed=9, mask_fraction=0.05))
+    samples = syn.make_samples(S)
+    packed = syn.pack_spectra(syn.make_dr12q_like_spectra(model, 3, seed=9, mask_fraction=0.05))
     with Engine(model, samples, set_parameters(k=8), path="fused") as eng:
         fused = eng.process(packed)
     with Engine(model, samples, set_parameters(k=8), path="panel_gemm") as eng:
         gemm = eng.process(packed)
     for key in KEYS:
         assert _rel_err(gemm[key], fused[key]) < 1e-11, (key, _rel_err(gemm[key], fused[key]))
+    for path, tol in (("panel_gemm_i8", 1e-8), ("panel_gemm_i8_24", 5e-7)):
+        with Engine(model, samples, set_parameters(k=8), path=path) as eng:
+            out = eng.process(packed)
+        for key in KEYS:
+            assert _rel_err(out[key], gemm[key]) < tol, (path, key, _rel_err(out[key], gemm[key]))
 
 
 def test_panel_gemm_edge_cases():
