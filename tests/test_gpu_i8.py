@@ -150,7 +150,7 @@ def test_i8_long_spectrum_batch_falls_back_to_fp64():
 
 def test_panel_gemm_i8_long_spectrum_batch_falls_back_to_fp64():
     """The same kI8MaxSlots guard on the int8 panel-GEMM path (gemm_i8.hip): the batch holding a
-    30,500-pixel spectrum runs the fp64 weights + dgemm + LDL^T, bit-identical to path='panel_gemm'."""
+    30,500-pixel spectrum runs the fp64 weights + fp64 GEMM + LDL^T, bit-identical to path='panel_gemm'."""
     model = syn.make_model(k=20)
     samples = syn.make_samples(64)
     base = syn.make_spectrum(model, 1)
