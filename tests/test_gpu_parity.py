@@ -147,6 +147,30 @@ def test_edge_cases_small_and_empty():
         assert np.all(np.isnan(out["sample_log_likelihoods_dla"][-1]))
 
 
+@pytest.mark.parametrize("S", [1, 2])
+@pytest.mark.parametrize("path,tol", [("fused", 1e-9), ("panel_gemm", 1e-9), ("fused_i8", 1e-8),
+                                      ("panel_gemm_i8", 1e-8), ("panel_gemm_i8_24", 5e-7)])
+def test_one_and_two_dla_samples(S, path, tol):
+    """num_dla_samples of 1 and 2 (process_qsos.m:184-212 with S = 1, 2) on every likelihood path:
+    the 64-sample blocks, 128-sample GEMM tiles and 16-sample LDL^T blocks almost empty, against the
+    oracle; with one sample the log-mean-exp is that sample's value exactly (:202-209)."""
+    from oracle import gpdla_oracle as O
+    model = syn.make_model(k=20, seed=S)
+    samples = syn.make_samples(S)
+    spectra = syn.make_dr12q_like_spectra(model, 3, seed=S, mask_fraction=0.05)
+    with Engine(model, samples, set_parameters(k=20), path=path) as eng:
+        out = eng.process(syn.pack_spectra(spectra))
+    assert out["sample_log_likelihoods_dla"].shape == (3, S)
+    for q, sp in enumerate(spectra):
+        ref = O.process_spectrum(sp["wavelengths"], sp["flux"], sp["noise_variance"], sp["pixel_mask"],
+                                 sp["z_qso"], model, samples["offset_samples"], samples["nhi_samples"])
+        assert _rel_err(out["sample_log_likelihoods_dla"][q], ref["sample_log_likelihoods_dla"]) < tol, (path, q)
+        assert _rel_err(out["log_likelihoods_no_dla"][q], ref["log_likelihood_no_dla"]) < tol, (path, q)
+        assert _rel_err(out["log_likelihoods_dla"][q], ref["log_likelihood_dla"]) < tol, (path, q)
+    if S == 1:
+        np.testing.assert_array_equal(out["log_likelihoods_dla"], out["sample_log_likelihoods_dla"][:, 0])
+
+
 @pytest.mark.parametrize("k", [4, 10, 16, 24])
 def test_other_ranks(k):
     from oracle import gpdla_oracle as O
