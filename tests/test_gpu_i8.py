@@ -175,10 +175,10 @@ PANEL_I8 = [("panel_gemm_i8", I8_TOL), ("panel_gemm_i8_24", I8_24_TOL)]
 
 
 @pytest.mark.parametrize("path,tol", PANEL_I8)
-@pytest.mark.parametrize("k", [7, 20, 40, 50, 64])
+@pytest.mark.parametrize("k", [1, 7, 20, 40, 50, 64])
 def test_panel_gemm_i8_equals_fp64(k, path, tol):
     """The int8 panel-GEMM paths (gemm_i8.hip) against the fp64 panel-GEMM path: ragged DR12Q-shaped
-    spectra with masks, 16,500 samples for k = 50.  The 24-bit path's launch layouts: k = 7, one Gram
+    spectra with masks, 16,500 samples for k = 50.  The 24-bit path's launch layouts: k = 1 and 7, one Gram
     tile (gemm_i8_kernel<3>); k = 20, B-stationary Gram beside a u launch (no spare blocks); k = 40,
     6 / 7 Gram columns per XCD with the u tile fused on the spare blocks; k = 50 the same at 10 / 10;
     k = 64 (the largest rank), 16 / 17 columns and a u launch; spectra over 832 slots take
