@@ -19,6 +19,21 @@
 #include "device_common.h"
 #include "internal.h"
 
+#include <utility>
+
+namespace {
+// f(std::integral_constant<int, i>{}) for i = 0 .. N - 1, each i a compile-time constant (inline-asm
+// immediates and register-set indices need that; #pragma unroll only folds them after the fact)
+template <int N, typename F, int... I>
+__device__ inline void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename F>
+__device__ inline void static_for(F&& f) {
+  static_for_impl<N>(f, std::make_integer_sequence<int, N>{});
+}
+}  // namespace
+
 namespace gpdla {
 
 namespace {
@@ -671,7 +686,7 @@ __device__ inline void bst_run(const GemmI8Args& a, const SpecInfo& inf, uint8_t
   }
   const int g = lane >> 4;
   const int wt = wave_s & 3;                     // the wave's 32 rows of its 128-sample tile
-  const int64_t a_lane = ((int64_t)g * 128 + 32 * wt + (lane & 15)) * 16;
+  const uint32_t a_lane = (uint32_t)((g * 128 + 32 * wt + (lane & 15)) * 16);  // the lane's byte offset
   const uint8_t* adig = a.adig + (kU ? a.rows * a.kstride * 4 : 0);  // [type (Gram, u)][...]
   // this wave's sample tiles: st_i = st0 + i span, i = 0 .. nt - 1
   const int span = kTiles * G;
@@ -693,26 +708,27 @@ __device__ inline void bst_run(const GemmI8Args& a, const SpecInfo& inf, uint8_t
   // invisible to the compiler's waitcnt pass (which, around the guarded steps and the tile-end
   // stores, merged its queue model conservatively and drained the prefetch two steps ahead); land()
   // waits for them explicitly and hands the registers over through an empty "+v" asm.
+  // The step's base address is wave-uniform (SGPR pair, saddr form); the lane's offset is one fixed
+  // VGPR, so a prefetch needs no VGPR address of its own.
   auto load_a = [&](int gs, v4i (&r)[2][ND]) {
     const int i = gs / nks, ks = gs - i * nks;
-    const uint8_t* A0 = adig + ((int64_t)(st0 + i * span) * nksmax + ks) * 16 * 2048 + a_lane;
+    const uint8_t* A0 = adig + ((int64_t)(st0 + i * span) * nksmax + ks) * 16 * 2048;
 #pragma unroll
     for (int p = 0; p < ND; ++p) {
       const uint8_t* ap = A0 + p * 8192;
-      asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(r[0][p]) : "v"(ap) : "memory");
-      asm volatile("global_load_dwordx4 %0, %1, off offset:256" : "=v"(r[1][p]) : "v"(ap) : "memory");
+      asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(r[0][p]) : "v"(a_lane), "s"(ap) : "memory");
+      asm volatile("global_load_dwordx4 %0, %1, %2 offset:256" : "=v"(r[1][p]) : "v"(a_lane), "s"(ap) : "memory");
     }
   };
-  // A(g) has landed once at most the 2 ND min(DEPTH, last - g) newer loads of A(g + 1 .. g + DEPTH)
-  // are outstanding (vmcnt is in order; a tile-end epilogue's stores in between make this wait longer,
-  // never too short).  Prefetches past the wave's last step are not issued: a load whose value is
-  // never read leaves its registers free for the compiler while the hardware may still write them.
-  auto land = [&](int g, v4i (&r)[2][ND]) {
-    static_assert(DEPTH == 2 || DEPTH == 3, "land() spells out the waits for DEPTH 2 and 3");
-    if (last - g >= DEPTH) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * ND * DEPTH) : "memory");
-    else if (DEPTH == 3 && last - g == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * ND * 2) : "memory");
-    else if (last - g == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * ND) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // A(g) has landed once at most CNT newer vector-memory operations are outstanding: 2 ND per later
+  // A step already issued (vmcnt is in order; a tile-end epilogue's stores in between make the wait
+  // longer, never too short).  Every call site passes a compile-time count, and no prefetch is issued
+  // under a condition (see the pipeline below): tools/isa_inflight.py checks the shipped ISA for a
+  // register touched while its load is in flight, which a guarded prefetch beside a guarded wait
+  // makes undecidable for it (and a prefetch whose value is never read is exactly the round-5 fault:
+  // its registers are free to the compiler while the hardware may still write them).
+  auto land = [&](auto cnt, v4i (&r)[2][ND]) {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(decltype(cnt)::value) : "memory");
 #pragma unroll
     for (int rt = 0; rt < 2; ++rt)
 #pragma unroll
@@ -721,12 +737,14 @@ __device__ inline void bst_run(const GemmI8Args& a, const SpecInfo& inf, uint8_t
   // B operands of column tile ct (rows 16 ct .. + 15 of the unit): K granule g of a row sits in 16-B
   // slot (g + 2 ((row >> 2) & 3)) & 3 of its 64 B (convert_gemm_i8_kernel's swizzle; a unit starts at
   // a multiple of 32 rows of its entry tile, so the local row gives the same slot)
+  // ((row >> 2) & 3) does not depend on ct, so the lane's part of the address is one offset for every
+  // column tile and plane (the rest folds into the ds_read offset)
+  const int b_lane = (lane & 15) * 64 + 16 * ((g + 2 * (((lane & 15) >> 2) & 3)) & 3);
   auto read_b = [&](int ks, int ct, v4i (&Bd)[ND]) {
-    const uint8_t* Bc = Bs + ks * kStepBytes;
-    const int row = 16 * ct + (lane & 15);
+    const uint8_t* Bc = Bs + ks * kStepBytes + b_lane;
 #pragma unroll
     for (int p = 0; p < ND; ++p)
-      Bd[p] = *reinterpret_cast<const v4i*>(Bc + p * (W * 64) + row * 64 + 16 * ((g + 2 * ((row >> 2) & 3)) & 3));
+      Bd[p] = *reinterpret_cast<const v4i*>(Bc + p * (W * 64) + 16 * ct * 64);
   };
   auto mfmas = [&](const v4i (&Ar)[2][ND], const v4i (&Bd)[ND], int ct) {
 #pragma unroll
@@ -740,7 +758,9 @@ __device__ inline void bst_run(const GemmI8Args& a, const SpecInfo& inf, uint8_t
   auto epilogue = [&](int s_tile) {
 #pragma unroll
     for (int ct = 0; ct < NCT; ++ct) {
-      const int c = 16 * ct + (lane & 15), e = ebase + c;
+      int c = 16 * ct + (lane & 15);
+      asm volatile("" : "+v"(c));   // the column's addresses stay inside the loop (hoisted, they spilled)
+      const int e = ebase + c;
       if (!valid_entry(e)) continue;
       const double scl = s_ent[0][c], offl = s_ent[1][c];
 #pragma unroll
@@ -768,9 +788,9 @@ __device__ inline void bst_run(const GemmI8Args& a, const SpecInfo& inf, uint8_t
   // (NCT is even, so the two register sets alternate in step)
   v4i Bb[2][ND];
   int ks = 0, tile = 0;
-  auto step = [&](int g, v4i (&Ar)[2][ND]) {
+  auto step = [&](auto cnt, v4i (&Ar)[2][ND]) {
     const int ksn = ks + 1 == nks ? 0 : ks + 1;
-    land(g, Ar);
+    land(cnt, Ar);
 #pragma unroll
     for (int ct = 0; ct < NCT; ++ct) {
       __builtin_amdgcn_sched_barrier(0);
@@ -787,21 +807,48 @@ __device__ inline void bst_run(const GemmI8Args& a, const SpecInfo& inf, uint8_t
     ks = ksn;
   };
   zero_acc();
-  // DEPTH + 1 A register sets in turn, the loop unrolled by DEPTH + 1 (compile-time set indices), each
-  // step guarded rather than broken out of (early exits from the unrolled body spilled ~70 VGPRs).
+  // DEPTH + 1 A register sets in turn, A(g) in set g % NS.  Streams shorter than NS + DEPTH steps go
+  // one step at a time.  Otherwise: the prologue issues A(0 .. DEPTH - 1); each main-loop round issues
+  // A(gs + u + DEPTH) and multiplies A(gs + u) for u < NS, all unconditionally (the loop runs while
+  // the round's last prefetch exists), each wait retiring exactly the set about to be read; the tail
+  // (R = total - gs in [DEPTH, NS - 1 + DEPTH] steps left, A(gs .. gs + DEPTH - 1) in flight) is one
+  // straight-line sequence per R, its waits counting the prefetches that remain.  Same steps in the
+  // same order as a single guarded loop: bit for bit the same sums.
   constexpr int NS = DEPTH + 1;
   v4i Ar[NS][2][ND];
-#pragma unroll
-  for (int u = 0; u < DEPTH; ++u)
-    if (u <= last) load_a(u, Ar[u]);
-  read_b(0, 0, Bb[0]);
-  for (int gs = 0; gs < total; gs += NS) {
-#pragma unroll
-    for (int u = 0; u < NS; ++u) {
-      if (gs + u + DEPTH <= last) load_a(gs + u + DEPTH, Ar[(u + DEPTH) % NS]);
-      if (u == 0 || gs + u < total) step(gs + u, Ar[u]);
+  if (total < NS + DEPTH) {
+    read_b(0, 0, Bb[0]);
+    for (int g = 0; g < total; ++g) {
+      load_a(g, Ar[0]);
+      step(std::integral_constant<int, 0>{}, Ar[0]);
     }
+    return;
   }
+  static_for<DEPTH>([&](auto u) { load_a(decltype(u)::value, Ar[decltype(u)::value]); });
+  read_b(0, 0, Bb[0]);
+  int gs = 0;
+  do {
+    static_for<NS>([&](auto uc) {
+      constexpr int u = decltype(uc)::value;
+      load_a(gs + u + DEPTH, Ar[(u + DEPTH) % NS]);
+      step(std::integral_constant<int, 2 * ND * DEPTH>{}, Ar[u]);
+    });
+    gs += NS;
+  } while (gs + NS - 1 + DEPTH <= last);
+  // tail: R = total - gs in [DEPTH, NS - 1 + DEPTH] steps left.  A(gs .. gs + DEPTH - 1) are in flight
+  // in Ar[0 .. DEPTH - 1]; the rest are loaded one step at a time (the wave's last NS - 1 steps at
+  // most), each load waited for before its registers are read.
+  const int R = total - gs;
+  static_for<NS - 1 + DEPTH>([&](auto tc) {
+    constexpr int t = decltype(tc)::value;
+    if constexpr (t < DEPTH) {
+      constexpr int ahead = DEPTH - 1 - t;   // loads of A(gs + t + 1 .. gs + DEPTH - 1) still newer
+      step(std::integral_constant<int, 2 * ND * ahead>{}, Ar[t]);
+    } else if (t < R) {
+      load_a(gs + t, Ar[t % NS]);
+      step(std::integral_constant<int, 0>{}, Ar[t % NS]);
+    }
+  });
 }
 
 // The launch: per XCD, nye entry-tile columns x G groups of Gram blocks; when the u tile is fused

@@ -249,6 +249,32 @@ def test_panel_gemm_i8_24_short_spectra_take_32_bit_digits():
         assert _rel_err(o24[key], ref[key]) < I8_24_TOL, (key, _rel_err(o24[key], ref[key]))
 
 
+@pytest.mark.parametrize("S", [300, 1400, 3000])
+def test_bst_pipeline_every_stream_length(S):
+    """gemm_i8_bst_kernel's A pipeline (gemm_i8.hip bst_run) has three shapes by a wave's K-step count
+    total = (sample tiles) x (64-slot K steps): one step at a time below NS + DEPTH = 5, otherwise the
+    unguarded main loop and a tail of R = 2, 3 or 4 steps.  Spectra of 3..13 K steps (129..832 pixels,
+    the B-stationary range) at 300 / 1,400 / 3,000 samples (1, 1-3, 1-6 sample tiles per wave) reach
+    every shape, for the Gram role and the u role; each must agree with the fp64 panel path at the
+    24-bit bar.  (A missing B read on the short path gave NaN at 129 pixels, caught by
+    test_panel_gemm_i8_24_short_spectra_take_32_bit_digits.)"""
+    model = syn.make_model(k=50, seed=11)
+    samples = syn.make_samples(S)
+    base = syn.make_spectrum(model, 5, z_qso=3.4, n_target=None, mask_fraction=0.0)
+    i0 = int(np.searchsorted(base["wavelengths"] / (1 + base["z_qso"]), 912.0))   # first in-range pixel
+    assert base["wavelengths"].size - i0 >= 832
+    spectra = []
+    for npx in (129, 193, 257, 321, 385, 449, 513, 577, 641, 705, 769, 832):
+        sl = slice(i0, i0 + npx)
+        spectra.append({kk: (v[sl] if isinstance(v, np.ndarray) else v) for kk, v in base.items()})
+    packed = syn.pack_spectra(spectra)
+    ref = _run(model, samples, packed, "panel_gemm")
+    out = _run(model, samples, packed, "panel_gemm_i8_24")
+    for key in KEYS:
+        assert np.all(np.isfinite(out[key])), key
+        assert _rel_err(out[key], ref[key]) < I8_24_TOL, (S, key, _rel_err(out[key], ref[key]))
+
+
 def _raw_profile(lam, z, N, f32):
     import ctypes as C
     lam = np.ascontiguousarray(lam, dtype=np.float64)
