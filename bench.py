@@ -47,11 +47,18 @@ def i8_ops_per_eval(n: float, k: int, gram_pairs: int = 10) -> float:
     return 2 * n * (gram_pairs * k * (k + 1) / 2 + 10 * k)
 
 
+FP32_MATRIX_PEAK_TFLOPS = 157.3   # MI355X f32-input MFMA = the f32 vector peak (MI355X_MICROARCH.md)
+
+
 def i8_roofline(st: dict, n: float, k: int, Q: int, S: int, steps: int, path: str) -> dict:
-    """Roofline of the int8 panel paths' dominant kernel, the int8 GEMM (gemm_i8.hip): its algorithmic
+    """Roofline of the int8 panel paths' dominant kernel, the int8 GEMM (gemm_i8.hip): its digit-expanded
     int8 ops per launch / its average launch time (HIP events around each launch on the engine's
     stream, gpdla_stats.contraction_ms), against the dense int8 MFMA peak (2x BF16 per clock,
-    MI355X_MICROARCH.md).  The whole batch (weights + GEMM + LDL^T) is reported beside it."""
+    MI355X_MICROARCH.md).  ``frac`` is the MFMA utilisation of the digit scheme, not algorithmic work:
+    every Gram entry costs 6 (24-bit path) or 10 (32-bit path) int8 digit-pair products and every u
+    entry 10.  The whole batch (weights + GEMM + LDL^T) is reported beside it in algorithmic flops
+    (SURVEY 8d F_eval), set against the FP32 matrix peak of the precision BASELINE quotes configs[4]
+    in."""
     pairs = 6 if path.endswith("-24") else 10
     ops = i8_ops_per_eval(n, k, pairs)
     nl = max(st["contraction_launches"], 1)
@@ -60,13 +67,24 @@ def i8_roofline(st: dict, n: float, k: int, Q: int, S: int, steps: int, path: st
     achieved = ops * evals_per_gemm / (gemm_ms * 1e-3) / 1e12
     batch_ms = st["likelihood_ms"] / max(st["likelihood_launches"], 1)
     evals_per_batch = Q * (S + 1) * steps / max(st["likelihood_launches"], 1)
+    alg = algorithmic_flops_per_eval(n, k) * evals_per_batch / (batch_ms * 1e-3) / 1e12
     return {"bound": "mfma", "mfma_dtype": "i8", "unit": "TOPS", "peak": I8_PEAK_TOPS, "achieved": achieved,
-            "frac": achieved / I8_PEAK_TOPS, "avg_launch_ms": gemm_ms, "evals_per_launch": evals_per_gemm,
+            "frac": achieved / I8_PEAK_TOPS,
+            "frac_meaning": f"MFMA utilisation of the digit scheme: {pairs} int8 digit-pair products per Gram entry "
+                            f"and 10 per u entry (digit-expanded int8 ops, not algorithmic work) over the dense "
+                            f"int8 peak",
+            "avg_launch_ms": gemm_ms, "evals_per_launch": evals_per_gemm,
             "i8_ops_per_eval": ops,
             "whole_batch": {"avg_ms": batch_ms, "evals": evals_per_batch,
-                            "achieved_tops": ops * evals_per_batch / (batch_ms * 1e-3) / 1e12,
-                            "fp64_equivalent_tflops": algorithmic_flops_per_eval(n, k) * evals_per_batch
-                                                      / (batch_ms * 1e-3) / 1e12},
+                            "digit_tops": ops * evals_per_batch / (batch_ms * 1e-3) / 1e12,
+                            "digit_frac_of_i8_peak": ops * evals_per_batch / (batch_ms * 1e-3) / 1e12 / I8_PEAK_TOPS,
+                            "algorithmic_tflops": alg,
+                            "fp32_matrix_peak_tflops": FP32_MATRIX_PEAK_TFLOPS,
+                            "algorithmic_over_fp32_matrix_peak": alg / FP32_MATRIX_PEAK_TFLOPS,
+                            "note": "algorithmic_tflops = SURVEY 8d's F_eval (packed Gram, projection, per-pixel "
+                                    "terms, Cholesky, solve) per evaluation over the batch time.  It may exceed "
+                                    "the FP32 matrix peak because the Gram/u contraction runs exactly on the int8 "
+                                    "matrix cores (DESIGN.md section 10), not in fp32 or fp64"},
             "note": "the int8 GEMM launch(es) of one spectrum and sample chunk only (the 24-bit path runs its Gram "
                     "and u contractions in one launch); the batch adds the weights and LDL^T kernels"}
 
@@ -91,18 +109,18 @@ def single_stream_stats(eng, step, streams: int = 2, steps: int = 2) -> dict:
 
 
 def panel_roofline_streams(timed: dict, alone: dict, streams: int = 2) -> dict:
-    """The panel paths' roofline record: the GEMM kernel's own rate (one stream, after the timed
-    region; agrees with a one-stream rocprofv3 trace) and beside it the timed region's overlapped
-    launches.  The batch figures (whole_batch, int8 paths) are the timed region's."""
+    """The panel paths' roofline record: the timed region's GEMM launches (HIP events around each launch
+    while a batch's spectra alternate over ``streams`` streams), and nested beside it the kernel's own
+    rate (one stream, after the timed region; agrees with a one-stream rocprofv3 trace).  With two
+    streams a launch shares the CUs with, and queues behind, the other stream's weights / LDL^T
+    kernels, so its event span is longer than its run time: the timed figure is the lower one."""
     if "avg_launch_ms" not in timed or "avg_launch_ms" not in alone:
         return timed
-    return {**alone, **({"whole_batch": timed["whole_batch"]} if "whole_batch" in timed else {}),
-            "measured": "GEMM launches with the batch on one compute stream, 2 steps after the timed region",
-            "timed_region": {"panel_streams": streams, "avg_launch_ms": timed["avg_launch_ms"],
-                             "achieved": timed["achieved"], "frac": timed["frac"],
-                             "note": "HIP events around each GEMM launch in the timed region, where a batch's "
-                                     "spectra alternate over panel_streams streams: the launch shares the CUs with, and "
-                                     "queues behind, the other streams' weights / LDL^T kernels"}}
+    return {**timed,
+            "measured": f"GEMM launches in the timed region ({streams} panel streams, HIP events incl. queueing)",
+            "one_stream": {k: alone[k] for k in ("avg_launch_ms", "achieved", "frac", "evals_per_launch") if k in alone}
+            | {"measured": "GEMM launches with the batch on one compute stream, 2 steps after the timed region "
+                           "(the kernel's own rate; profiles/round5/r11d_c5s1_summary.md)"}}
 
 
 def f64_gemm_roofline(st: dict, n: float, k: int, Q: int, S: int, steps: int) -> dict:
@@ -550,23 +568,31 @@ def refuse(msg: str, rank: int) -> None:
 
 
 def plan_only(wl: dict, world: int, rank: int, local_rank: int, dist, ndev: int | None = None,
-              rehearsal: bool = False) -> None:
+              rehearsal: bool = False, alternatives: bool = False) -> None:
     """--plan-only: the multi-rank layout (which spectra each rank evaluates and on which device)
     through the same launcher and process group as a measured run, without any GPU call.  ``ndev``
     is the device count planned against (default one per rank); the device-sharing refusal of a
-    measured run applies."""
+    measured run applies.  With ``alternatives`` (a multi-rank configs[1] line) it also plans the
+    alternatives that line would measure: configs[3]'s LPT shards of the full DR12Q count and the
+    configs[2] end-to-end run with every rank writing its own chunks."""
     dev, err = assign_device(world, local_rank, world if ndev is None else ndev, rehearsal)
     if err:
         refuse(err, rank)
+    from gp_dla_detection_amd import synthetic as syn
     pool_pixels = None
-    if wl["dr12q"]:
-        from gp_dla_detection_amd import synthetic as syn
-        pool_pixels = [p["wavelengths"].size for p in dr12q_pool(syn.make_model(k=wl["k"]))]
+    if wl["dr12q"] or alternatives:
+        pool_pixels = [p["wavelengths"].size for p in dr12q_pool(syn.make_model(k=20 if alternatives else wl["k"]))]
     ids = rank_spectrum_ids(wl, rank, world, pool_pixels)
-    allr = gather({"rank": rank, "local_rank": local_rank, "device": dev, "ids": ids}, world, dist)
+    mine = {"rank": rank, "local_rank": local_rank, "device": dev, "ids": ids}
+    if alternatives:
+        c4 = WORKLOADS["c4"]
+        c3ids = dr12q_shard_ids(pool_pixels, c4["spectra"], rank, world, split=True)
+        mine["c3"] = {"spectra": int(c3ids.size),
+                      "pixels": int(np.sum(np.asarray(pool_pixels)[c3ids % len(pool_pixels)]))}
+    allr = gather(mine, world, dist)
     if rank == 0:
         cat = np.concatenate([r["ids"] for r in allr])
-        print(json.dumps({
+        out = {
             "plan_only": True, "n_gpus": world, "rehearsal": bool(rehearsal and len({r["device"] for r in allr}) < world),
             "distinct_devices": len({r["device"] for r in allr}),
             "world_size": dist.get_world_size() if dist is not None else 1,
@@ -574,7 +600,22 @@ def plan_only(wl: dict, world: int, rank: int, local_rank: int, dist, ndev: int 
             "ranks": [{"rank": r["rank"], "local_rank": r["local_rank"], "device": r["device"],
                        "spectra": int(r["ids"].size), "first_spectrum": int(r["ids"][0]),
                        "last_spectrum": int(r["ids"][-1])} for r in allr],
-            "disjoint": bool(np.unique(cat).size == cat.size), "total_spectra": int(cat.size)}), flush=True)
+            "disjoint": bool(np.unique(cat).size == cat.size), "total_spectra": int(cat.size)}
+        if alternatives:
+            px = np.array([r["c3"]["pixels"] for r in allr], dtype=np.float64)
+            out["alternatives_planned"] = {
+                "configs3": {"workload": WORKLOADS["c4"]["label"], "scaling": "strong",
+                             "ranks": [{"rank": r["rank"], **r["c3"]} for r in allr],
+                             "total_spectra": int(sum(r["c3"]["spectra"] for r in allr)),
+                             "pixels_max_over_mean": float(px.max() / px.mean()),
+                             "fields": ["value", "wall_s", "north_star_under_60s", "ranks", "imbalance",
+                                        "invariant_calc_cddf_246", "checks_ok"]},
+                "e2e": {"workload": "configs[2] end to end on files", "writers": world,
+                        "note": "rank 0 writes the processed/ tree (untimed); every rank decodes, evaluates and "
+                                "writes its LPT block shard of whole v7.3 chunks (process.run_process_qsos)",
+                        "fields": ["value", "ms_per_step", "e2e.total_s", "e2e.load_s", "e2e.compute_s",
+                                   "e2e.write_s", "e2e.devices_used"]}}
+        print(json.dumps(out), flush=True)
 
 
 def configs4_alternative(dev: int, steps: int) -> dict:
@@ -727,6 +768,107 @@ def configs2_alternative(dev: int) -> dict:
             "checks_ok": bool(inv["finite"] and inv["max_abs_dev"] < 1e-10)}
 
 
+def configs3_alternative(dev: int, world: int, rank: int, dist, rehearsal: bool) -> dict | None:
+    """BASELINE configs[3] beside a multi-rank headline: the full DR12Q count
+    (162,861 DR12Q-shaped spectra x 10^4 samples, k = 20, fp64 fused path) split over the ranks by LPT on
+    pixel count (strong scaling, no collective on the data path; process_qsos.m:88's spectrum loop),
+    inputs resident and each rank's share of the 13 GB of sample log-likelihoods left in its HBM.  One
+    untimed warm-up call on each rank's first 1,024 spectra, then ONE timed call per rank between
+    barriers (elapsed max-reduced over the ranks, as the headline).  Per rank: spectra, pixels, kernel
+    ms and wall; the calc_cddf.py:246 invariant on every row of every rank.  Returns the record on rank
+    0 (None elsewhere)."""
+    from gp_dla_detection_amd import _lib as L
+    from gp_dla_detection_amd import synthetic as syn
+    from gp_dla_detection_amd.engine import Engine
+    from gp_dla_detection_amd.parameters import set_parameters
+    wl = WORKLOADS["c4"]
+    Qt, S, k = wl["spectra"], wl["samples"], wl["k"]
+    t0 = time.perf_counter()
+    model = syn.make_model(k=k)
+    samples = syn.make_samples(S)
+    pool = dr12q_pool(model)
+    ids = dr12q_shard_ids([p["wavelengths"].size for p in pool], Qt, rank, world, split=True)
+    packed = syn.pack_spectra([pool[i % len(pool)] for i in ids])
+    del pool
+    Q = ids.size
+    t = {key: L.DeviceArray.from_numpy(packed[key], device=dev)
+         for key in ("wavelengths", "flux", "noise_variance", "pixel_mask", "z_qsos")}
+    o_null, o_dla = L.DeviceArray(dev, Q, np.float64), L.DeviceArray(dev, Q, np.float64)
+    o_s, o_n = L.DeviceArray(dev, (Q, S), np.float64), L.DeviceArray(dev, Q, np.int32)
+    setup_s = time.perf_counter() - t0
+    offs = packed["offsets"]
+    local = []
+    with Engine(model, samples, set_parameters(k=k), device=dev) as eng:
+        def call(off):
+            eng.process_device(off, t["wavelengths"].ptr, t["flux"].ptr, t["noise_variance"].ptr,
+                               t["pixel_mask"].ptr, t["z_qsos"].ptr, o_null.ptr, o_dla.ptr, o_s.ptr, S,
+                               npix_ptr=o_n.ptr)
+        call(offs[:min(Q, 1024) + 1])
+        eng.synchronize()
+        eng.reset_stats()
+        el = timed_steps(lambda: call(offs), eng.synchronize, 1, dist, local)
+        st = eng.stats()
+    t1 = time.perf_counter()
+    inv = invariant_all_rows(o_s, o_dla, S)
+    check_s = time.perf_counter() - t1
+    npix = o_n.numpy()
+    for a in (*t.values(), o_null, o_dla, o_s, o_n):
+        a.free()
+    mine = {"rank": rank, "device": dev, "pci_bus_id": L.pci_bus_id(dev), "spectra": int(Q),
+            "pixels": int(np.sum(npix)), "kernel_ms": st["prep_ms"] + st["likelihood_ms"] + st["reduce_ms"],
+            "likelihood_ms": st["likelihood_ms"], "wall_s": local[0], "setup_untimed_s": setup_s,
+            "invariant_max_abs_dev": inv["max_abs_dev"], "finite": inv["finite"], "invariant_check_s": check_s}
+    ranks = gather(mine, world, dist)
+    if rank != 0:
+        return None
+    km = np.array([r["kernel_ms"] for r in ranks])
+    wm = np.array([r["wall_s"] for r in ranks])
+    px = np.array([r["pixels"] for r in ranks], dtype=np.float64)
+    shared = len({r["pci_bus_id"] for r in ranks}) < world
+    value = Qt * S / el
+    ok = all(r["finite"] for r in ranks) and max(r["invariant_max_abs_dev"] for r in ranks) < 1e-10
+    rec = {"value": None if shared else value, "unit": "evals/s", "wall_s": el, "ms_per_step": el * 1e3, "steps": 1,
+           "warmup": "one call on each rank's first 1,024 spectra", "scaling": "strong", "n_gpus": world,
+           "north_star_under_60s": bool(el < 60.0),
+           "config": {"workload": wl["label"] + "; inputs resident in HBM, each rank's outputs left in its HBM",
+                      "spectra": Qt, "num_samples": S, "k": k, "likelihood_path": "fused",
+                      "parallelism": f"spectrum-shard x{world} (LPT on pixel count)"},
+           "ranks": ranks,
+           "imbalance": {"kernel_ms_max_over_mean": float(km.max() / km.mean()),
+                         "wall_max_over_mean": float(wm.max() / wm.mean()),
+                         "pixels_max_over_mean": float(px.max() / px.mean())},
+           "invariant_calc_cddf_246": {"rows": int(sum(r["spectra"] for r in ranks)),
+                                       "max_abs_dev": max(r["invariant_max_abs_dev"] for r in ranks),
+                                       "finite": all(r["finite"] for r in ranks)},
+           "checks_ok": bool(ok)}
+    if shared:
+        rec["rehearsal"] = {"value_if_counted": value, "note": f"ranks shared {len({r['pci_bus_id'] for r in ranks})} "
+                                                               f"GPU(s): not a {world}-GPU point"}
+    return rec
+
+
+def e2e_alternative(args, world: int, rank: int, dist, dev: int) -> dict | None:
+    """alternatives.e2e: configs[2] end to end on files (e2e_record), at world = N each rank decoding,
+    computing and writing its own chunks; skipped (on every rank) when the disk under the output
+    directory lacks E2E_DISK_BYTES.  Returns the record on rank 0."""
+    import shutil
+    base = args.e2e_dir or "/tmp/gpdla_e2e_alt"
+    Path(base).parent.mkdir(parents=True, exist_ok=True)
+    free = shutil.disk_usage(Path(base).parent).free
+    if dist is not None:
+        box = [free]
+        dist.broadcast_object_list(box, src=0)
+        free = box[0]
+    if free < E2E_DISK_BYTES:
+        return {"skipped": f"{free / 1e9:.0f} GB free under {Path(base).parent}, "
+                           f"{E2E_DISK_BYTES / 1e9:.0f} GB needed (13 GB output + the processed/ tree)"} if rank == 0 else None
+    rec = e2e_record(162861, 10000, 20, base, False, world, rank, dist, dev)
+    if rank == 0 and world > 1 and rec["e2e"]["devices_used"] < world:
+        rec["rehearsal"] = {"value_if_counted": rec["value"], "note": "ranks shared GPUs: not an N-GPU point"}
+        rec["value"] = None
+    return rec
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=None,
@@ -757,6 +899,8 @@ def main():
     ap.add_argument("--rehearsal", action="store_true",
                     help="allow N ranks on fewer than N devices (ranks share GPUs); the line then carries "
                          "value null and is labelled a rehearsal, never an N-GPU point")
+    ap.add_argument("--no-configs3", action="store_true",
+                    help="skip alternatives.configs3 (the full DR12Q count split over the ranks) in a multi-rank line")
     ap.add_argument("--no-configs2", action="store_true",
                     help="skip alternatives.configs2 (full DR12Q count on this GPU) in the default line")
     ap.add_argument("--no-e2e", action="store_true",
@@ -793,7 +937,9 @@ def main():
         if getattr(args, key) is not None:
             wl[key] = getattr(args, key)
     if args.plan_only:
-        plan_only(wl, world, rank, local_rank, dist if world > 1 else None, args.plan_devices, args.rehearsal)
+        plan_only(wl, world, rank, local_rank, dist if world > 1 else None, args.plan_devices, args.rehearsal,
+                  alternatives=(world > 1 and not args.no_alt and not wl["dr12q"] and wl["k"] == 20
+                                and args.path == "auto"))
         if world > 1:
             with _stdout_to_stderr():
                 dist.destroy_process_group()
@@ -918,7 +1064,9 @@ def main():
         alt = {"fused_i8": {
             "value": Q * S * args.steps / el2, "unit": "evals/s", "ms_per_step": el2 / args.steps * 1e3,
             "kernel_ms": {"prep+convert": st2["prep_ms"] / max(st2["prep_launches"], 1), "likelihood": l2},
-            "fp64_equivalent_tflops": algorithmic_flops_per_eval(n_mean, args.k) * Q * (S + 1) / (l2 * 1e-3) / 1e12,
+            "algorithmic_tflops": algorithmic_flops_per_eval(n_mean, args.k) * Q * (S + 1) / (l2 * 1e-3) / 1e12,
+            "algorithmic_tflops_note": "SURVEY 8d F_eval over the likelihood kernel time; the fp64 fused kernel's "
+                                       "peak is 78.6 TF/s, this one computes the Gram/u contraction on int8 MFMA",
             "max_rel_err_vs_fp64": {"sample_log_likelihoods_dla(256 spectra)": rel, "log_likelihoods_dla": rel_dla},
             "note": "likelihood_i8_kernel<20>: Gram/u contraction exact on v_mfma_i32_16x16x64_i8 over "
                     "32-bit-quantised weights/panel (4 digits, levels <= 3), fp64 everywhere else; "
@@ -934,19 +1082,19 @@ def main():
     for a in (*t.values(), o_null, o_dla, o_s, o_n):
         a.free()
 
-    if alt is not None and not args.no_configs2:
+    if world > 1 and not args.no_alt and not wl["dr12q"] and args.k == 20 and args.path == "auto":
+        # the north-star configs at N ranks: configs[3] = the full DR12Q count split
+        # over the ranks, and configs[2] end to end on files with every rank writing its own chunks
+        alt = {}
+        if not args.no_configs3:
+            alt["configs3"] = configs3_alternative(dev, world, rank, dist, args.rehearsal)
+        if not args.no_e2e:
+            alt["e2e"] = e2e_alternative(args, world, rank, dist, dev)
+    elif alt is not None and not args.no_configs2:
         # BASELINE configs[2]: the full DR12Q count on this GPU, driver-timed (north star "< 60 s")
         alt["configs2"] = configs2_alternative(dev)
-    if alt is not None and not args.no_e2e:
-        import shutil
-        base = args.e2e_dir or "/tmp/gpdla_e2e_alt"
-        Path(base).parent.mkdir(parents=True, exist_ok=True)
-        free = shutil.disk_usage(Path(base).parent).free
-        if free >= E2E_DISK_BYTES:
-            alt["e2e"] = e2e_record(162861, 10000, 20, base, False, 1, 0, None, dev)
-        else:
-            alt["e2e"] = {"skipped": f"{free / 1e9:.0f} GB free under {Path(base).parent}, "
-                                     f"{E2E_DISK_BYTES / 1e9:.0f} GB needed (13 GB output + the processed/ tree)"}
+    if world == 1 and alt is not None and not args.no_e2e:
+        alt["e2e"] = e2e_alternative(args, 1, 0, None, dev)
 
     q_total = Q
     if world > 1:  # spectra over all ranks (LPT shards of configs[3] differ in size)

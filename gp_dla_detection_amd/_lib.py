@@ -33,6 +33,7 @@ dp = C.POINTER(C.c_double)
 i64p = C.POINTER(C.c_int64)
 u8p = C.POINTER(C.c_uint8)
 i32p = C.POINTER(C.c_int32)
+fp = C.POINTER(C.c_float)
 
 
 class Model(C.Structure):
@@ -74,6 +75,18 @@ class Stats(C.Structure):
                 ("contraction_ms", C.c_double), ("contraction_launches", C.c_int64)]
 
 
+class DlaPrior(C.Structure):
+    _fields_ = [("alpha", C.c_double), ("uniform_min", C.c_double), ("uniform_max", C.c_double),
+                ("fit_min", C.c_double), ("fit_max", C.c_double), ("fit_upper", C.c_double)]
+
+
+class PreloadParams(C.Structure):
+    _fields_ = [("normalization_min_lambda", C.c_double), ("normalization_max_lambda", C.c_double),
+                ("min_lambda", C.c_double), ("max_lambda", C.c_double),
+                ("loading_min_lambda", C.c_double), ("loading_max_lambda", C.c_double),
+                ("min_num_pixels", C.c_int32), ("brightsky_bit", C.c_int32)]
+
+
 # every symbol include/gpdla.h declares, with its ctypes signature
 SIGNATURES = {
     "gpdla_engine_create": (C.c_int, [C.c_int32, C.POINTER(Model), C.POINTER(Samples), C.POINTER(Params), C.POINTER(C.c_void_p)]),
@@ -95,6 +108,12 @@ SIGNATURES = {
     "gpdla_objective_destroy": (None, [C.c_void_p]),
     "gpdla_spectrum_loss_f64": (C.c_int, [dp, dp, dp, dp, dp, C.c_int64, C.c_int32, C.c_double, C.c_double,
                                           C.c_double, dp, dp, dp, dp, dp, dp]),
+    "gpdla_halton_rr2_f64": (C.c_int, [C.c_int32, C.c_int64, C.c_int64, C.c_int64, C.POINTER(C.c_int32), C.c_int32, dp]),
+    "gpdla_generate_dla_samples_f64": (C.c_int, [C.c_int32, dp, C.c_int64, C.c_int64, C.POINTER(DlaPrior), dp, dp, dp,
+                                                 dp]),
+    "gpdla_read_spec_f32": (C.c_int, [C.c_int32, C.c_int64, fp, fp, i32p, fp, fp, u8p]),
+    "gpdla_preload_qsos_f32": (C.c_int, [C.c_int32, C.c_int64, i64p, fp, fp, fp, i32p, dp, C.POINTER(PreloadParams),
+                                         u8p, i64p, fp, fp, fp, u8p, dp, fp]),
     "gpdla_diag_faddeeva_w": (C.c_int, [C.c_double, C.c_double, dp, dp]),
     "gpdla_diag_line_table_error": (C.c_int, [C.c_int32, dp]),
     "gpdla_diag_raw_profile3": (C.c_int, [dp, C.c_int64, C.c_double, C.c_double, C.c_int32, dp]),
@@ -109,7 +128,7 @@ SIGNATURES = {
 }
 
 # GPDLA_ABI_VERSION of include/gpdla.h this binding is written against
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 _lib = None
 

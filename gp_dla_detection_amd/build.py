@@ -9,7 +9,7 @@ from pathlib import Path
 PKG = Path(__file__).resolve().parent
 CSRC = PKG / "csrc"
 SOURCES = ["kernels.hip", "kernels_i8.hip", "gemm_path.hip", "gemm_i8.hip", "gemm_f64.hip", "engine.hip", "objective.hip",
-           "faddeeva_host.cpp"]
+           "dla_samples.hip", "ingest.hip", "faddeeva_host.cpp"]
 OUT = PKG / "libgpdla.so"
 
 

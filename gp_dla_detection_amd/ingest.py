@@ -1,24 +1,29 @@
 """Spectrum ingest: read_spec.m and preload_qsos.m.
 
-``read_spec`` loads an SDSS DR12Q coadded "speclite" FITS file -- binary-table HDU 1, columns
-1-4 = flux, loglam, ivar, and_mask (read_spec.m:11-25) -- and derives wavelengths, noise
-variance and the bad-pixel mask (read_spec.m:27-38).  ``preload_qsos`` normalises each
-catalogue spectrum by its median flux in the 1310-1325 A rest window, applies the filter-flag
-rules and keeps the 910-1217 A rest range plus one unmasked pixel on either side
-(preload_qsos.m:13-70), producing the cells process_qsos reads (preloaded_qsos.mat).
+``read_spec_columns`` loads an SDSS DR12Q coadded "speclite" FITS file -- binary-table HDU 1,
+columns 1-4 = flux, loglam, ivar, and_mask (read_spec.m:11-25) -- on the host: the FITS reader is a
+numpy implementation of the binary-table subset these files use (no astropy on the GPU box).
+Everything numeric runs on the GPU (csrc/ingest.hip): ``read_spec`` derives wavelengths, noise
+variance and the bad-pixel mask (read_spec.m:27-38, ``gpdla_read_spec_f32``); ``preload_qsos``
+sends a batch of catalogue spectra as one CSR of their fitsread columns, and the device applies
+read_spec's rules, normalises each spectrum by its median flux in the 1310-1325 A rest window,
+sets the filter-flag bits and keeps the 910-1217 A rest range plus one unmasked pixel on either
+side (preload_qsos.m:18-67, ``gpdla_preload_qsos_f32``), producing the cells process_qsos reads
+(preloaded_qsos.mat).
 
-The FITS reader is a numpy implementation of the binary-table subset these files use (no
-astropy on the GPU box).  MATLAB's fitsread returns a 'E' column as single precision, and
-read_spec/preload_qsos keep computing in single (10.^loglam, 1./ivar, the normalisation); that
-is reproduced here (float32 arithmetic, float32 cells, widened to float64 only when packed for
-the engine) so the preloaded cells hold the values and the class the reference's cells hold.
+MATLAB's fitsread returns an 'E' column as single precision, and read_spec / preload_qsos keep
+computing in single (10.^loglam, 1./ivar, the normalisation); the device does the same (float32
+arithmetic, float32 cells, widened to float64 only when packed for the engine), with 10.^loglam
+correctly rounded to single.  There is no CPU path: without a HIP device the calls raise.
 """
 from __future__ import annotations
 
+import ctypes as C
 import os
 
 import numpy as np
 
+from . import _lib as L
 from . import parameters as P
 
 BRIGHTSKY = 24  # read_spec.m:9 (1-based bit of the and_mask)
@@ -135,35 +140,62 @@ def read_bintable(path: str, hdu: int = 1, columns=None) -> list:
     return out
 
 
-def read_spec(filename: str):
-    """[wavelengths, flux, noise_variance, pixel_mask] = read_spec(filename) (read_spec.m)."""
-    flux, log_wavelengths, ivar, and_mask = read_bintable(filename, 1, [1, 2, 3, 4])     # :11-25
-    flux = np.asarray(flux, dtype=np.float32)
-    log_wavelengths = np.asarray(log_wavelengths, dtype=np.float32)
-    ivar = np.asarray(ivar, dtype=np.float32)
-    wavelengths = np.power(np.float32(10), log_wavelengths)                              # :28
-    with np.errstate(divide="ignore"):
-        noise_variance = np.float32(1) / ivar                                            # :31
-    and_mask = np.asarray(and_mask).astype(np.int64)
-    pixel_mask = (ivar == 0) | (((and_mask >> (BRIGHTSKY - 1)) & 1) == 1)                # :36-38
-    return wavelengths, flux, noise_variance, pixel_mask
+def read_spec_columns(filename: str):
+    """fitsread(filename, 'binarytable', 1, 'tablecolumns', 1:4) (read_spec.m:11-25): flux, loglam and
+    ivar as single, and_mask as int32 (host)."""
+    flux, log_wavelengths, ivar, and_mask = read_bintable(filename, 1, [1, 2, 3, 4])
+    return (np.ascontiguousarray(flux, dtype=np.float32), np.ascontiguousarray(log_wavelengths, dtype=np.float32),
+            np.ascontiguousarray(ivar, dtype=np.float32), np.ascontiguousarray(and_mask, dtype=np.int32))
 
 
-def nanmedian(v: np.ndarray):
-    """MATLAB's nanmedian (preload_qsos.m:33) in the array's own class: NaNs dropped, the middle
-    element, or for an even count median.m's meanof(a, b) = a + (b - a) / 2 when a and b are finite
-    with the same sign, else (a + b) / 2 -- numpy's (a + b) / 2 can differ from it in the last bit."""
-    v = np.sort(v[~np.isnan(v)])
-    n = v.size
-    if n == 0:
-        return v.dtype.type(np.nan)
-    if n % 2:
-        return v[n // 2]
-    a, b = v[n // 2 - 1], v[n // 2]
-    two = v.dtype.type(2)
-    if np.isfinite(a) and np.isfinite(b) and np.sign(a) == np.sign(b):
-        return a + (b - a) / two
-    return (a + b) / two
+def read_spec(filename: str, device: int = 0):
+    """[wavelengths, flux, noise_variance, pixel_mask] = read_spec(filename) (read_spec.m): the columns
+    read on the host, read_spec.m:27-38 on the device."""
+    flux, loglam, ivar, and_mask = read_spec_columns(filename)
+    n = flux.size
+    w, nv, pm = np.empty(n, np.float32), np.empty(n, np.float32), np.empty(n, np.uint8)
+    L.check(L.load().gpdla_read_spec_f32(device, n, L.ptr(loglam, C.c_float), L.ptr(ivar, C.c_float),
+                                         L.ptr(and_mask, C.c_int32), L.ptr(w, C.c_float), L.ptr(nv, C.c_float),
+                                         L.ptr(pm, C.c_uint8)))
+    return w, flux, nv, pm.astype(bool)
+
+
+def preload_params() -> "L.PreloadParams":
+    """set_parameters.m:21-30's ingest constants and read_spec.m:9's BRIGHTSKY bit."""
+    return L.PreloadParams(P.NORMALIZATION_MIN_LAMBDA, P.NORMALIZATION_MAX_LAMBDA, P.MIN_LAMBDA, P.MAX_LAMBDA,
+                           P.LOADING_MIN_LAMBDA, P.LOADING_MAX_LAMBDA, P.MIN_NUM_PIXELS, BRIGHTSKY)
+
+
+def preload_batch(z_qsos, filter_flags, columns, device: int = 0) -> dict:
+    """preload_qsos.m:18-67 for one batch on the device.  ``columns[i]``: spectrum i's fitsread columns
+    (flux, loglam, ivar, and_mask), or None where filter_flags[i] > 0 (not read, :19-21).  Returns the
+    cells (lists of single / logical arrays), normalisers, updated flags and the single medians."""
+    z = np.ascontiguousarray(z_qsos, dtype=np.float64)
+    flags = np.array(filter_flags, dtype=np.uint8).ravel().copy()
+    Q = z.size
+    lens = np.array([0 if c is None else np.asarray(c[0]).size for c in columns], dtype=np.int64)
+    off = np.zeros(Q + 1, np.int64)
+    np.cumsum(lens, out=off[1:])
+    N = int(off[-1])
+    cat = lambda k, dt: (np.concatenate([np.asarray(c[k], dt) for c in columns if c is not None])   # noqa: E731
+                         if N else np.zeros(1, dt))
+    fl, ll, iv, am = cat(0, np.float32), cat(1, np.float32), cat(2, np.float32), cat(3, np.int32)
+    cap = max(N, 1)
+    ooff = np.zeros(Q + 1, np.int64)
+    w_o, f_o, nv_o = np.empty(cap, np.float32), np.empty(cap, np.float32), np.empty(cap, np.float32)
+    m_o = np.empty(cap, np.uint8)
+    norm, med = np.zeros(Q), np.empty(Q, np.float32)
+    params = preload_params()
+    L.check(L.load().gpdla_preload_qsos_f32(device, Q, L.ptr(off, C.c_int64), L.ptr(fl, C.c_float),
+                                            L.ptr(ll, C.c_float), L.ptr(iv, C.c_float), L.ptr(am, C.c_int32),
+                                            L.ptr(z), C.byref(params), L.ptr(flags, C.c_uint8),
+                                            L.ptr(ooff, C.c_int64), L.ptr(w_o, C.c_float), L.ptr(f_o, C.c_float),
+                                            L.ptr(nv_o, C.c_float), L.ptr(m_o, C.c_uint8), L.ptr(norm),
+                                            L.ptr(med, C.c_float)))
+    cells = lambda a: [a[ooff[i]:ooff[i + 1]].copy() for i in range(Q)]   # noqa: E731
+    return dict(all_wavelengths=cells(w_o), all_flux=cells(f_o), all_noise_variance=cells(nv_o),
+                all_pixel_mask=[c.astype(bool) for c in cells(m_o)], all_normalizers=norm, filter_flags=flags,
+                medians=med)
 
 
 def spec_filename(spectra_directory: str, plate: int, mjd: int, fiber_id: int) -> str:
@@ -171,52 +203,35 @@ def spec_filename(spectra_directory: str, plate: int, mjd: int, fiber_id: int) -
     return f"{spectra_directory}/{int(plate)}/spec-{int(plate)}-{int(mjd)}-{int(fiber_id):04d}.fits"
 
 
-def preload_qsos(z_qsos, plates, mjds, fiber_ids, filter_flags, file_loader, log=None) -> dict:
-    """preload_qsos.m:10-71.  ``file_loader(plate, mjd, fiber_id)`` returns read_spec's tuple.
+def preload_qsos(z_qsos, plates, mjds, fiber_ids, filter_flags, file_loader, log=None, device: int = 0,
+                 batch: int = 8192) -> dict:
+    """preload_qsos.m:10-71.  ``file_loader(plate, mjd, fiber_id)`` returns the spectrum's fitsread
+    columns (flux, loglam, ivar, and_mask; ``read_spec_columns``): the files are read on the host, and
+    read_spec.m:27-38 with preload_qsos.m:26-67 run on the device, ``batch`` spectra per launch.
     Returns the saved variables (cells as lists, filter_flags updated with bits 3 and 4)."""
     z_qsos = np.asarray(z_qsos, dtype=np.float64).ravel()
     filter_flags = np.array(filter_flags, dtype=np.uint8).ravel().copy()
     Q = z_qsos.size
-    all_w, all_f, all_n, all_m = ([np.zeros(0) for _ in range(Q)] for _ in range(4))
+    keys = ("all_wavelengths", "all_flux", "all_noise_variance", "all_pixel_mask")
+    out = {k: [] for k in keys}
     all_normalizers = np.zeros(Q)
-    for i in range(Q):
-        if filter_flags[i] > 0:                                                           # :19-21
-            continue
-        w, fl, nv, pm = file_loader(plates[i], mjds[i], fiber_ids[i])                     # :23-24
-        # emitted_wavelengths (:26); single-precision cells stay single as in MATLAB
-        rest = w / (np.float32(1 + z_qsos[i]) if w.dtype == np.float32 else 1 + z_qsos[i])
-        ind = (rest >= P.NORMALIZATION_MIN_LAMBDA) & (rest <= P.NORMALIZATION_MAX_LAMBDA) & ~pm  # :29-31
-        med = nanmedian(fl[ind])                                                          # :33
-        if np.isnan(med):                                                                 # :36-39
-            filter_flags[i] |= 1 << 2
-            continue
-        ind = (rest >= P.MIN_LAMBDA) & (rest <= P.MAX_LAMBDA) & ~pm                       # :41-43
-        if np.count_nonzero(ind) < P.MIN_NUM_PIXELS:                                       # :46-49
-            filter_flags[i] |= 1 << 3
-            continue
-        all_normalizers[i] = med                                                          # :51
-        fl = fl / med                                                                     # :53
-        nv = nv / (med * med)                                                             # :54
-        ind = (rest >= P.LOADING_MIN_LAMBDA) & (rest <= P.LOADING_MAX_LAMBDA)             # :56-57
-        avail = np.flatnonzero(~ind & ~pm)                                                # :60
-        if ind.any():
-            first, last = np.flatnonzero(ind)[0], np.flatnonzero(ind)[-1]
-            after, before = avail[avail > last], avail[avail < first]
-            if after.size:
-                ind[after.min()] = True                                                  # :61
-            if before.size:
-                ind[before.max()] = True                                                 # :62
-        # the cells keep fitsread's single class, as the reference's preloaded_qsos.mat holds them;
-        # pack_spectra widens them (exactly) to the engine's fp64
-        all_w[i], all_f[i] = w[ind], fl[ind]                                               # :64-67
-        all_n[i], all_m[i] = nv[ind], pm[ind].astype(bool)
+    for b0 in range(0, Q, batch):
+        sl = slice(b0, min(Q, b0 + batch))
+        cols = [None if filter_flags[i] > 0 else file_loader(plates[i], mjds[i], fiber_ids[i])   # :19-24
+                for i in range(sl.start, sl.stop)]
+        res = preload_batch(z_qsos[sl], filter_flags[sl], cols, device=device)
+        for k in keys:
+            out[k].extend(res[k])
+        all_normalizers[sl] = res["all_normalizers"]
+        filter_flags[sl] = res["filter_flags"]
         if log:
-            log(f"loaded quasar {i + 1} of {Q} ({plates[i]}/{mjds[i]}/{int(fiber_ids[i]):04d})")
+            for i in range(sl.start, sl.stop):
+                if res["all_wavelengths"][i - sl.start].size:
+                    log(f"loaded quasar {i + 1} of {Q} ({plates[i]}/{mjds[i]}/{int(fiber_ids[i]):04d})")
     return dict(loading_min_lambda=P.LOADING_MIN_LAMBDA, loading_max_lambda=P.LOADING_MAX_LAMBDA,
                 normalization_min_lambda=P.NORMALIZATION_MIN_LAMBDA,
                 normalization_max_lambda=P.NORMALIZATION_MAX_LAMBDA, min_num_pixels=P.MIN_NUM_PIXELS,
-                all_wavelengths=all_w, all_flux=all_f, all_noise_variance=all_n, all_pixel_mask=all_m,
-                all_normalizers=all_normalizers, filter_flags=filter_flags)
+                **out, all_normalizers=all_normalizers, filter_flags=filter_flags)
 
 
 def run_preload_qsos(base_directory: str, release: str) -> dict:
@@ -238,7 +253,7 @@ def run_preload_qsos(base_directory: str, release: str) -> dict:
     spectra_dir = f"{base_directory}/{release}/spectra"
     out = preload_qsos(np.ravel(cat["z_qsos"]), np.ravel(cat["plates"]), np.ravel(cat["mjds"]),
                        np.ravel(cat["fiber_ids"]), np.ravel(cat["filter_flags"]),
-                       lambda p, m, f: read_spec(spec_filename(spectra_dir, p, m, f)))
+                       lambda p, m, f: read_spec_columns(spec_filename(spectra_dir, p, m, f)))
     flags = out.pop("filter_flags")
     savemat73(f"{d}/preloaded_qsos.mat", {k: (np.float64(v) if np.isscalar(v) else v) for k, v in out.items()})
     cpath = f"{d}/catalog.mat"

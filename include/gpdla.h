@@ -11,6 +11,10 @@
  *     (log_mvnpdf_low_rank.m:5-33, process_qsos.m:151,196)
  *   process_qsos.m:88-220 per-spectrum loop + parfor    gpdla_engine_create / _process /
  *     over DLA samples (process_qsos.m:184-198)            _synchronize / _destroy
+ *   generate_dla_samples.m:8-57 (haltonset/scramble,     gpdla_generate_dla_samples_f64,
+ *     ksdensity, polyfit, integral, fzero)                 gpdla_halton_rr2_f64
+ *   read_spec.m:27-38, preload_qsos.m:18-67              gpdla_read_spec_f32,
+ *                                                          gpdla_preload_qsos_f32
  *
  * Conventions
  *   - Plain pointers and sizes only.  The caller owns every buffer; the engine owns only its
@@ -43,8 +47,9 @@ extern "C" {
 
 /* ABI version (gpdla_version()).  2: gpdla_stats gained contraction_ms / contraction_launches
  * (its size changed: a caller compiled against a version-1 header must use gpdla_engine_get_stats_n
- * with its own sizeof(gpdla_stats), or be rebuilt).  3: gpdla_device_pci_bus_id. */
-#define GPDLA_ABI_VERSION 3
+ * with its own sizeof(gpdla_stats), or be rebuilt).  3: gpdla_device_pci_bus_id.  4: the DLA-sample
+ * generator (gpdla_halton_rr2_f64, gpdla_generate_dla_samples_f64) and the ingest kernels. */
+#define GPDLA_ABI_VERSION 4
 
 #define GPDLA_MEM_HOST 0
 #define GPDLA_MEM_DEVICE 1
@@ -205,6 +210,58 @@ int gpdla_spectrum_loss_f64(const double* y, const double* lya_1pz, const double
                             const double* M, const double* omega2, int64_t n, int32_t k, double c_0,
                             double tau_0, double beta, double* nlog_p, double* dM, double* dlog_omega,
                             double* dlog_c_0, double* dlog_tau_0, double* dlog_beta);
+
+/* ---- DLA parameter samples ------------------------------------------------------
+ * generate_dla_samples.m:8-57 on the device: the RR2-scrambled Halton points (:8-9), ksdensity of the
+ * catalogue's column densities on the 1,000-point fit grid at MATLAB's default bandwidth (:32-33), the
+ * quadratic log-density fit (:34, host QR) normalised over [fit_min, fit_upper] (:37-38) and the inverse
+ * mixture CDF of every sample's second Halton coordinate (:42-55, fzero), nhi = 10^log_nhi (:57).
+ * Host buffers.  The prior's fields are set_parameters.m:49-53's (0.9, 20, 23, 20, 22) and the 25.0 of
+ * generate_dla_samples.m:38. */
+typedef struct gpdla_dla_prior {
+  double alpha;                    /* weight of the fitted component (set_parameters.m:49) */
+  double uniform_min, uniform_max; /* uniform component of log10 N_HI (:50-51) */
+  double fit_min, fit_max;         /* KDE / fit range (:52-53) */
+  double fit_upper;                /* upper limit of the normalising integral (generate_dla_samples.m:38) */
+} gpdla_dla_prior;
+/* Points start, start + stride, ... (num of them) of the RR2-scrambled Halton sequence in `dims` bases
+ * (haltonset(dims, 'Skip', start, 'Leap', stride - 1) + scramble(..., 'RR2'); index 0 is the origin):
+ * out[j * dims + d], bit-exact.  Bases 2..64, dims <= 16. */
+int gpdla_halton_rr2_f64(int32_t device, int64_t start, int64_t stride, int64_t num, const int32_t* bases,
+                         int32_t dims, double* out);
+/* log_nhis: the catalogue's n_data column densities (the non-empty cells concatenated, :26-28).
+ * Writes num_samples offsets, log10 N_HI and N_HI samples; fit (may be NULL) receives the polyfit
+ * coefficients c2, c1, c0, the normaliser Z and the KDE bandwidth.  GPDLA_ENUMERIC when the density
+ * estimate vanishes on the fit grid or the fit does not normalise. */
+int gpdla_generate_dla_samples_f64(int32_t device, const double* log_nhis, int64_t n_data, int64_t num_samples,
+                                   const gpdla_dla_prior* prior, double* offset_samples, double* log_nhi_samples,
+                                   double* nhi_samples, double* fit);
+
+/* ---- Spectrum ingest -----------------------------------------------------------
+ * read_spec.m:27-38 and preload_qsos.m:18-67 on the device, over the fitsread columns of a catalogue
+ * (FITS parsing stays on the host).  Host buffers.  Thresholds are compared exactly (the defaults are
+ * all representable in single); brightsky_bit is read_spec.m:9's 1-based bit of the and_mask (24). */
+typedef struct gpdla_preload_params {
+  double normalization_min_lambda, normalization_max_lambda;   /* set_parameters.m:29-30 (1310, 1325) */
+  double min_lambda, max_lambda;                               /* :33-34 (911.75, 1215.75) */
+  double loading_min_lambda, loading_max_lambda;               /* :21-22 (910, 1217) */
+  int32_t min_num_pixels;                                      /* :26 (200) */
+  int32_t brightsky_bit;                                       /* read_spec.m:9 (24) */
+} gpdla_preload_params;
+/* wavelengths = 10.^loglam (single, correctly rounded), noise_variance = 1 ./ ivar,
+ * pixel_mask = ivar == 0 | bitget(and_mask, 24) (read_spec.m:27-38), elementwise over n pixels. */
+int gpdla_read_spec_f32(int32_t device, int64_t n, const float* loglam, const float* ivar, const int32_t* and_mask,
+                        float* wavelengths, float* noise_variance, uint8_t* pixel_mask);
+/* preload_qsos.m:18-67 over num_quasars spectra in CSR (offsets[Q + 1], offsets[0] = 0; the fitsread
+ * columns flux, loglam, ivar, and_mask; z_qsos[Q]).  filter_flags[Q] (in/out): entries > 0 are skipped;
+ * bit 3 (4) / bit 4 (8) are set for an unnormalisable spectrum / too few pixels.  Out: the cells in CSR
+ * (out_offsets[Q + 1]; each out_* array needs offsets[Q] entries at most), normalizers[Q] (0 where not
+ * loaded) and, if not NULL, medians[Q] (the single normalisation median, NaN where undefined). */
+int gpdla_preload_qsos_f32(int32_t device, int64_t num_quasars, const int64_t* offsets, const float* flux,
+                           const float* loglam, const float* ivar, const int32_t* and_mask, const double* z_qsos,
+                           const gpdla_preload_params* params, uint8_t* filter_flags, int64_t* out_offsets,
+                           float* out_wavelengths, float* out_flux, float* out_noise_variance,
+                           uint8_t* out_pixel_mask, double* normalizers, float* medians);
 
 /* Diagnostics (test support; not used by the compute path).
  * Re/Im of the Faddeeva function the line tables are fitted from (host, long double). */

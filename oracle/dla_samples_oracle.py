@@ -88,7 +88,9 @@ def polyfit_qr(x: np.ndarray, y: np.ndarray, n: int) -> np.ndarray:
     return np.linalg.solve(R, Q.T @ y)
 
 
-def generate_dla_samples(cells, num_dla_samples: int, alpha: float = ALPHA) -> dict:
+def generate_dla_samples(cells, num_dla_samples: int, alpha: float = ALPHA, sample_indices=None) -> dict:
+    """``sample_indices`` (optional): solve :51-54 only for these samples (the others are NaN) -- the
+    per-sample quadrature and Brent root are slow, so checks at 10^5 samples take a subset."""
     log_nhis = np.concatenate([np.asarray(c, dtype=np.float64).ravel() for c in cells
                                if np.asarray(c).size > 0])                          # :26-28
     x = np.linspace(FIT_MIN, FIT_MAX, 1000)                                        # :32
@@ -111,8 +113,10 @@ def generate_dla_samples(cells, num_dla_samples: int, alpha: float = ALPHA) -> d
 
     offsets = np.array([halton_rr2_point(i, 2) for i in range(num_dla_samples)])  # :13
     us = np.array([halton_rr2_point(i, 3) for i in range(num_dla_samples)])
-    out = np.zeros(num_dla_samples)
-    for i, u in enumerate(us):                                                     # :51-54
+    out = np.full(num_dla_samples, np.nan)
+    todo = range(num_dla_samples) if sample_indices is None else sample_indices
+    for i in todo:                                                                 # :51-54
+        u = us[i]
         g = lambda t: cdf(t) - u                                                   # noqa: E731
         if g(FIT_MIN) >= 0:
             out[i] = FIT_MIN

@@ -1,9 +1,9 @@
 """CPU oracle for read_spec.m and preload_qsos.m -- TEST INFRASTRUCTURE ONLY.
 
-Only ``tests/`` runs this module, as the checker of gp_dla_detection_amd/ingest.py.  It needs
-astropy (the FITS reader independent of the product's own numpy one) and is executed with the
-interpreter that has it (/opt/conda/bin/python3.9 in the build container; absent on the GPU box,
-where the test is skipped):
+Only ``tests/`` runs this module, as the checker of gp_dla_detection_amd/ingest.py and its device
+kernels (csrc/ingest.hip).  Its FITS path needs astropy (a reader independent of the product's own
+numpy one) and is executed with the interpreter that has it (/opt/conda/bin/python3.9 in the build
+container; absent on the GPU box):
 
     python3.9 oracle/ingest_oracle.py <job.npz> <out.npz>
 
@@ -26,8 +26,9 @@ Restated, in MATLAB's order and classes:
   - the 910-1217 A loading range plus one unmasked pixel on either side, the first found after
     the range's last pixel, then the last before its first (:56-62; ``min``/``max`` of an empty
     set index nothing).
-Single-precision elementary functions (10.^x) follow C powf here; MATLAB's may differ in the last
-ulp (unpinned).  Parity status: no reference outputs exist (the spectra are downloaded), so the
+10.^x is taken correctly rounded to single (the double power rounded once); MATLAB's single pow may
+differ in the last ulp (unpinned).  ``preload_from_columns`` is the same restatement on columns
+already read (no astropy: the GPU tests run it on the box against the device kernels).  Parity status: no reference outputs exist (the spectra are downloaded), so the
 oracle is pinned by the .m files' semantics as MATLAB documents them, not by executed outputs.
 """
 from __future__ import annotations
@@ -43,7 +44,8 @@ LOADING_MIN, LOADING_MAX = 910.0, 1217.0           # set_parameters.m:21-22
 MIN_NUM_PIXELS = 200                               # set_parameters.m:26
 
 
-def read_spec(filename):
+def read_columns(filename):
+    """fitsread(filename, 'binarytable', 1, 'tablecolumns', 1:4) (read_spec.m:11-25), astropy."""
     if not hasattr(np, "asscalar"):          # astropy 4.3 with numpy >= 1.23
         np.asscalar = lambda a: a.item()
     if not hasattr(np, "alen"):
@@ -56,13 +58,24 @@ def read_spec(filename):
         log_wavelengths = np.array(data[names[1]])                                 # :19
         ivar = np.array(data[names[2]])                                            # :22
         and_mask = np.array(data[names[3]])                                        # :25
-    flux, log_wavelengths, ivar = (a.astype(a.dtype.newbyteorder("=")) for a in (flux, log_wavelengths, ivar))
-    wavelengths = np.float32(10.0) ** log_wavelengths                              # :28
+    return tuple(a.astype(a.dtype.newbyteorder("=")) for a in (flux, log_wavelengths, ivar, and_mask))
+
+
+def derive(flux, log_wavelengths, ivar, and_mask):
+    """read_spec.m:27-38 on the fitsread columns, in single.  10.^loglam is taken correctly rounded to
+    single (the double power rounded once: over every float32 loglam in [3.5, 4.1] that equals the
+    extended-precision value rounded to single, tests/test_ingest.py); MATLAB's own single pow is
+    unpinned at the last ulp."""
+    wavelengths = (10.0 ** np.asarray(log_wavelengths, np.float64)).astype(np.float32)   # :28
     with np.errstate(divide="ignore"):
         noise_variance = np.float32(1.0) / ivar                                    # :31
-    bit = (and_mask.astype(np.int64) >> (BRIGHTSKY - 1)) & 1                       # bitget(and_mask, 24)
+    bit = (np.asarray(and_mask).astype(np.int64) >> (BRIGHTSKY - 1)) & 1           # bitget(and_mask, 24)
     pixel_mask = (ivar == 0) | (bit == 1)                                          # :36-38
     return wavelengths, flux, noise_variance, pixel_mask
+
+
+def read_spec(filename):
+    return derive(*read_columns(filename))
 
 
 def matlab_median(v):
@@ -79,47 +92,60 @@ def matlab_median(v):
     return (a + b) / v.dtype.type(2)
 
 
-def preload_qsos(z_qsos, plates, mjds, fiber_ids, filter_flags, spectra_dir):
+def preload_one(w, fl, nv, pm, z):
+    """preload_qsos.m:26-67 for one spectrum: (flag bits to set, median, cells or None)."""
+    rest = w / np.float32(1.0 + z)                                                 # :26 (single)
+    ind = (rest >= NORMALIZATION_MIN) & (rest <= NORMALIZATION_MAX) & ~pm          # :29-31
+    vals = fl[ind]
+    med = matlab_median(vals[~np.isnan(vals)])                                     # :33 nanmedian
+    if np.isnan(med):                                                              # :36-39
+        return 1 << 2, med, None
+    ind = (rest >= MIN_LAMBDA) & (rest <= MAX_LAMBDA) & ~pm                        # :41-43
+    if np.count_nonzero(ind) < MIN_NUM_PIXELS:                                     # :46-49
+        return 1 << 3, med, None
+    fl = fl / med                                                                  # :53
+    nv = nv / (med * med)                                                          # :54 (single)
+    ind = (rest >= LOADING_MIN) & (rest <= LOADING_MAX)                            # :56-57
+    available = [j for j in range(ind.size) if not ind[j] and not pm[j]]           # :60
+    sel = [j for j in range(ind.size) if ind[j]]
+    if sel:
+        after = [j for j in available if j > sel[-1]]
+        if after:
+            ind[min(after)] = True                                                 # :61
+        sel = [j for j in range(ind.size) if ind[j]]
+        before = [j for j in available if j < sel[0]]
+        if before:
+            ind[max(before)] = True                                                # :62
+    return 0, med, (w[ind], fl[ind], nv[ind], pm[ind])                             # :64-67
+
+
+def preload_from_columns(z_qsos, filter_flags, columns):
+    """preload_qsos.m:18-67 over spectra given as their fitsread columns (flux, loglam, ivar,
+    and_mask) -- ``columns[i]`` may be None for an entry that is pre-filtered (filter_flags > 0)."""
     Q = len(z_qsos)
     flags = np.array(filter_flags, dtype=np.uint8).copy()
     out = dict(all_wavelengths=[None] * Q, all_flux=[None] * Q, all_noise_variance=[None] * Q,
-               all_pixel_mask=[None] * Q, all_normalizers=np.zeros(Q))
+               all_pixel_mask=[None] * Q, all_normalizers=np.zeros(Q), medians=np.full(Q, np.nan, np.float32))
     for i in range(Q):                                                             # :18
         if flags[i] > 0:                                                           # :19-21
             continue
-        p, m, f = int(plates[i]), int(mjds[i]), int(fiber_ids[i])
-        w, fl, nv, pm = read_spec(f"{spectra_dir}/{p}/spec-{p}-{m}-{f:04d}.fits")  # :23-24
-        rest = w / np.float32(1.0 + z_qsos[i])                                     # :26 (single)
-        ind = (rest >= NORMALIZATION_MIN) & (rest <= NORMALIZATION_MAX) & ~pm      # :29-31
-        vals = fl[ind]
-        med = matlab_median(vals[~np.isnan(vals)])                                 # :33 nanmedian
-        if np.isnan(med):                                                          # :36-39
-            flags[i] |= 1 << 2
-            continue
-        ind = (rest >= MIN_LAMBDA) & (rest <= MAX_LAMBDA) & ~pm                    # :41-43
-        if np.count_nonzero(ind) < MIN_NUM_PIXELS:                                 # :46-49
-            flags[i] |= 1 << 3
+        bits, med, cells = preload_one(*derive(*columns[i]), z_qsos[i])            # :23-67
+        flags[i] |= bits
+        out["medians"][i] = med
+        if cells is None:
             continue
         out["all_normalizers"][i] = med                                            # :51
-        fl = fl / med                                                              # :53
-        nv = nv / (med * med)                                                      # :54 (single)
-        ind = (rest >= LOADING_MIN) & (rest <= LOADING_MAX)                        # :56-57
-        available = [j for j in range(ind.size) if not ind[j] and not pm[j]]       # :60
-        sel = [j for j in range(ind.size) if ind[j]]
-        if sel:
-            after = [j for j in available if j > sel[-1]]
-            if after:
-                ind[min(after)] = True                                             # :61
-            sel = [j for j in range(ind.size) if ind[j]]
-            before = [j for j in available if j < sel[0]]
-            if before:
-                ind[max(before)] = True                                            # :62
-        out["all_wavelengths"][i] = w[ind]                                         # :64-67
-        out["all_flux"][i] = fl[ind]
-        out["all_noise_variance"][i] = nv[ind]
-        out["all_pixel_mask"][i] = pm[ind]
+        for key, c in zip(("all_wavelengths", "all_flux", "all_noise_variance", "all_pixel_mask"), cells):
+            out[key][i] = c
     out["filter_flags"] = flags
     return out
+
+
+def preload_qsos(z_qsos, plates, mjds, fiber_ids, filter_flags, spectra_dir):
+    cols = [None if filter_flags[i] > 0 else
+            read_columns(f"{spectra_dir}/{int(plates[i])}/spec-{int(plates[i])}-{int(mjds[i])}-{int(fiber_ids[i]):04d}.fits")
+            for i in range(len(z_qsos))]                                           # :23-24
+    return preload_from_columns(z_qsos, filter_flags, cols)
 
 
 def main(job_path, out_path):

@@ -45,20 +45,33 @@ def test_i8_roofline_uses_the_gemm_launches(bench):
 
 
 def test_panel_roofline_streams_record(bench):
-    """With two panel streams the roofline is the GEMM's one-stream launch (measured after the timed
-    region) and the timed region's overlapped launches sit beside it; the batch figures stay the timed
-    region's.  A record without launch timing passes through unchanged."""
+    """With two panel streams the roofline is the timed region's GEMM launches, with
+    the kernel's one-stream launch (measured after the timed region) nested beside it; the batch
+    figures stay the timed region's.  A record without launch timing passes through unchanged."""
     st2 = {"contraction_ms": 32.0, "contraction_launches": 20, "likelihood_ms": 28.0, "likelihood_launches": 2}
     st1 = {"contraction_ms": 2.0, "contraction_launches": 2, "likelihood_ms": 16.0, "likelihood_launches": 1}
     timed = bench.i8_roofline(st2, 800, 50, Q=10, S=99, steps=2, path="panel-GEMM-int8-24")
     alone = bench.i8_roofline(st1, 800, 50, Q=1, S=99, steps=2, path="panel-GEMM-int8-24")
     r = bench.panel_roofline_streams(timed, alone, 2)
-    assert r["avg_launch_ms"] == 1.0 and r["frac"] == alone["frac"]
-    assert r["timed_region"]["avg_launch_ms"] == 1.6 and r["timed_region"]["panel_streams"] == 2
-    assert r["timed_region"]["frac"] == pytest.approx(timed["frac"]) and r["frac"] > r["timed_region"]["frac"]
+    assert r["avg_launch_ms"] == 1.6 and r["frac"] == pytest.approx(timed["frac"])
+    assert r["one_stream"]["avg_launch_ms"] == 1.0 and r["one_stream"]["frac"] == pytest.approx(alone["frac"])
+    assert r["one_stream"]["frac"] > r["frac"]
     assert r["whole_batch"] == timed["whole_batch"]
     f64 = bench.f64_gemm_roofline({**st1, "contraction_launches": 0}, 800, 50, 1, 99, 2)
     assert bench.panel_roofline_streams(f64, alone) is f64
+
+
+def test_no_field_reads_as_a_fraction_above_one(bench):
+    """Honest units: the int8 frac says what it measures, the batch's algorithmic rate
+    is named as such and set against the FP32 matrix peak, and no 'fp64-equivalent' figure remains."""
+    st = {"contraction_ms": 0.54, "contraction_launches": 1, "likelihood_ms": 0.47, "likelihood_launches": 1}
+    r = bench.i8_roofline(st, 800, 50, Q=1, S=100000, steps=1, path="panel-GEMM-int8-24")
+    assert "digit" in r["frac_meaning"] and "6" in r["frac_meaning"]
+    wb = r["whole_batch"]
+    assert "fp64_equivalent_tflops" not in wb and wb["fp32_matrix_peak_tflops"] == 157.3
+    assert wb["algorithmic_over_fp32_matrix_peak"] == pytest.approx(wb["algorithmic_tflops"] / 157.3)
+    assert 0 < wb["digit_frac_of_i8_peak"] < 1 and 0 < r["frac"] < 1
+    assert "fp64_equivalent" not in (ROOT / "bench.py").read_text()
 
 
 def test_profiled_traffic_lookup(bench):

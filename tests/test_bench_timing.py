@@ -100,6 +100,16 @@ def test_launcher_starts_n_ranks(workload, total):
     assert d["disjoint"] and d["total_spectra"] == total
     if workload == "c2":
         assert [x["spectra"] for x in d["ranks"]] == [1024, 1024]
+        # a multi-rank configs[1] line also measures configs[3] (the full DR12Q count LPT-split over the
+        # ranks, strong scaling) and configs[2] end to end with every rank writing
+        ap = d["alternatives_planned"]
+        c3 = ap["configs3"]
+        assert c3["total_spectra"] == 162861 and [x["rank"] for x in c3["ranks"]] == [0, 1]
+        assert c3["pixels_max_over_mean"] < 1.0001 and c3["scaling"] == "strong"
+        assert {"value", "ranks", "imbalance", "invariant_calc_cddf_246"} <= set(c3["fields"])
+        assert ap["e2e"]["writers"] == 2 and "e2e.write_s" in ap["e2e"]["fields"]
+    else:
+        assert "alternatives_planned" not in d
 
 
 def test_launcher_world_mismatch_fails():

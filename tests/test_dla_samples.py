@@ -1,15 +1,14 @@
-"""generate_dla_samples (generate_dla_samples.m:1-63) restated in gp_dla_detection_amd/dla_samples.py.
-
-Parity is pinned by the published definitions the reference calls (no sample file or catalogue
-ships with it): RR2-scrambled Halton digits (Kocis & Whiten 1997), MATLAB ksdensity's default
-bandwidth rule and Gaussian kernel, and the mixture CDF / its inverse."""
+"""The checkers of generate_dla_samples (generate_dla_samples.m:1-63), pinned on the CPU before they judge
+the device kernels (tests/test_gpu_dla_samples.py): oracle/dla_samples_closed_form.py (the algorithm
+csrc/dla_samples.hip implements, vectorised in numpy) against MATLAB's documented Halton output, the
+published definitions (RR2 digits, ksdensity's default bandwidth and Gaussian kernel, the mixture CDF
+and its inverse) and oracle/dla_samples_oracle.py (MATLAB's order, step by step).  No sample file or
+catalogue ships with the reference.  The product itself has no CPU path."""
 import numpy as np
 import pytest
 from scipy import integrate, stats
 
-from gp_dla_detection_amd import dla_samples as D
-from gp_dla_detection_amd import matv73 as M
-from gp_dla_detection_amd import process as PR
+from oracle import dla_samples_closed_form as D
 
 
 def test_rr2_permutations():
@@ -98,26 +97,11 @@ def test_generate_dla_samples_marginals(prior):
     assert np.max(np.abs(np.sort(out["offset_samples"]) - (np.arange(4000) + 0.5) / 4000)) < 1e-3
 
 
-def test_run_generate_dla_samples_files(tmp_path, prior):
-    _, log_nhis = prior
-    d = tmp_path / "dr12q" / "processed"
-    d.mkdir(parents=True)
-    cells = list(np.array_split(log_nhis, 100))
-    M.savemat73(str(d / "catalog.mat"), dict(log_nhis=dict(dr9q_concordance=cells)))
-    out = D.run_generate_dla_samples(str(tmp_path), "dr12q", "dr9q_concordance", num_dla_samples=500)
-    r = M.loadmat73(str(d / "dla_samples.mat"))
-    assert r["offset_samples"].shape == (1, 500)                   # MATLAB row (h5py (500, 1))
-    np.testing.assert_array_equal(r["log_nhi_samples"].ravel(), out["log_nhi_samples"])
-    assert float(r["alpha"][0, 0]) == 0.9
-    s = PR.load_dla_samples(str(d / "dla_samples.mat"))
-    np.testing.assert_array_equal(s["nhi_samples"], out["nhi_samples"])
-
-
 def test_matches_the_oracle_restatement(prior):
-    """Product vs oracle/dla_samples_oracle.py, the step-by-step MATLAB-order restatement of
+    """Closed form vs oracle/dla_samples_oracle.py, the step-by-step MATLAB-order restatement of
     generate_dla_samples.m (digit-by-digit RR2 Halton, ksdensity loop, QR polyfit, quadrature
     integral for Z and the CDF, bracket + Brent fzero): offsets bit for bit, log N_HI to 1e-11
-    (the oracle's quadrature and root tolerances; the product integrates in closed form)."""
+    (the oracle's quadrature and root tolerances; the closed form integrates exactly)."""
     from oracle import dla_samples_oracle as DO
     _, log_nhis = prior
     cells = list(np.array_split(log_nhis, 40)) + [np.zeros(0)]
@@ -126,3 +110,15 @@ def test_matches_the_oracle_restatement(prior):
     np.testing.assert_array_equal(got["offset_samples"], want["offset_samples"])
     np.testing.assert_allclose(got["log_nhi_samples"], want["log_nhi_samples"], rtol=0, atol=1e-11)
     np.testing.assert_allclose(got["nhi_samples"], want["nhi_samples"], rtol=1e-10)
+
+
+def test_product_has_no_cpu_path():
+    """The product generator runs on the device only: without one it fails loudly (no numpy fallback)."""
+    from gp_dla_detection_amd import _lib as L
+    from gp_dla_detection_amd import dla_samples as DS
+    if L.load().gpdla_device_count() > 0:
+        pytest.skip("a HIP device is present")
+    with pytest.raises(L.GpdlaError, match="no HIP device"):
+        DS.generate_dla_samples(np.r_[20.3, 20.6, 21.0], 10)
+    with pytest.raises(L.GpdlaError, match="no HIP device"):
+        DS.halton_rr2(4)

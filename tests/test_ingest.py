@@ -1,6 +1,8 @@
-"""Spectrum ingest (read_spec.m, preload_qsos.m).  The numpy FITS reader is
-checked against a file written by astropy (tests/golden/make_fits_fixture.py); read_spec and
-preload_qsos against the rules of read_spec.m:27-38 and preload_qsos.m:25-72."""
+"""Spectrum ingest (read_spec.m, preload_qsos.m) on the CPU: the host FITS reader
+against a file written by astropy (tests/golden/make_fits_fixture.py), the test-side FITS writer, and
+the checker the device kernels are judged by (oracle/ingest_oracle.py) pinned to the .m files' rules:
+read_spec.m:27-38, preload_qsos.m:18-67, MATLAB's median, and its columns path against its astropy path.
+The product's numeric stage runs on the GPU only (tests/test_gpu_ingest.py)."""
 import shutil
 from pathlib import Path
 
@@ -8,8 +10,8 @@ import numpy as np
 import pytest
 
 from gp_dla_detection_amd import ingest as I
-from gp_dla_detection_amd import matv73 as M
 from gp_dla_detection_amd import parameters as P
+from oracle import ingest_oracle as O
 
 GOLDEN = Path(__file__).parent / "golden"
 
@@ -28,46 +30,68 @@ def test_bintable_reader_matches_astropy_file():
     assert k64.tolist() == [1, -2, 3, 2 ** 40, -(2 ** 40)]
 
 
-def test_read_spec_rules():
+def test_oracle_read_spec_rules():
     exp = np.load(GOLDEN / "speclite_fixture.npz")
-    w, f, nv, pm = I.read_spec(str(GOLDEN / "speclite_fixture.fits"))
+    w, f, nv, pm = O.derive(exp["flux"], exp["loglam"], exp["ivar"], exp["and_mask"])
     assert w.dtype == np.float32                                         # fitsread 'E' -> single
-    assert np.array_equal(w, np.float32(10) ** exp["loglam"])           # :28
+    assert np.array_equal(w, (10.0 ** exp["loglam"].astype(np.float64)).astype(np.float32))   # :28
     with np.errstate(divide="ignore"):
         assert np.array_equal(nv, np.float32(1) / exp["ivar"])          # :31
     want = (exp["ivar"] == 0) | ((exp["and_mask"] & (1 << 23)) != 0)   # :36-38, BRIGHTSKY = bit 24
     assert np.array_equal(pm, want) and pm.any() and (~pm).any()
 
 
+def test_single_power_is_correctly_rounded_over_the_sdss_range():
+    """read_spec.m:28's 10.^loglam in single: the double power rounded once equals the extended-precision
+    value rounded once for EVERY float32 loglam in [3.5, 4.1] (2.3M values: 3162-12589 A), i.e. it is the
+    correctly rounded single there -- the definition the device kernel implements.  numpy's float32
+    power (C powf) is not: it differs on ~20% of them."""
+    lo, hi = np.float32(3.5).view(np.uint32), np.float32(4.1).view(np.uint32)
+    x = np.arange(lo, hi + 1, dtype=np.uint32).view(np.float32)
+    d = (10.0 ** x.astype(np.float64)).astype(np.float32)
+    ld = (np.longdouble(10) ** x.astype(np.longdouble)).astype(np.float32)
+    if np.finfo(np.longdouble).nmant < 63:
+        pytest.skip("no x87 extended long double here")
+    assert np.array_equal(d, ld)
+
+
 def _spectrum(z, n_lo=3400, n_hi=5600, step=1e-4, mask_window=False, seed=0):
+    """fitsread columns (flux, loglam, ivar, and_mask) of a synthetic coadd."""
     rng = np.random.default_rng(seed)
     loglam = np.arange(np.log10(n_lo), np.log10(n_hi), step).astype(np.float32)
-    w = np.float32(10) ** loglam
-    f = rng.normal(3, 0.2, w.size).astype(np.float32)
-    nv = rng.uniform(0.01, 0.02, w.size).astype(np.float32)
-    pm = rng.uniform(size=w.size) < 0.1
+    f = rng.normal(3, 0.2, loglam.size).astype(np.float32)
+    iv = rng.uniform(50, 100, loglam.size).astype(np.float32)
+    iv[rng.uniform(size=loglam.size) < 0.05] = 0
+    am = np.where(rng.uniform(size=loglam.size) < 0.05, 1 << 23, 0).astype(np.int32)
     if mask_window:
-        rest = w / np.float32(1 + z)
-        pm |= (rest >= 1310) & (rest <= 1325)
-    return w, f, nv, pm
+        rest = (10.0 ** loglam.astype(np.float64)).astype(np.float32) / np.float32(1 + z)
+        iv[(rest >= 1310) & (rest <= 1325)] = 0
+    return f, loglam, iv, am
 
 
-def test_preload_qsos_flags_normalisation_and_range():
-    z = np.array([2.5, 2.5, 2.5, 3.2, 2.5])
-    flags = np.array([0, 1, 0, 0, 0], dtype=np.uint8)
+CASES_Z = np.array([2.5, 2.5, 2.5, 3.2, 2.5])
+CASES_FLAGS = np.array([0, 1, 0, 0, 0], dtype=np.uint8)
+
+
+def preload_cases():
+    """Five catalogue entries: plain, pre-filtered, masked normalisation window, too few pixels, plain."""
     specs = {0: _spectrum(2.5, seed=1), 2: _spectrum(2.5, mask_window=True, seed=2),
              3: _spectrum(3.2, n_lo=5000, seed=3), 4: _spectrum(2.5, seed=4)}
-    out = I.preload_qsos(z, [0, 1, 2, 3, 4], [0] * 5, [0] * 5, flags, lambda p, m, f: specs[p])
+    return CASES_Z, CASES_FLAGS, [specs.get(q) for q in range(5)]
+
+
+def check_preload_rules(out, z, cols):
+    """preload_qsos.m's rules, restated inline, on a result dict (the oracle's or the device's)."""
     ff = out["filter_flags"]
     assert ff[1] == 1                                                   # already filtered: skipped
     assert ff[2] == 4                                                   # bit 3: no normalising pixel
     assert ff[3] == 8                                                   # bit 4: < min_num_pixels
     assert ff[0] == 0 and ff[4] == 0
     for q in (0, 4):
-        w, f, nv, pm = specs[q]
+        w, f, nv, pm = O.derive(*cols[q])
         rest = w / np.float32(1 + z[q])
         win = (rest >= P.NORMALIZATION_MIN_LAMBDA) & (rest <= P.NORMALIZATION_MAX_LAMBDA) & ~pm
-        med = np.median(f[win])
+        med = O.matlab_median(f[win])
         assert out["all_normalizers"][q] == med
         ind = (rest >= P.LOADING_MIN_LAMBDA) & (rest <= P.LOADING_MAX_LAMBDA)
         first, last = np.flatnonzero(ind)[[0, -1]]
@@ -77,71 +101,17 @@ def test_preload_qsos_flags_normalisation_and_range():
             keep[avail[avail > last].min()] = True
         if (avail < first).any():                       # MATLAB: ind(max([])) = true is a no-op
             keep[avail[avail < first].max()] = True
-        assert np.array_equal(out["all_wavelengths"][q], w[keep].astype(np.float64))
-        assert np.array_equal(out["all_flux"][q], (f / med)[keep].astype(np.float64))
-        assert np.array_equal(out["all_noise_variance"][q], (nv / (med * med))[keep].astype(np.float64))
+        assert np.array_equal(out["all_wavelengths"][q], w[keep])
+        assert np.array_equal(out["all_flux"][q], (f / med)[keep])
+        assert np.array_equal(out["all_noise_variance"][q], (nv / (med * med))[keep])
         assert np.array_equal(out["all_pixel_mask"][q], pm[keep])
-    assert out["all_wavelengths"][2].size == 0 and out["all_normalizers"][2] == 0
+    assert out["all_wavelengths"][2] is None or out["all_wavelengths"][2].size == 0
+    assert out["all_normalizers"][2] == 0
 
 
-def test_run_preload_qsos_tree(tmp_path):
-    spectra = tmp_path / "dr12q" / "spectra"
-    for plate, mjd, fiber in ((4000, 55000, 12), (4001, 55001, 7)):
-        d = spectra / str(plate)
-        d.mkdir(parents=True)
-        shutil.copy(GOLDEN / "speclite_fixture.fits", d / f"spec-{plate}-{mjd}-{fiber:04d}.fits")
-    proc = tmp_path / "dr12q" / "processed"
-    proc.mkdir(parents=True)
-    M.savemat73(str(proc / "catalog.mat"), dict(z_qsos=np.array([2.03, 2.5]), plates=np.array([4000, 4001.0]),
-                                                mjds=np.array([55000, 55001.0]), fiber_ids=np.array([12, 7.0]),
-                                                filter_flags=np.array([0, 2], dtype=np.uint8)))
-    out = I.run_preload_qsos(str(tmp_path), "dr12q")
-    assert out["filter_flags"].tolist() == [8, 2]        # too few in-range pixels in the fixture; pre-filtered
-    cat = M.loadmat73(str(proc / "catalog.mat"))
-    assert cat["filter_flags"].ravel().tolist() == [8, 2]
-    pre = M.loadmat73(str(proc / "preloaded_qsos.mat"))
-    assert pre["all_flux"].shape == (2, 1) and float(pre["min_num_pixels"][0, 0]) == 200
-
-
-def _spectra_tree(tmp_path):
-    spectra = tmp_path / "dr12q" / "spectra"
-    for plate, mjd, fiber in ((4000, 55000, 12), (4001, 55001, 7)):
-        d = spectra / str(plate)
-        d.mkdir(parents=True)
-        shutil.copy(GOLDEN / "speclite_fixture.fits", d / f"spec-{plate}-{mjd}-{fiber:04d}.fits")
-    proc = tmp_path / "dr12q" / "processed"
-    proc.mkdir(parents=True)
-    return proc
-
-
-def test_run_preload_qsos_appends_in_place(tmp_path):
-    """preload_qsos.m:82-83 save(..., 'filter_flags', '-append'): a MATLAB catalog.mat with
-    containers.Map objects (libhdf5-written fixture) keeps every byte except filter_flags' data."""
-    proc = _spectra_tree(tmp_path)
-    shutil.copy(GOLDEN / "catalog_mcos.mat", proc / "catalog.mat")
-    before = (proc / "catalog.mat").read_bytes()
-    assert M.rewrite_blockers(str(proc / "catalog.mat"))          # the Maps cannot round-trip
-    out = I.run_preload_qsos(str(tmp_path), "dr12q")
-    assert out["filter_flags"].tolist() == [8, 2] and out["filter_flags_path"].endswith("catalog.mat")
-    after = (proc / "catalog.mat").read_bytes()
-    diff = [i for i in range(len(before)) if before[i] != after[i]]
-    assert len(before) == len(after) and len(diff) == 1           # the one flag byte that changed
-    cat = M.loadmat73(str(proc / "catalog.mat"))
-    assert cat["filter_flags"].ravel().tolist() == [8, 2] and cat["filter_flags"].dtype == np.uint8
-
-
-def test_run_preload_qsos_never_rewrites_objects(tmp_path, monkeypatch):
-    """When filter_flags cannot be overwritten in place and the file holds MATLAB objects, the
-    catalog is left untouched and the flags go to a sidecar file."""
-    proc = _spectra_tree(tmp_path)
-    shutil.copy(GOLDEN / "catalog_mcos.mat", proc / "catalog.mat")
-    before = (proc / "catalog.mat").read_bytes()
-    monkeypatch.setattr(M, "update_variable", lambda *a, **k: False)
-    with pytest.warns(UserWarning, match="not rewritten"):
-        out = I.run_preload_qsos(str(tmp_path), "dr12q")
-    assert (proc / "catalog.mat").read_bytes() == before
-    side = M.loadmat73(out["filter_flags_path"])
-    assert side["filter_flags"].ravel().tolist() == [8, 2]
+def test_oracle_preload_rules():
+    z, flags, cols = preload_cases()
+    check_preload_rules(O.preload_from_columns(z, flags, cols), z, cols)
 
 
 def test_own_fits_writer_roundtrip(tmp_path):
@@ -168,15 +138,12 @@ def _has_astropy():
     return subprocess.run([H5PY_PY, "-c", "import astropy.io.fits"], capture_output=True).returncode == 0
 
 
-@pytest.mark.skipif(not _has_astropy(), reason="no interpreter with astropy (GPU box)")
-def test_preload_matches_the_oracle_restatement(tmp_path):
-    """Product read_spec + preload_qsos against oracle/ingest_oracle.py, the line-by-line
-    restatement of read_spec.m and preload_qsos.m that reads the FITS files with astropy (run with
-    the interpreter that has it).  Cases: plain spectra (odd and even counts in the normalisation
-    window), a pre-filtered entry, a masked normalisation window (bit 3), too few pixels (bit 4),
-    NaN fluxes in the window, BRIGHTSKY-masked pixels, loading-range edges with and without an
-    unmasked neighbour.  Every saved variable must agree bit for bit (cells widened to double)."""
-    import subprocess
+def write_oracle_cases(tmp_path):
+    """Eight catalogue entries written as speclite files that take every branch of preload_qsos.m:
+    plain spectra (odd and even counts in the normalisation window), a pre-filtered entry, a masked
+    normalisation window (bit 3), too few pixels (bit 4), NaN fluxes in the window, BRIGHTSKY-masked
+    pixels, loading-range edges with and without an unmasked neighbour.  Returns the catalogue columns
+    and the spectra directory."""
     from fits_writer import write_speclite
     rng = np.random.default_rng(17)
     spectra = tmp_path / "spectra"
@@ -188,8 +155,7 @@ def test_preload_matches_the_oracle_restatement(tmp_path):
     z, plates, mjds, fibers, flags = [], [], [], [], []
     for q, (zq, lo, hi, pre, mwin, nanw, mfirst) in enumerate(cases):
         ll = np.arange(np.log10(lo), np.log10(hi), 1e-4).astype(np.float32)
-        w = np.float32(10) ** ll
-        rest = w / np.float32(1 + zq)
+        rest = (10.0 ** ll.astype(np.float64)).astype(np.float32) / np.float32(1 + zq)
         f = rng.normal(3.0, 0.4, ll.size).astype(np.float32)
         iv = rng.uniform(20, 80, ll.size).astype(np.float32)
         iv[rng.uniform(size=ll.size) < 0.05] = 0
@@ -209,11 +175,21 @@ def test_preload_matches_the_oracle_restatement(tmp_path):
         d.mkdir(parents=True, exist_ok=True)
         write_speclite(str(d / f"spec-{p}-{m}-{fi:04d}.fits"), f, ll, iv, am)
         z.append(zq); plates.append(p); mjds.append(m); fibers.append(fi); flags.append(pre)
-    got = I.preload_qsos(z, plates, mjds, fibers, np.array(flags, np.uint8),
-                         lambda p, m, f: I.read_spec(I.spec_filename(str(spectra), p, m, f)))
+    return (np.array(z), np.array(plates), np.array(mjds), np.array(fibers), np.array(flags, np.uint8)), spectra
+
+
+@pytest.mark.skipif(not _has_astropy(), reason="no interpreter with astropy (GPU box)")
+def test_oracle_columns_path_equals_its_astropy_path(tmp_path):
+    """The oracle's columns restatement (what the GPU tests run on the box, fed by the host FITS reader)
+    against the same oracle reading the files with astropy under python3.9: every saved variable bit
+    for bit on the eight branch cases."""
+    import subprocess
+    (z, plates, mjds, fibers, flags), spectra = write_oracle_cases(tmp_path)
+    cols = [None if flags[i] > 0 else I.read_spec_columns(I.spec_filename(str(spectra), plates[i], mjds[i], fibers[i]))
+            for i in range(z.size)]
+    got = O.preload_from_columns(z, flags, cols)
     job = tmp_path / "job.npz"
-    np.savez(job, z_qsos=np.array(z), plates=np.array(plates), mjds=np.array(mjds), fiber_ids=np.array(fibers),
-             filter_flags=np.array(flags, np.uint8), spectra_dir=str(spectra))
+    np.savez(job, z_qsos=z, plates=plates, mjds=mjds, fiber_ids=fibers, filter_flags=flags, spectra_dir=str(spectra))
     oracle = Path(__file__).resolve().parents[1] / "oracle" / "ingest_oracle.py"
     res = subprocess.run([H5PY_PY, "-B", str(oracle), str(job), str(tmp_path / "out.npz")], capture_output=True,
                          text=True)
@@ -223,21 +199,23 @@ def test_preload_matches_the_oracle_restatement(tmp_path):
     assert sorted(set(got["filter_flags"].tolist())) == [0, 1, 4, 8]          # every branch exercised
     np.testing.assert_array_equal(got["all_normalizers"], want["all_normalizers"])
     for key in ("all_wavelengths", "all_flux", "all_noise_variance", "all_pixel_mask"):
-        for q in range(len(cases)):
+        for q in range(z.size):
             name = f"{key}__{q}"
             if name in want.files:
-                np.testing.assert_array_equal(got[key][q], want[name].astype(got[key][q].dtype), err_msg=name)
+                np.testing.assert_array_equal(got[key][q], want[name], err_msg=name)
             else:
-                assert got[key][q].size == 0, name
+                assert got[key][q] is None, name
 
 
 def test_nanmedian_is_matlabs():
-    """median.m's meanof for an even count (a + (b - a) / 2 for finite same-sign a, b), NaNs dropped,
-    in single: cases where numpy's (a + b) / 2 rounds differently."""
+    """The oracle's median.m: meanof for an even count (a + (b - a) / 2 for finite same-sign a, b), NaNs
+    dropped by the caller, in single: cases where numpy's (a + b) / 2 rounds differently."""
+    def nanmedian(v):
+        return O.matlab_median(v[~np.isnan(v)])
     f = np.float32
     a, b = f(1.0000001), f(3.9999998)
     v = np.array([b, np.nan, a], dtype=np.float32)
-    assert I.nanmedian(v) == a + (b - a) / f(2)
+    assert nanmedian(v) == a + (b - a) / f(2)
     rng = np.random.default_rng(3)
     seen = 0
     for _ in range(2000):
@@ -245,7 +223,20 @@ def test_nanmedian_is_matlabs():
         s = np.sort(x)
         lo, hi = s[x.size // 2 - 1], s[x.size // 2]
         want = lo + (hi - lo) / f(2) if np.sign(lo) == np.sign(hi) else (lo + hi) / f(2)
-        assert I.nanmedian(x) == want and I.nanmedian(x).dtype == np.float32
+        assert nanmedian(x) == want and nanmedian(x).dtype == np.float32
         seen += want != np.median(x)
     assert seen > 0                                   # numpy's median differs on some of these
-    assert np.isnan(I.nanmedian(np.array([np.nan], np.float32)))
+    assert np.isnan(nanmedian(np.array([np.nan], np.float32)))
+
+
+def test_product_has_no_cpu_path():
+    """read_spec's rules and preload_qsos's numeric stage run on the device only: without one they fail
+    loudly (no numpy fallback)."""
+    from gp_dla_detection_amd import _lib as L
+    if L.load().gpdla_device_count() > 0:
+        pytest.skip("a HIP device is present")
+    with pytest.raises(L.GpdlaError, match="no HIP device"):
+        I.read_spec(str(GOLDEN / "speclite_fixture.fits"))
+    z, flags, cols = preload_cases()
+    with pytest.raises(L.GpdlaError, match="no HIP device"):
+        I.preload_batch(z, flags, cols)
