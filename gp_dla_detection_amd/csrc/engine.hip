@@ -705,15 +705,18 @@ int gpdla_engine_process(gpdla_engine* e, const gpdla_spectra* sp, const gpdla_r
     int rc;
     if ((rc = grow(&e->d_meta, &e->cap_meta, per_batch))) return rc;
     if ((rc = grow(&e->d_info, &e->cap_q, (size_t)QB))) return rc;
-    // + one LDS row of slack: the staging DMA reads whole 1 KiB pieces (kernels.hip stage_chunk)
-    if ((rc = grow(&e->d_panel, &e->cap_slots,
+    // + one LDS row of slack: the staging DMA reads whole 1 KiB pieces (kernels.hip stage_chunk).  The
+    // int8 panel batches never read the Khatri-Rao panel (prep skips it, convert_gemm_i8_kernel forms
+    // the products from the M rows), so they do not grow it (a few hundred MB at k = 50)
+    if (!batch_gemm_i8 &&
+        (rc = grow(&e->d_panel, &e->cap_slots,
                    (size_t)(slots * row + (e->gemm ? gemm_panel_slack(row) : panel_lds_row_doubles(e->K)))))) return rc;
     if ((rc = grow(&e->d_lam, &e->cap_lam, (size_t)lams))) return rc;
     if (e->gemm) {
       const int64_t ldm = gemm_ldm(e->K);
       if ((rc = grow(&e->d_pm, &e->cap_pm, (size_t)(slots * ldm + gemm_panel_slack(ldm))))) return rc;
       // the rows gemm_f64 reads past the batch's last slot: zero (finite, against zero weights)
-      HIP_TRY(hipMemsetAsync(e->d_panel + slots * row, 0, gemm_panel_slack(row) * 8, st));
+      if (!batch_gemm_i8) HIP_TRY(hipMemsetAsync(e->d_panel + slots * row, 0, gemm_panel_slack(row) * 8, st));
       HIP_TRY(hipMemsetAsync(e->d_pm + slots * ldm, 0, gemm_panel_slack(ldm) * 8, st));
       if ((rc = grow(&e->d_srow, &e->cap_srow, (size_t)slots * 8))) return rc;
       const int64_t sets = e->panel_streams;  // one workspace set per panel stream

@@ -153,13 +153,23 @@ class Engine:
 
     def set_stream(self, stream_handle: int | None) -> None:
         """Order the engine's kernels on an external hipStream_t handle (e.g. torch's
-        ``current_stream().cuda_stream``); None restores the engine's own stream.  Handle 0 is the
-        null stream (torch's default stream): gpdla_engine_use_null_stream, since the C ABI reads a
-        NULL handle as "restore"."""
+        ``current_stream().cuda_stream``).  Handle 0 is the null stream (torch's default stream,
+        gpdla_engine_use_null_stream), since the C ABI reads a NULL handle as "restore".  None restores
+        the engine's own stream, as ``restore_stream()`` does; before round 6, 0 meant "restore" too, so a
+        caller passing 0 for that now gets the null stream -- a warning says so."""
         if stream_handle == 0:
+            import warnings
+            warnings.warn("Engine.set_stream(0) selects the null stream (torch's default stream); use "
+                          "restore_stream() or set_stream(None) for the engine's own stream", stacklevel=2)
             L.check(self.lib.gpdla_engine_use_null_stream(self._h))
+        elif stream_handle is None:
+            self.restore_stream()
         else:
-            L.check(self.lib.gpdla_engine_set_stream(self._h, C.c_void_p(stream_handle or 0)))
+            L.check(self.lib.gpdla_engine_set_stream(self._h, C.c_void_p(stream_handle)))
+
+    def restore_stream(self) -> None:
+        """Back to the engine's own (non-blocking) stream."""
+        L.check(self.lib.gpdla_engine_set_stream(self._h, C.c_void_p(0)))
 
     def set_panel_streams(self, n: int) -> None:
         """Panel-GEMM paths: spectra of a batch alternate over n (1..4) compute streams."""

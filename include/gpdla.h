@@ -138,12 +138,17 @@ typedef struct gpdla_results {
   int32_t* num_pixels;                 /* [Q]   n, unmasked in-range pixels (may be NULL) */
 } gpdla_results;
 
-/* Kernel-time accounting (HIP events on the engine's stream), cumulative since create/reset. */
+/* Kernel-time accounting (HIP events on the engine's stream), cumulative since create/reset.
+ * likelihood_ms spans each batch's likelihood work on the engine's stream.  contraction_ms is the sum
+ * of the event spans around each Gram/u GEMM launch (panel-GEMM paths): with one panel stream those
+ * spans lie inside likelihood_ms; with panel_streams > 1 the launches of different streams overlap in
+ * time and each span also counts the time its launch waits behind the other streams' kernels, so the
+ * sum is not part of likelihood_ms and can exceed it (set 1 panel stream to time the kernel alone). */
 typedef struct gpdla_stats {
   double prep_ms, likelihood_ms, reduce_ms;
   int64_t prep_launches, likelihood_launches, reduce_launches;
   int64_t spectra, sample_evals;       /* sample_evals = sum over spectra of S (null evals excluded) */
-  double contraction_ms;               /* panel-GEMM paths: the Gram/u GEMM launches (part of likelihood_ms) */
+  double contraction_ms;               /* panel-GEMM paths: summed GEMM launch spans (see above) */
   int64_t contraction_launches;
 } gpdla_stats;
 
