@@ -1,7 +1,8 @@
 // Spectrum ingest on gfx950: read_spec.m's derived columns and preload_qsos.m's numeric
 // stage, batched over a CSR of the catalogue's spectra (FITS parsing stays on the host).
 //
-//   read_spec.m:27-28   wavelengths = 10.^loglam     single, rounded once: (float)pow(10.0, (double)loglam)
+//   read_spec.m:27-28   wavelengths = 10.^loglam     single, rounded once from double (wavelength():
+//                                                   exp2 with a rounding-boundary guard, else pow)
 //                                                   -- the correctly rounded single over every float32
 //                                                   loglam in [3.5, 4.1] (checked exhaustively against
 //                                                   extended precision); MATLAB's own single pow is
@@ -9,7 +10,10 @@
 //   read_spec.m:30-31   noise_variance = 1 ./ ivar   single IEEE division
 //   read_spec.m:36-38   pixel_mask = ivar == 0 | bitget(and_mask, 24)
 //   preload_qsos.m:19-21  entries with filter_flags > 0 are skipped (empty cells)
-//   preload_qsos.m:26     rest = wavelengths / (1 + z)  (single: the double 1 + z rounded to single)
+//   preload_qsos.m:26     rest = wavelengths / (1 + z)  (single: the double 1 + z rounded to single);
+//                         the three range tests on rest become loglam intervals found once per
+//                         spectrum (rest is monotone in loglam; see first_key_past), so only the cells'
+//                         wavelengths need the pow
 //   preload_qsos.m:29-33  nanmedian of the flux over unmasked pixels with rest in [1310, 1325]: the
 //                         window's values gathered in LDS, NaNs dropped, bitonic-sorted, MATLAB's
 //                         median (meanof(a, b) = a + (b - a) / 2 for finite same-sign a, b)
@@ -20,11 +24,13 @@
 //                         and the last unmasked pixel before its first
 //   preload_qsos.m:64-67  the selected pixels, in order (a block-wide ordered compaction)
 //
-// One 256-thread block per spectrum in each of two launches: the first finds the median, the flags,
+// Three launches: the range ends as loglam keys (one wave per spectrum); then one 256-thread block
+// per spectrum in each of two: the median, the flags,
 // the loading range's ends and neighbours and the cell length; the host turns the lengths into CSR
-// offsets; the second writes the cells (an order-preserving compaction: the selection is a mask, as in
-// the reference, not assumed contiguous).  HBM-bound elementwise work: the input columns are read twice
-// (16 B per pixel each time) and ~13 B per selected pixel written.
+// offsets; the second writes the cells (an order-preserving compaction over the span from the lower
+// neighbour to the upper one: the selection is a mask, as in the reference, not assumed contiguous).
+// HBM-bound elementwise work: loglam, ivar and and_mask read once per pixel (12 B), flux only in the
+// normalisation window; the span's columns re-read and 13 B per selected pixel written.
 #include <hip/hip_runtime.h>
 
 #include <climits>
@@ -40,6 +46,13 @@ namespace {
 
 constexpr int kIngestThreads = 256;
 constexpr int kWindowCap = 4096;            // normalisation-window values per spectrum held in LDS
+#ifndef GPDLA_INGEST_SCAN_UNROLL
+#define GPDLA_INGEST_SCAN_UNROLL 4
+#endif
+constexpr int kUnroll = GPDLA_INGEST_SCAN_UNROLL;   // scan rounds whose loads are issued together
+#ifndef GPDLA_INGEST_WRITE_UNROLL
+#define GPDLA_INGEST_WRITE_UNROLL 4           // write-pass rounds whose loads are issued together
+#endif
 
 struct IngestArgs {
   int64_t Q;
@@ -56,6 +69,7 @@ struct IngestArgs {
   float* median;
   int64_t* count;                           // cell length (0 when skipped or filtered)
   int64_t* ends;                            // [Q][4]: first, last of the loading range, after, before (-1 = none)
+  int32_t* keys;                            // [Q][6]: the three ranges as loglam order keys [lo, hi)
   int32_t* status;                          // 1: a normalisation window over kWindowCap values
   // pass-2 outputs
   const int64_t* out_off;                   // [Q + 1]
@@ -66,21 +80,90 @@ struct IngestArgs {
   double* normalizers;
 };
 
-struct PixelView {
-  float w, nv, rest;
-  bool mask;
-};
-
-__device__ inline PixelView pixel(const IngestArgs& a, int64_t i, float one_pz) {
-  PixelView v;
-  v.w = (float)pow(10.0, (double)a.loglam[i]);                                  // read_spec.m:28
-  v.nv = 1.0f / a.ivar[i];                                                        // :31
-  v.mask = a.ivar[i] == 0.0f || ((a.and_mask[i] >> (a.p.brightsky_bit - 1)) & 1); // :36-38
-  v.rest = v.w / one_pz;                                                          // preload_qsos.m:26
-  return v;
+__device__ inline bool pixel_mask(const IngestArgs& a, int64_t i) {
+  return a.ivar[i] == 0.0f || ((a.and_mask[i] >> (a.p.brightsky_bit - 1)) & 1);    // read_spec.m:36-38
 }
 
-__device__ inline bool in_range(float r, double lo, double hi) { return (double)r >= lo && (double)r <= hi; }
+// read_spec.m:28, 10.^loglam in single, correctly rounded: 2^(loglam log2 10) in double (relative error
+// < 3e-15: the product's two roundings at |t| < 120 and exp2's ulp) rounded once to single -- the
+// correctly rounded single unless the double lies within 1e-14 of a rounding boundary (a midpoint
+// between singles; half that spacing below a power of two), where the double pow decides.
+__device__ inline float wavelength(float loglam) {
+  const double t = (double)loglam * 3.3219280948873623478703194;
+  if (!(fabs(t) < 120.0)) return (float)pow(10.0, (double)loglam);               // NaN, inf, outside
+  const double wd = exp2(t);
+  const float w = (float)wd;
+  const double h = ldexp(1.0, ilogbf(w) - 24);                                    // half an ulp of w
+  const double r = fabs(wd - (double)w), tol = 1e-14 * wd;
+  if (fabs(r - h) <= tol || fabs(r - 0.5 * h) <= tol) return (float)pow(10.0, (double)loglam);
+  return w;
+}
+
+// The three rest-frame ranges of preload_qsos.m (:29 normalisation, :41 model, :56 loading) as
+// intervals of loglam.  rest(L) = single(single(10^L) / single(1 + z)) (:26) is non-decreasing in L:
+// the correctly rounded single 10^L is, and so are the IEEE division by a positive constant and the
+// widening to double for the comparison.  So {L : lo <= rest(L) <= hi} is an interval of float32 L,
+// found once per spectrum -- its ends are the first L with rest(L) >= lo and the first with
+// rest(L) > hi -- and each pixel's test is two integer compares on its loglam's order key, exactly the
+// reference's comparison with no per-pixel pow.  Order key: the float's bits, negatives mirrored, so
+// that key order is float order (NaN keys land beyond +inf or below -inf and are excluded apart).
+constexpr int kRanges = 3;
+constexpr int32_t kKeyMin = (int32_t)0x807FFFFF;         // key(-inf)
+constexpr int32_t kKeyNone = 0x7F800001;                 // one past key(+inf): "no such L"
+
+__device__ inline int32_t order_key(float f) {
+  const int32_t i = __float_as_int(f);
+  return i >= 0 ? i : i ^ 0x7FFFFFFF;
+}
+__device__ inline float key_float(int32_t k) { return __int_as_float(k >= 0 ? k : k ^ 0x7FFFFFFF); }
+
+__device__ inline bool past(float loglam, float one_pz, double end, bool strict) {
+  const double r = (double)(wavelength(loglam) / one_pz);
+  return strict ? r > end : r >= end;
+}
+
+// The first key whose L is past `end` (kKeyNone if none).  The step lies within an ulp or two of the
+// double-precision estimate log10(end (1 + z)); lanes 10 j .. 10 j + 9 of a wave test the ten keys
+// around it for end j (six ends, one ballot); an end whose step is not among its ten keys (a
+// degenerate end or z) is found by its lane's binary search over every key.
+__device__ inline int32_t find_key(double end, bool strict, float one_pz, unsigned group) {
+  const int32_t c = order_key((float)log10(end * (double)one_pz)) - 5;
+  if (group != 0 && !(group & 1)) return c + __ffs(group) - 1;
+  int64_t lo = kKeyMin, hi = (int64_t)kKeyNone;                                   // answer in [lo, hi]
+  while (lo < hi) {
+    const int64_t mid = lo + (hi - lo) / 2;
+    if (past(key_float((int32_t)mid), one_pz, end, strict)) hi = mid; else lo = mid + 1;
+  }
+  return (int32_t)lo;
+}
+
+enum : unsigned { kNormWindow = 1, kModelRange = 2, kLoadingRange = 4 };
+
+__device__ inline unsigned range_bits(float loglam, const int32_t* keys) {
+  const int32_t k = order_key(loglam);
+  unsigned bits = 0;
+#pragma unroll
+  for (int r = 0; r < kRanges; ++r) bits |= (k >= keys[2 * r] && k < keys[2 * r + 1]) ? 1u << r : 0u;
+  return isnan(loglam) ? 0u : bits;
+}
+
+// The six interval ends of each spectrum, one wave per spectrum (pass 0: the pow stays out of the
+// scan's register budget).
+constexpr int kKeySpectraPerBlock = 4;
+
+__global__ __launch_bounds__(64 * kKeySpectraPerBlock) void preload_keys_kernel(IngestArgs a) {
+  const int64_t q = (int64_t)blockIdx.x * kKeySpectraPerBlock + (threadIdx.x >> 6);
+  if (q >= a.Q || a.flags_in[q] > 0) return;
+  const double end[2 * kRanges] = {a.p.normalization_min_lambda, a.p.normalization_max_lambda, a.p.min_lambda,
+                                   a.p.max_lambda, a.p.loading_min_lambda, a.p.loading_max_lambda};
+  const float one_pz = (float)(1.0 + a.z[q]);
+  const int lane = threadIdx.x & 63, j = min(lane / 10, 2 * kRanges - 1);
+  const int32_t c = order_key((float)log10(end[j] * (double)one_pz)) - 5;
+  const bool t = lane < 10 * 2 * kRanges && past(key_float(c + lane % 10), one_pz, end[j], j & 1);
+  const uint64_t bal = __ballot(t);
+  if (lane < 2 * kRanges)
+    a.keys[q * 2 * kRanges + lane] = find_key(end[lane], lane & 1, one_pz, (unsigned)(bal >> (10 * lane)) & 0x3FFu);
+}
 
 template <typename T, typename Op>
 __device__ inline T block_reduce(T v, T* red, Op op) {
@@ -112,21 +195,41 @@ __global__ __launch_bounds__(kIngestThreads) void preload_scan_kernel(IngestArgs
   }
   if (threadIdx.x == 0) nwin = 0;
   __syncthreads();
-  const float one_pz = (float)(1.0 + a.z[q]);
+  int32_t kr[2 * kRanges];
+#pragma unroll
+  for (int j = 0; j < 2 * kRanges; ++j) kr[j] = a.keys[q * 2 * kRanges + j];
   int32_t nrange = 0;
   int64_t nload = 0, first = LLONG_MAX, last = -1;
-  for (int64_t i = b + threadIdx.x; i < e; i += kIngestThreads) {
-    const PixelView v = pixel(a, i, one_pz);
-    const float fl = a.flux[i];
-    if (!v.mask && in_range(v.rest, a.p.normalization_min_lambda, a.p.normalization_max_lambda) && !isnan(fl)) {
-      const int slot = atomicAdd(&nwin, 1);                                      // :29-33 (order: sorted below)
-      if (slot < kWindowCap) win[slot] = fl;
+  for (int64_t c = b + threadIdx.x; c < e; c += kIngestThreads * kUnroll) {
+    float ll[kUnroll], iv[kUnroll];
+    int32_t am[kUnroll];
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {                                           // all loads first
+      const int64_t i = c + u * kIngestThreads;
+      const bool ok = i < e;
+      ll[u] = ok ? a.loglam[i] : 0.0f;
+      iv[u] = ok ? a.ivar[i] : 0.0f;
+      am[u] = ok ? a.and_mask[i] : 0;
     }
-    nrange += !v.mask && in_range(v.rest, a.p.min_lambda, a.p.max_lambda);       // :41-43
-    if (in_range(v.rest, a.p.loading_min_lambda, a.p.loading_max_lambda)) {     // :56-57
-      ++nload;
-      first = min(first, i - b);
-      last = max(last, i - b);
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      const int64_t i = c + u * kIngestThreads;
+      if (i >= e) break;
+      const unsigned r = range_bits(ll[u], kr);
+      const bool mask = iv[u] == 0.0f || ((am[u] >> (a.p.brightsky_bit - 1)) & 1);
+      if (!mask && (r & kNormWindow)) {
+        const float fl = a.flux[i];                                               // flux read in the window only
+        if (!isnan(fl)) {
+          const int slot = atomicAdd(&nwin, 1);                                  // :29-33 (order: sorted below)
+          if (slot < kWindowCap) win[slot] = fl;
+        }
+      }
+      nrange += !mask && (r & kModelRange);                                       // :41-43
+      if (r & kLoadingRange) {                                                    // :56-57
+        ++nload;
+        first = min(first, i - b);
+        last = max(last, i - b);
+      }
     }
   }
   nrange = block_reduce(nrange, red32, [](int32_t x, int32_t y) { return x + y; });
@@ -174,22 +277,24 @@ __global__ __launch_bounds__(kIngestThreads) void preload_scan_kernel(IngestArgs
       med = (slo == shi && isfinite(lo) && isfinite(hi)) ? lo + (hi - lo) / 2.0f : (lo + hi) / 2.0f;
     }
   }
-  // the loading range's unmasked neighbours (:60-62)
+  // the loading range's unmasked neighbours (:60-62).  No pixel outside [first, last] is in the loading
+  // range (they are its extreme indices), so the neighbours are the nearest unmasked pixels on either
+  // side: found 256 at a time outward from the range, stopping at the first chunk that holds one.
   int64_t after = LLONG_MAX, before = -1;
   if (last >= 0) {
-    for (int64_t i = b + threadIdx.x; i < e; i += kIngestThreads) {
-      const int64_t j = i - b;
-      if (j > last || j < first) {
-        const PixelView v = pixel(a, i, one_pz);
-        if (!v.mask && !in_range(v.rest, a.p.loading_min_lambda, a.p.loading_max_lambda)) {
-          if (j > last) after = min(after, j);
-          if (j < first) before = max(before, j);
-        }
-      }
+    for (int64_t c = b + last + 1; c < e; c += kIngestThreads) {
+      const int64_t i = c + threadIdx.x;
+      if (i < e && !pixel_mask(a, i)) after = min(after, i - b);
+      after = block_reduce(after, red64, [](int64_t x, int64_t y) { return x < y ? x : y; });
+      if (after != LLONG_MAX) break;
+    }
+    for (int64_t c = b + first - 1; c >= b; c -= kIngestThreads) {
+      const int64_t i = c - threadIdx.x;
+      if (i >= b && !pixel_mask(a, i)) before = max(before, i - b);
+      before = block_reduce(before, red64, [](int64_t x, int64_t y) { return x > y ? x : y; });
+      if (before >= 0) break;
     }
   }
-  after = block_reduce(after, red64, [](int64_t x, int64_t y) { return x < y ? x : y; });
-  before = block_reduce(before, red64, [](int64_t x, int64_t y) { return x > y ? x : y; });
   if (threadIdx.x != 0) return;
   ends[0] = last >= 0 ? first : -1;
   ends[1] = last;
@@ -218,36 +323,54 @@ __global__ __launch_bounds__(kIngestThreads) void preload_write_kernel(IngestArg
   const int64_t b = a.off[q], e = a.off[q + 1];
   const int64_t* ends = a.ends + q * 4;
   const int64_t after = ends[2], before = ends[3];
-  const float one_pz = (float)(1.0 + a.z[q]);
+  const int32_t klo = a.keys[q * 2 * kRanges + 4], khi = a.keys[q * 2 * kRanges + 5];
   const float med = a.median[q];
   const float med2 = med * med;                                                   // :54 (single)
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   int64_t base = a.out_off[q];
   if (threadIdx.x == 0) a.normalizers[q] = (double)med;                           // :51
-  for (int64_t c0 = b; c0 < e; c0 += kIngestThreads) {
-    const int64_t i = c0 + threadIdx.x;
-    bool sel = false;
-    PixelView v{};
-    if (i < e) {
-      v = pixel(a, i, one_pz);
-      const int64_t j = i - b;
-      sel = in_range(v.rest, a.p.loading_min_lambda, a.p.loading_max_lambda) || j == after || j == before;
+  // nothing outside [before or first, after or last] is selected
+  const int64_t lo = b + (before >= 0 ? before : ends[0]), hi = b + (after >= 0 ? after : ends[1]) + 1;
+  constexpr int kWU = GPDLA_INGEST_WRITE_UNROLL;
+  for (int64_t c0 = lo; c0 < hi; c0 += kIngestThreads * kWU) {
+    float w[kWU], fl[kWU], iv[kWU];
+    int32_t am[kWU];
+#pragma unroll
+    for (int u = 0; u < kWU; ++u) {                                               // every column's loads first
+      const int64_t i = c0 + u * kIngestThreads + threadIdx.x;
+      const bool ok = i < hi;
+      w[u] = ok ? a.loglam[i] : 0.0f;
+      fl[u] = ok ? a.flux[i] : 0.0f;
+      iv[u] = ok ? a.ivar[i] : 0.0f;
+      am[u] = ok ? a.and_mask[i] : 0;
     }
-    const uint64_t bal = __ballot(sel);
-    const int before_me = __popcll(bal & ((1ull << lane) - 1));
-    __syncthreads();
-    if (lane == 0) wave_tot[wave] = __popcll(bal);
-    __syncthreads();
-    int64_t wo = 0;
-    for (int w = 0; w < wave; ++w) wo += wave_tot[w];
-    if (sel) {
-      const int64_t o = base + wo + before_me;
-      a.w_out[o] = v.w;                                                           // :64-67
-      a.f_out[o] = a.flux[i] / med;                                               // :53
-      a.nv_out[o] = v.nv / med2;                                                  // :54
-      a.m_out[o] = v.mask;
+#pragma unroll
+    for (int u = 0; u < kWU; ++u) {
+      const int64_t cu = c0 + u * kIngestThreads;
+      if (cu >= hi) break;                                                        // block-uniform
+      const int64_t i = cu + threadIdx.x;
+      bool sel = false;
+      if (i < hi) {
+        const int64_t j = i - b;
+        const int32_t k = order_key(w[u]);
+        sel = j == after || j == before || (k >= klo && k < khi && !isnan(w[u]));
+      }
+      const uint64_t bal = __ballot(sel);
+      const int before_me = __popcll(bal & ((1ull << lane) - 1));
+      __syncthreads();
+      if (lane == 0) wave_tot[wave] = __popcll(bal);
+      __syncthreads();
+      int64_t wo = 0;
+      for (int k = 0; k < wave; ++k) wo += wave_tot[k];
+      if (sel) {
+        const int64_t o = base + wo + before_me;
+        a.w_out[o] = wavelength(w[u]);                                            // :64-67
+        a.f_out[o] = fl[u] / med;                                                 // :53
+        a.nv_out[o] = (1.0f / iv[u]) / med2;                                      // read_spec.m:31, :54
+        a.m_out[o] = iv[u] == 0.0f || ((am[u] >> (a.p.brightsky_bit - 1)) & 1);   // read_spec.m:36-38
+      }
+      base += wave_tot[0] + wave_tot[1] + wave_tot[2] + wave_tot[3];
     }
-    base += wave_tot[0] + wave_tot[1] + wave_tot[2] + wave_tot[3];
   }
 }
 
@@ -255,7 +378,7 @@ __global__ void read_spec_kernel(int64_t n, const float* loglam, const float* iv
                                  int32_t brightsky_bit, float* w, float* nv, uint8_t* mask) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  w[i] = (float)pow(10.0, (double)loglam[i]);                                     // read_spec.m:28
+  w[i] = wavelength(loglam[i]);                                                   // read_spec.m:28
   nv[i] = 1.0f / ivar[i];                                                         // :31
   mask[i] = ivar[i] == 0.0f || ((and_mask[i] >> (brightsky_bit - 1)) & 1);        // :36-38
 }
@@ -325,7 +448,7 @@ int gpdla_preload_qsos_f32(int32_t device, int64_t num_quasars, const int64_t* o
   HIP_TRY(hipMalloc(&d_pix.p, (size_t)N * 16 + 16));
   HIP_TRY(hipMalloc(&d_z.p, (size_t)Q * 8));
   HIP_TRY(hipMalloc(&d_fl.p, (size_t)Q * 2));
-  HIP_TRY(hipMalloc(&d_res.p, (size_t)Q * (4 + 8 + 32 + 8)));
+  HIP_TRY(hipMalloc(&d_res.p, (size_t)Q * 72));
   HIP_TRY(hipMalloc(&d_status.p, 4));
   HIP_TRY(hipMalloc(&d_ooff.p, (size_t)(Q + 1) * 8));
   char* pix = (char*)d_pix.p;
@@ -354,8 +477,11 @@ int gpdla_preload_qsos_f32(int32_t device, int64_t num_quasars, const int64_t* o
   a.median = (float*)res;
   a.count = (int64_t*)(res + Q * 8);           // 8-byte aligned: Q * 4 rounded by the 2x below
   a.ends = (int64_t*)(res + Q * 16);
+  a.keys = (int32_t*)(res + Q * 48);
   a.status = (int32_t*)d_status.p;
-  // (median at [0, 4Q), count at [8Q, 16Q), ends at [16Q, 48Q) within the Q * 52-byte block)
+  // (median at [0, 4Q), count at [8Q, 16Q), ends at [16Q, 48Q), keys at [48Q, 72Q))
+  preload_keys_kernel<<<(unsigned)((Q + kKeySpectraPerBlock - 1) / kKeySpectraPerBlock), 64 * kKeySpectraPerBlock>>>(a);
+  HIP_TRY(hipGetLastError());
   preload_scan_kernel<<<(unsigned)Q, kIngestThreads>>>(a);
   HIP_TRY(hipGetLastError());
   std::vector<int64_t> count(Q);

@@ -161,3 +161,25 @@ def write_processed_tree(base: str, model: dict, samples: dict, spectra: list, r
                 prior_ind=" prior_catalog.in_dr9 & prior_catalog.los_inds(dla_catalog_name) & "
                           "(prior_catalog.filter_flags == 0)",
                 release=release, test_set_name=release, test_ind="(catalog.filter_flags == 0)")
+
+
+def make_boss_coadd_columns(rng, z_qso: float, n_pixels: int = 4607):
+    """fitsread columns (flux, loglam, ivar, and_mask) of a synthetic full BOSS coadd (3600-10400 A at
+    1e-4 dex, read_spec.m:11-25's classes) for the ingest path: ~4% zero-ivar and ~3% BRIGHTSKY pixels,
+    2% of spectra with a masked 1310-1325 A normalisation window (preload_qsos.m bit 3), 2% with no
+    usable pixel in 911.75-1215.75 A (bit 4), 6% with NaN fluxes in the window."""
+    ll = (np.log10(3600.0) + 1e-4 * np.arange(n_pixels)).astype(np.float32)
+    f = rng.normal(2.0, 0.5, ll.size).astype(np.float32)
+    iv = rng.uniform(1, 50, ll.size).astype(np.float32)
+    iv[rng.uniform(size=ll.size) < 0.04] = 0
+    am = np.where(rng.uniform(size=ll.size) < 0.03, 1 << 23, 0).astype(np.int32)
+    rest = (10.0 ** ll.astype(np.float64)).astype(np.float32) / np.float32(1 + z_qso)
+    win = np.flatnonzero((rest >= 1310) & (rest <= 1325))
+    u = rng.uniform()
+    if u < 0.02:
+        iv[win] = 0
+    elif u < 0.04:
+        iv[(rest >= 911.75) & (rest <= 1215.75)] = 0
+    elif u < 0.10 and win.size:
+        f[win[::5]] = np.nan
+    return f, ll, iv, am

@@ -63,7 +63,7 @@ def read_columns(filename):
 
 def derive(flux, log_wavelengths, ivar, and_mask):
     """read_spec.m:27-38 on the fitsread columns, in single.  10.^loglam is taken correctly rounded to
-    single (the double power rounded once: over every float32 loglam in [3.5, 4.1] that equals the
+    single (the double power rounded once: over every float32 loglam in [3.0, 4.5] that equals the
     extended-precision value rounded to single, tests/test_ingest.py); MATLAB's own single pow is
     unpinned at the last ulp."""
     wavelengths = (10.0 ** np.asarray(log_wavelengths, np.float64)).astype(np.float32)   # :28

@@ -20,6 +20,7 @@ pytestmark = pytest.mark.gpu
 from gp_dla_detection_amd import _lib as L  # noqa: E402
 from gp_dla_detection_amd import ingest as I  # noqa: E402
 from gp_dla_detection_amd import matv73 as M  # noqa: E402
+from gp_dla_detection_amd import synthetic as syn  # noqa: E402
 from oracle import ingest_oracle as O  # noqa: E402
 from test_ingest import check_preload_rules, preload_cases, write_oracle_cases  # noqa: E402
 
@@ -59,9 +60,10 @@ def test_read_spec_fixture_bit_exact():
 
 
 def test_read_spec_every_loglam_of_the_sdss_range():
-    """The device's 10.^loglam in single is the correctly rounded value for every one of the 2.3M float32
-    loglam in [3.5, 4.1]; 1 ./ ivar and the mask rule on random columns alongside."""
-    lo, hi = np.float32(3.5).view(np.uint32), np.float32(4.1).view(np.uint32)
+    """The device's 10.^loglam in single is the correctly rounded value for every one of the 5.2M float32
+    loglam in [3.0, 4.5] (1,000-31,623 A, around SDSS's 3,600-10,400 A); 1 ./ ivar and the mask rule on
+    random columns alongside."""
+    lo, hi = np.float32(3.0).view(np.uint32), np.float32(4.5).view(np.uint32)
     ll = np.arange(lo, hi + 1, dtype=np.uint32).view(np.float32)
     rng = np.random.default_rng(2)
     iv = rng.uniform(0, 100, ll.size).astype(np.float32)
@@ -95,24 +97,86 @@ def test_preload_matches_the_oracle_on_every_branch(tmp_path):
     _assert_equal_results(got, want)
 
 
-def _boss_coadd(rng, z):
-    """Raw fitsread columns of a full BOSS coadd (3600-10400 A at 1e-4 dex), with masks, NaNs, an
-    occasionally masked normalisation window and occasionally too few usable pixels."""
-    ll = (np.log10(3600.0) + 1e-4 * np.arange(4607)).astype(np.float32)
-    f = rng.normal(2.0, 0.5, ll.size).astype(np.float32)
-    iv = rng.uniform(1, 50, ll.size).astype(np.float32)
-    iv[rng.uniform(size=ll.size) < 0.04] = 0
-    am = np.where(rng.uniform(size=ll.size) < 0.03, 1 << 23, 0).astype(np.int32)
-    rest = (10.0 ** ll.astype(np.float64)).astype(np.float32) / np.float32(1 + z)
-    win = np.flatnonzero((rest >= 1310) & (rest <= 1325))
-    u = rng.uniform()
-    if u < 0.02:
-        iv[win] = 0                                         # unnormalisable -> bit 3
-    elif u < 0.04:
-        iv[(rest >= 911.75) & (rest <= 1215.75)] = 0        # too few pixels -> bit 4
-    elif u < 0.10 and win.size:
-        f[win[::5]] = np.nan                                # NaNs dropped by nanmedian
+def _neighbour_cases():
+    """Spectra whose loading-range neighbours sit far from the range (masked runs of 1, 255, 256, 257 and
+    700 pixels on either side; a run ending at the normalisation window, which stays unmasked), none
+    below (everything before masked, or the range starting at pixel 0), plus a spectrum with its pixels
+    permuted (the loading range is a scattered mask, not a slice)."""
+    rng = np.random.default_rng(77)
+    z, cols = [], []
+    for zq, run_after, run_before in ((3.0, 1, 1), (3.6, 255, 256), (3.6, 256, 257), (3.6, 700, 300),
+                                      (3.0, 10 ** 6, 10 ** 6), (2.9, 0, 0)):
+        f, ll, iv, am = syn.make_boss_coadd_columns(rng, zq)
+        iv[(np.arange(iv.size) % 97) == 5] = 0                # scattered masked pixels everywhere
+        am[:] = 0
+        f[np.isnan(f)] = 1.0
+        w, _, _, _ = O.derive(f, ll, iv, am)
+        rest = w / np.float32(1 + zq)
+        ind = np.flatnonzero((rest >= 910) & (rest <= 1217))
+        iv[ind[-1] + 1:ind[-1] + 1 + run_after] = 0
+        iv[max(ind[0] - run_before, 0):ind[0]] = 0
+        iv[(rest >= 1310) & (rest <= 1325)] = 1.0             # keep the normalisation window usable
+        z.append(zq)
+        cols.append((f, ll, iv, am))
+    f, ll, iv, am = syn.make_boss_coadd_columns(rng, 2.6)
+    perm = rng.permutation(f.size)
+    z.append(2.6)
+    cols.append(tuple(c[perm] for c in (f, ll, iv, am)))
+    return np.array(z), np.zeros(len(z), np.uint8), cols
+
+
+def test_preload_neighbour_search_and_scattered_ranges():
+    z, flags, cols = _neighbour_cases()
+    got = I.preload_batch(z, flags, cols)
+    want = O.preload_from_columns(z, flags, cols)
+    assert (want["filter_flags"] == 0).all()
+    _assert_equal_results(got, want)
+
+
+ENDS = (1310.0, 1325.0, 911.75, 1215.75, 910.0, 1217.0)     # set_parameters.m:21-22, 29-30, 33-34
+
+
+def _boundary_spectrum(z, nrange_target=None):
+    """A BOSS grid plus every float32 loglam within 81 ulps of the six range ends at this z, fluxes all
+    distinct (any change of the window's membership moves the median).  With nrange_target, all but
+    that many pixels of [911.75, 1215.75] are masked -- the ones near its ends kept -- so one pixel
+    counted on the wrong side flips the min_num_pixels filter (target 200 passes, 199 fails)."""
+    grid = (np.log10(3600.0) + 1e-4 * np.arange(4607)).astype(np.float32)
+    near = [(np.float32(np.log10(e * (1 + z))).view(np.uint32) + np.arange(-81, 82, dtype=np.int64)).astype(np.uint32)
+            .view(np.float32) for e in ENDS]
+    ll = np.unique(np.concatenate([grid] + near))
+    f = np.arange(ll.size, dtype=np.float32) + 1
+    iv = np.ones(ll.size, np.float32)
+    am = np.zeros(ll.size, np.int32)
+    if nrange_target is not None:
+        w = O.derive(f, ll, iv, am)[0]
+        rest = w / np.float32(1 + z)
+        inside = np.flatnonzero((rest >= ENDS[2]) & (rest <= ENDS[3]))
+        edge = np.flatnonzero(np.isin(ll, np.concatenate(near)))
+        keep = np.concatenate([np.intersect1d(inside, edge), np.setdiff1d(inside, edge)])[:nrange_target]
+        iv[np.setdiff1d(inside, keep)] = 0
     return f, ll, iv, am
+
+
+def test_preload_range_ends_ulp_by_ulp():
+    """The kernels' fast range estimate hands every pixel near a range end to the correctly rounded
+    path: at 64 redshifts over [2, 6.5], every float32 loglam within 81 ulps (~4.5e-5 relative) of each
+    of the six ends lands where the oracle puts it -- window membership through the median, the model
+    range through the 200-pixel filter at its threshold, the loading range through the cells."""
+    zs = np.linspace(2.0, 6.5, 64)
+    z, cols = [], []
+    for zq in zs:
+        for t in (None, 200, 199):
+            z.append(zq)
+            cols.append(_boundary_spectrum(zq, t))
+    z = np.array(z)
+    flags = np.zeros(z.size, np.uint8)
+    got = I.preload_batch(z, flags, cols)
+    want = O.preload_from_columns(z, flags, cols)
+    ff = want["filter_flags"]
+    assert (ff[1::3] == 0).all() and (ff[2::3] == 8).all()      # the threshold cases sit on the threshold
+    _assert_equal_results(got, want)
+    assert np.array_equal(got["medians"], want["medians"], equal_nan=True)
 
 
 def test_preload_dr12q_count_batch():
@@ -122,7 +186,7 @@ def test_preload_dr12q_count_batch():
     Qt, npool = 162861, 4096
     rng = np.random.default_rng(31)
     zp = rng.uniform(2.15, 5.5, npool)
-    pool = [_boss_coadd(rng, z) for z in zp]
+    pool = [syn.make_boss_coadd_columns(rng, z) for z in zp]
     pre = (rng.uniform(size=npool) < 0.02).astype(np.uint8)
     want = O.preload_from_columns(zp, pre, [None if pre[i] else pool[i] for i in range(npool)])
     sel = np.arange(Qt) % npool
