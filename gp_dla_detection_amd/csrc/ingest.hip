@@ -15,8 +15,9 @@
 //                         spectrum (rest is monotone in loglam; see first_key_past), so only the cells'
 //                         wavelengths need the pow
 //   preload_qsos.m:29-33  nanmedian of the flux over unmasked pixels with rest in [1310, 1325]: the
-//                         window's values gathered in LDS, NaNs dropped, bitonic-sorted, MATLAB's
-//                         median (meanof(a, b) = a + (b - a) / 2 for finite same-sign a, b)
+//                         window's values gathered in LDS, NaNs dropped, bitonic-sorted (a radix
+//                         select over the spectrum when more than kWindowCap), MATLAB's median
+//                         (meanof(a, b) = a + (b - a) / 2 for finite same-sign a, b)
 //   preload_qsos.m:36-49  bit 3 (value 4) when that median is NaN; bit 4 (value 8) when fewer than
 //                         min_num_pixels unmasked pixels have rest in [911.75, 1215.75]
 //   preload_qsos.m:51-54  normaliser; flux / median, noise_variance / median^2 (single)
@@ -45,7 +46,7 @@ namespace gpdla {
 namespace {
 
 constexpr int kIngestThreads = 256;
-constexpr int kWindowCap = 4096;            // normalisation-window values per spectrum held in LDS
+constexpr int kWindowCap = 4096;            // median-set values per spectrum sorted in LDS (more: radix select)
 #ifndef GPDLA_INGEST_SCAN_UNROLL
 #define GPDLA_INGEST_SCAN_UNROLL 4
 #endif
@@ -70,7 +71,6 @@ struct IngestArgs {
   int64_t* count;                           // cell length (0 when skipped or filtered)
   int64_t* ends;                            // [Q][4]: first, last of the loading range, after, before (-1 = none)
   int32_t* keys;                            // [Q][6]: the three ranges as loglam order keys [lo, hi)
-  int32_t* status;                          // 1: a normalisation window over kWindowCap values
   // pass-2 outputs
   const int64_t* out_off;                   // [Q + 1]
   float* w_out;
@@ -175,6 +175,35 @@ __device__ inline T block_reduce(T v, T* red, Op op) {
   return op(op(red[0], red[1]), op(red[2], red[3]));
 }
 
+// A pixel of the median's set (preload_qsos.m:29-33): unmasked, in the normalisation window, flux
+// not NaN (nanmedian).
+__device__ inline bool in_window(const IngestArgs& a, int64_t i, const int32_t* kr) {
+  return !pixel_mask(a, i) && (range_bits(a.loglam[i], kr) & kNormWindow) && !isnan(a.flux[i]);
+}
+
+// The k-th smallest (0-based) flux of the median's set when the set overflows LDS (a finely sampled
+// spectrum): a radix select on the values' order keys, one bit per pass over the spectrum -- exact,
+// and no sort.
+__device__ float window_select(const IngestArgs& a, int64_t b, int64_t e, const int32_t* kr, int64_t k,
+                               int64_t* red) {
+  uint32_t prefix = 0, seen = 0;                  // the key bits decided so far, and which bits those are
+  for (int bit = 31; bit >= 0; --bit) {
+    int64_t zeros = 0;                            // set members matching the prefix with this bit clear
+    for (int64_t i = b + threadIdx.x; i < e; i += kIngestThreads) {
+      if (!in_window(a, i, kr)) continue;
+      const uint32_t u = (uint32_t)order_key(a.flux[i]) ^ 0x80000000u;
+      zeros += (u & seen) == prefix && !((u >> bit) & 1u);
+    }
+    zeros = block_reduce(zeros, red, [](int64_t x, int64_t y) { return x + y; });
+    if (k >= zeros) {
+      k -= zeros;
+      prefix |= 1u << bit;
+    }
+    seen |= 1u << bit;
+  }
+  return key_float((int32_t)(prefix ^ 0x80000000u));
+}
+
 __global__ __launch_bounds__(kIngestThreads) void preload_scan_kernel(IngestArgs a) {
   __shared__ float win[kWindowCap];
   __shared__ int nwin;
@@ -238,41 +267,40 @@ __global__ __launch_bounds__(kIngestThreads) void preload_scan_kernel(IngestArgs
   last = block_reduce(last, red64, [](int64_t x, int64_t y) { return x > y ? x : y; });
   __syncthreads();
   const int n = nwin;
+  float lo = NAN, hi = NAN;                       // the set's middle values (the same one for odd n)
   if (n > kWindowCap) {
-    if (threadIdx.x == 0) {
-      atomicOr(a.status, 1);
-      a.flags_out[q] = flags;
-      a.count[q] = 0;
-    }
-    return;
-  }
-  // bitonic sort of the window (padded with +inf to a power of two)
-  int np2 = 1;
-  while (np2 < n) np2 <<= 1;
-  for (int i = n + threadIdx.x; i < np2; i += kIngestThreads) win[i] = INFINITY;
-  __syncthreads();
-  for (int k = 2; k <= np2; k <<= 1) {
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int i = threadIdx.x; i < np2; i += kIngestThreads) {
-        const int l = i ^ j;
-        if (l > i) {
-          const float x = win[i], y = win[l];
-          const bool up = (i & k) == 0;
-          if ((x > y) == up) {
-            win[i] = y;
-            win[l] = x;
+    hi = window_select(a, b, e, kr, n / 2, red64);
+    lo = (n & 1) ? hi : window_select(a, b, e, kr, n / 2 - 1, red64);
+  } else if (n > 0) {
+    // bitonic sort of the window (padded with +inf to a power of two)
+    int np2 = 1;
+    while (np2 < n) np2 <<= 1;
+    for (int i = n + threadIdx.x; i < np2; i += kIngestThreads) win[i] = INFINITY;
+    __syncthreads();
+    for (int k = 2; k <= np2; k <<= 1) {
+      for (int j = k >> 1; j > 0; j >>= 1) {
+        for (int i = threadIdx.x; i < np2; i += kIngestThreads) {
+          const int l = i ^ j;
+          if (l > i) {
+            const float x = win[i], y = win[l];
+            const bool up = (i & k) == 0;
+            if ((x > y) == up) {
+              win[i] = y;
+              win[l] = x;
+            }
           }
         }
+        __syncthreads();
       }
-      __syncthreads();
     }
+    hi = win[n / 2];
+    lo = (n & 1) ? hi : win[n / 2 - 1];
   }
   float med = NAN;                                                                // median.m of an empty set
   if (n > 0) {
     if (n & 1) {
-      med = win[n / 2];
+      med = hi;
     } else {                                                                      // median.m's meanof(a, b)
-      const float lo = win[n / 2 - 1], hi = win[n / 2];
       const int slo = (lo > 0.0f) - (lo < 0.0f), shi = (hi > 0.0f) - (hi < 0.0f);   // MATLAB sign
       med = (slo == shi && isfinite(lo) && isfinite(hi)) ? lo + (hi - lo) / 2.0f : (lo + hi) / 2.0f;
     }
@@ -443,13 +471,12 @@ int gpdla_preload_qsos_f32(int32_t device, int64_t num_quasars, const int64_t* o
   out_offsets[0] = 0;
   if (Q == 0) return GPDLA_OK;
   HIP_TRY(hipSetDevice(device));
-  DevBuf d_off, d_pix, d_z, d_fl, d_res, d_status, d_ooff, d_out;
+  DevBuf d_off, d_pix, d_z, d_fl, d_res, d_ooff, d_out;
   HIP_TRY(hipMalloc(&d_off.p, (size_t)(Q + 1) * 8));
   HIP_TRY(hipMalloc(&d_pix.p, (size_t)N * 16 + 16));
   HIP_TRY(hipMalloc(&d_z.p, (size_t)Q * 8));
   HIP_TRY(hipMalloc(&d_fl.p, (size_t)Q * 2));
   HIP_TRY(hipMalloc(&d_res.p, (size_t)Q * 72));
-  HIP_TRY(hipMalloc(&d_status.p, 4));
   HIP_TRY(hipMalloc(&d_ooff.p, (size_t)(Q + 1) * 8));
   char* pix = (char*)d_pix.p;
   HIP_TRY(hipMemcpy(d_off.p, offsets, (size_t)(Q + 1) * 8, hipMemcpyHostToDevice));
@@ -461,7 +488,6 @@ int gpdla_preload_qsos_f32(int32_t device, int64_t num_quasars, const int64_t* o
   }
   HIP_TRY(hipMemcpy(d_z.p, z_qsos, (size_t)Q * 8, hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(d_fl.p, filter_flags, (size_t)Q, hipMemcpyHostToDevice));
-  HIP_TRY(hipMemset(d_status.p, 0, 4));
   char* res = (char*)d_res.p;
   IngestArgs a{};
   a.Q = Q;
@@ -478,18 +504,13 @@ int gpdla_preload_qsos_f32(int32_t device, int64_t num_quasars, const int64_t* o
   a.count = (int64_t*)(res + Q * 8);           // 8-byte aligned: Q * 4 rounded by the 2x below
   a.ends = (int64_t*)(res + Q * 16);
   a.keys = (int32_t*)(res + Q * 48);
-  a.status = (int32_t*)d_status.p;
   // (median at [0, 4Q), count at [8Q, 16Q), ends at [16Q, 48Q), keys at [48Q, 72Q))
   preload_keys_kernel<<<(unsigned)((Q + kKeySpectraPerBlock - 1) / kKeySpectraPerBlock), 64 * kKeySpectraPerBlock>>>(a);
   HIP_TRY(hipGetLastError());
   preload_scan_kernel<<<(unsigned)Q, kIngestThreads>>>(a);
   HIP_TRY(hipGetLastError());
   std::vector<int64_t> count(Q);
-  int32_t status = 0;
   HIP_TRY(hipMemcpy(count.data(), a.count, (size_t)Q * 8, hipMemcpyDeviceToHost));
-  HIP_TRY(hipMemcpy(&status, d_status.p, 4, hipMemcpyDeviceToHost));
-  if (status & 1)
-    return set_error(GPDLA_EUNSUPPORTED, "preload_qsos: a normalisation window holds more than %d pixels", kWindowCap);
   for (int64_t q = 0; q < Q; ++q) out_offsets[q + 1] = out_offsets[q] + count[q];
   const int64_t M = out_offsets[Q];
   HIP_TRY(hipMemcpy(d_ooff.p, out_offsets, (size_t)(Q + 1) * 8, hipMemcpyHostToDevice));

@@ -179,6 +179,46 @@ def test_preload_range_ends_ulp_by_ulp():
     assert np.array_equal(got["medians"], want["medians"], equal_nan=True)
 
 
+def _fine_spectra(rng, z, dex, ties=False):
+    """A finely sampled spectrum whose normalisation window holds more values than the scan sorts in LDS
+    (4,096): the median then comes from the radix select.  Returned twice: as drawn, and with one more
+    window pixel masked (odd and even set sizes), with the set sizes."""
+    ll = np.arange(np.log10(3400.0), np.log10(6000.0), dex).astype(np.float32)
+    f = rng.normal(1.0, 2.0, ll.size).astype(np.float32)
+    if ties:
+        f = np.round(f * 4) / 4                                   # many equal values, both signs
+    iv = rng.uniform(1, 50, ll.size).astype(np.float32)
+    iv[rng.uniform(size=ll.size) < 0.05] = 0
+    am = np.where(rng.uniform(size=ll.size) < 0.03, 1 << 23, 0).astype(np.int32)
+    f[rng.uniform(size=ll.size) < 0.02] = np.nan
+    f[rng.integers(0, ll.size, 3)] = np.inf
+    f[rng.integers(0, ll.size, 2)] = -np.inf
+    w = O.derive(f, ll, iv, am)[0]
+    rest = w / np.float32(1 + z)
+    win = np.flatnonzero((rest >= 1310) & (rest <= 1325) & (iv > 0) & (am == 0) & ~np.isnan(f))
+    iv2 = iv.copy()
+    iv2[win[win.size // 2]] = 0
+    return [(f, ll, iv, am), (f, ll, iv2, am)], [win.size, win.size - 1]
+
+
+def test_preload_median_of_a_window_beyond_lds():
+    rng = np.random.default_rng(12)
+    z, cols, sizes = [], [], []
+    for zq, dex, ties in ((2.5, 1e-6, False), (3.1, 7e-7, True), (2.5, 1e-4, False)):
+        c, n = _fine_spectra(rng, zq, dex, ties)
+        z += [zq, zq]
+        cols += c
+        sizes += n
+    assert min(sizes[:4]) > 4096 and max(sizes[4:]) < 4096
+    z = np.array(z)
+    flags = np.zeros(z.size, np.uint8)
+    got = I.preload_batch(z, flags, cols)
+    want = O.preload_from_columns(z, flags, cols)
+    assert (want["filter_flags"] == 0).all()
+    assert np.array_equal(got["medians"], want["medians"])
+    _assert_equal_results(got, want)
+
+
 def test_preload_dr12q_count_batch():
     """162,861 catalogue entries (DR12Q's count, README.md:115): a pool of 4,096 distinct full coadds at
     z in [2.15, 5.5] tiled to the count, 2% pre-filtered; the device result of every entry must equal the
