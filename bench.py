@@ -193,7 +193,7 @@ def host_cores() -> dict:
             "usable": usable}
 
 
-def cpu_baseline(model, samples, spectra, budget_s: float, k: int) -> dict:
+def cpu_baseline(model, samples, spectra, budget_s: float, k: int, widened: bool = False) -> dict:
     """The reference's CPU path, restated in C++ with OpenMP over the DLA samples like its parfor
     (oracle/cpu_ref.cpp: process_qsos.m:184-198, voigt.c:253-304 with an own Faddeeva function in
     place of libcerf, log_mvnpdf_low_rank.m:5-33 in MATLAB operation order), on every host core the
@@ -232,6 +232,7 @@ def cpu_baseline(model, samples, spectra, budget_s: float, k: int) -> dict:
     # secondary: the numpy restatement, one process, one BLAS thread, 3 s
     with mp.get_context("spawn").Pool(1) as pool:
         nd, nel = pool.map(_numpy_worker, [(model, spectra[0], off, nhi, 3.0)])[0]
+    wide = widened_cpu_baseline() if widened else None
     return {"value": done / el, "unit": "evals/s", "cores": threads, "kind": "port",
             "sample": f"{done} (spectrum, DLA-sample) evaluations = {nspec} whole spectra x {off.size} samples of the "
                       f"bench workload in {el:.1f} s; C++ OpenMP restatement of process_qsos.m:184-198 "
@@ -241,7 +242,30 @@ def cpu_baseline(model, samples, spectra, budget_s: float, k: int) -> dict:
             "host": hc,
             "configs0_null_eval_us": c1_us, "configs0_log_likelihood_no_dla": ll0,
             "numpy_1core": {"value": nd / nel, "unit": "evals/s", "cores": 1,
-                            "sample": f"{nd} evaluations of spectrum 0 in {nel:.1f} s (oracle/gpdla_oracle.py)"}}
+                            "sample": f"{nd} evaluations of spectrum 0 in {nel:.1f} s (oracle/gpdla_oracle.py)"},
+            "widened": wide}
+
+
+def widened_cpu_baseline() -> dict:
+    """The numpy restatements of the widened rows on one core, beside alternatives.dla_samples and
+    alternatives.ingest: generate_dla_samples at 10^5 samples (oracle/dla_samples_closed_form.py) and
+    preload_qsos over 1,024 of the ingest leg's BOSS coadds (oracle/ingest_oracle.py)."""
+    from oracle import dla_samples_closed_form as DC
+    from oracle import ingest_oracle as IO
+    ln = widened_catalogue()
+    t0 = time.perf_counter()
+    DC.generate_dla_samples(ln, WIDENED_SAMPLES)
+    el_s = time.perf_counter() - t0
+    zp, pool = boss_pool(1024)
+    t0 = time.perf_counter()
+    IO.preload_from_columns(zp, np.zeros(zp.size, np.uint8), pool)
+    el_p = time.perf_counter() - t0
+    npx = sum(c[0].size for c in pool)
+    return {"generate_dla_samples": {"value": WIDENED_SAMPLES / el_s, "unit": "samples/s", "cores": 1, "kind": "port",
+                                     "sample": f"{WIDENED_SAMPLES} samples in {el_s:.2f} s (numpy/scipy restatement)"},
+            "preload_qsos": {"value": npx / el_p, "unit": "pixels/s", "cores": 1, "kind": "port",
+                             "sample": f"1,024 synthetic BOSS coadds ({npx:,} pixels) in {el_p:.2f} s "
+                                       "(numpy restatement, columns already in memory)"}}
 
 
 # BASELINE.json configs (SURVEY.md 8d).  c2 is the bench line the driver records.
@@ -618,6 +642,114 @@ def plan_only(wl: dict, world: int, rank: int, local_rank: int, dist, ndev: int 
         print(json.dumps(out), flush=True)
 
 
+# SURVEY 8f-2 / 8f-4 (the widened rows) beside the headline: synthetic inputs of the reference's shape
+WIDENED_SAMPLES = 100_000                   # generate_dla_samples at configs[4]'s sample count
+DR12Q_COUNT, BOSS_POOL, INGEST_BATCH = 162_861, 4_096, 16_384
+INGEST_PROFILE = ROOT / "profiles" / "round6" / "r12p_ingest.json"
+
+
+def widened_catalogue() -> np.ndarray:
+    """A DLA catalogue's log N_HI column (generate_dla_samples.m:25-30's input): 1,000 values."""
+    rng = np.random.default_rng(5)
+    return np.r_[rng.normal(20.55, 0.3, 800), rng.uniform(20.3, 21.8, 200)]
+
+
+def boss_pool(npool: int, seed: int = 31):
+    """fitsread columns of npool synthetic full BOSS coadds (3600-10400 A) at z in [2.15, 5.5]."""
+    from gp_dla_detection_amd import synthetic as syn
+    rng = np.random.default_rng(seed)
+    zp = rng.uniform(2.15, 5.5, npool)
+    return zp, [syn.make_boss_coadd_columns(rng, z) for z in zp]
+
+
+def dla_samples_alternative(dev: int, reps: int = 5) -> dict:
+    """generate_dla_samples.m:8-57 on the device at 10^5 samples (RR2 Halton, the KDE on
+    the fit grid, the per-sample inverse CDF; gpdla_generate_dla_samples_f64, host buffers in and
+    out).  One warm-up call, then ``reps`` timed calls; kernel times from HIP events in the library."""
+    from gp_dla_detection_amd import _lib as L
+    from gp_dla_detection_amd import dla_samples as DS
+    ln = widened_catalogue()
+    DS.generate_dla_samples(ln, WIDENED_SAMPLES, device=dev)
+    kms = np.zeros(3)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        out = DS.generate_dla_samples(ln, WIDENED_SAMPLES, device=dev)
+        kms += np.array(L.last_call_kernel_ms()[:3])
+    el = (time.perf_counter() - t0) / reps
+    kms /= reps
+    off, lnhi, nhi = out["offset_samples"], out["log_nhi_samples"], out["nhi_samples"]
+    ok = bool(np.all((off >= 0) & (off <= 1)) and np.all((lnhi >= 20) & (lnhi <= 23))
+              and np.all(np.isfinite(nhi)) and np.allclose(nhi, 10.0 ** lnhi, rtol=1e-15, atol=0))
+    return {"value": WIDENED_SAMPLES / el, "unit": "samples/s", "ms_per_step": el * 1e3, "steps": reps,
+            "config": {"workload": "generate_dla_samples.m at 10^5 samples over a 1,000-value synthetic log N_HI "
+                                   "catalogue (SURVEY 8f-2); host buffers in and out"},
+            "kernel_ms": {"kde": kms[0], "halton_rr2": kms[1], "inverse_cdf": kms[2]},
+            "note": "the call is launch- and copy-bound (three small kernels); the inverse CDF is one "
+                    "bracketed-Newton solve per sample in fp64",
+            "checks_ok": ok}
+
+
+def ingest_alternative(dev: int) -> dict:
+    """preload_qsos.m:18-67 (with read_spec.m:27-38) on the device over the DR12Q count --
+    162,861 catalogue entries, full BOSS coadds (a pool of 4,096 distinct synthetic ones, tiled) -- in
+    16,384-spectrum batches through gpdla_preload_qsos_f32.  The boundary takes host buffers (FITS is
+    parsed on the host), so ``value`` (input pixels/s) includes the CSR packing, PCIe copies and the
+    splitting into cells; ``roofline`` is the scan and write kernels' algorithmic bytes (12 B per
+    input pixel, 29 B per selected one) over their HIP-event times."""
+    from gp_dla_detection_amd import _lib as L
+    from gp_dla_detection_amd import ingest as I
+    t0 = time.perf_counter()
+    zp, pool = boss_pool(BOSS_POOL)
+    setup_s = time.perf_counter() - t0
+    sel = np.arange(DR12Q_COUNT) % BOSS_POOL
+    flags = np.zeros(DR12Q_COUNT, np.uint8)
+    I.preload_batch(zp[:256], flags[:256], [pool[i] for i in range(256)], device=dev)   # warm-up
+    kms = np.zeros(3)
+    npx = nsel = 0
+    ff = []
+    ok = True
+    t0 = time.perf_counter()
+    for b0 in range(0, DR12Q_COUNT, INGEST_BATCH):
+        idx = sel[b0:b0 + INGEST_BATCH]
+        cols = [pool[i] for i in idx]
+        r = I.preload_batch(zp[idx], flags[b0:b0 + INGEST_BATCH], cols, device=dev)
+        kms += np.array(L.last_call_kernel_ms()[:3])
+        npx += sum(c[0].size for c in cols)
+        nsel += sum(c.size for c in r["all_wavelengths"])
+        ff.append(r["filter_flags"])
+        good = r["filter_flags"] == 0
+        ok = ok and bool(np.all(np.isfinite(r["all_normalizers"][good])))
+    el = time.perf_counter() - t0
+    ff = np.concatenate(ff)
+    alg = {"scan": 12.0 * npx, "write": 29.0 * nsel}
+    per = {k: {"ms": kms[i], "algorithmic_bytes": alg[k], "gbs": alg[k] / (kms[i] * 1e-3) / 1e9,
+               "frac": alg[k] / (kms[i] * 1e-3) / 1e9 / HBM_PEAK_GBS} for i, k in ((1, "scan"), (2, "write"))}
+    both = (alg["scan"] + alg["write"]) / ((kms[1] + kms[2]) * 1e-3) / 1e9
+    traffic = None
+    if INGEST_PROFILE.exists():   # PMC bytes of the same workload (tools/profile_ingest.sh)
+        kp = json.loads(INGEST_PROFILE.read_text())["kernels"]
+        traffic = sum(kp[k]["pmc_bytes"] for k in ("preload_scan_kernel", "preload_write_kernel"))
+    return {"value": npx / el, "unit": "pixels/s", "wall_s": el, "ms_per_step": el * 1e3, "steps": 1,
+            "warmup": "one call on 256 spectra",
+            "config": {"workload": "preload_qsos.m's numeric stage over the DR12Q count (162,861 entries, full "
+                                   "3600-10400 A BOSS coadds: a pool of 4,096 distinct synthetic ones tiled), "
+                                   "16,384 spectra per call (SURVEY 8f-4)",
+                       "spectra": DR12Q_COUNT, "pixels_in": int(npx), "pixels_selected": int(nsel)},
+            "kernel_ms": {"keys_total": kms[0], "scan_total": kms[1], "write_total": kms[2]},
+            "roofline": {"bound": "hbm", "unit": "GB/s", "peak": HBM_PEAK_GBS, "achieved": both,
+                         "frac": both / HBM_PEAK_GBS, "traffic": traffic,
+                         "traffic_source": f"{INGEST_PROFILE.relative_to(ROOT)}: FETCH_SIZE x2 + WRITE_SIZE of both "
+                                           "kernels over the same workload (incl. one 256-spectrum warm-up launch), "
+                                           f"against {alg['scan'] + alg['write']:.3e} algorithmic bytes"
+                                           if traffic else None,
+                         "kernel": "preload_scan_kernel + preload_write_kernel (all launches)", "per_kernel": per,
+                         "note": "algorithmic bytes: 12 B per input pixel (scan: loglam, ivar, and_mask), 29 B per "
+                                 "selected pixel (write: 16 B in, 13 B out)"},
+            "value_note": "host buffers in and out: CSR packing, PCIe copies and cell splitting included",
+            "filter_flags": {str(int(v)): int(c) for v, c in zip(*np.unique(ff, return_counts=True))},
+            "setup_untimed_s": setup_s, "checks_ok": ok}
+
+
 def configs4_alternative(dev: int, steps: int) -> dict:
     """BASELINE configs[4] beside the headline: 128 spectra x 10^5 DLA samples, k = 50, on the
     panel_gemm_i8_24 path, ``steps`` timed steps on resident inputs after one warm-up step; its GEMM
@@ -905,6 +1037,8 @@ def main():
                     help="skip alternatives.configs2 (full DR12Q count on this GPU) in the default line")
     ap.add_argument("--no-e2e", action="store_true",
                     help="skip alternatives.e2e (configs[2] end to end on files) in the default line")
+    ap.add_argument("--no-widened", action="store_true",
+                    help="skip alternatives.dla_samples / .ingest (SURVEY 8f-2, 8f-4) in the default line")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and (args.gpus or 1) > 1:
@@ -967,7 +1101,8 @@ def main():
     # CPU baseline first, while no process has touched the GPU (its workers are spawned)
     cpu = None
     if rank == 0 and world == 1 and args.cpu_budget > 0:
-        cpu = cpu_baseline(model, samples, spectra, args.cpu_budget, args.k)
+        cpu = cpu_baseline(model, samples, spectra, args.cpu_budget, args.k,
+                           widened=not args.no_alt and not args.no_widened and not wl["dr12q"] and args.k == 20)
     # one GPU per local rank; fewer devices than ranks is refused unless --rehearsal (ranks share devices)
     dev, err = assign_device(world, local_rank, L.load().gpdla_device_count(), args.rehearsal)
     if err:
@@ -1075,6 +1210,9 @@ def main():
             a.free()
         # BASELINE configs[4] (k = 50, 10^5 samples) on the int8 panel-GEMM path, driver-timed
         alt["configs4"] = configs4_alternative(dev, args.steps)
+        if not args.no_widened:  # SURVEY 8f-2 and 8f-4 on the device, CPU restatements in cpu_baseline
+            alt["dla_samples"] = dla_samples_alternative(dev)
+            alt["ingest"] = ingest_alternative(dev)
 
     # sanity: finite outputs and the calc_cddf.py:246 normalisation invariant on every spectrum
     inv = invariant_all_rows(o_s, o_dla, S)

@@ -123,12 +123,13 @@ SIGNATURES = {
     "gpdla_memcpy_dtoh": (C.c_int, [C.c_int32, C.c_void_p, C.c_void_p, C.c_int64]),
     "gpdla_last_error": (C.c_char_p, []),
     "gpdla_version": (C.c_int32, []),
+    "gpdla_last_call_kernel_ms": (C.c_int, [C.POINTER(C.c_double), C.c_int32, C.POINTER(C.c_int32)]),
     "gpdla_device_count": (C.c_int32, []),
     "gpdla_device_pci_bus_id": (C.c_int, [C.c_int32, C.c_char_p, C.c_int32]),
 }
 
 # GPDLA_ABI_VERSION of include/gpdla.h this binding is written against
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 _lib = None
 
@@ -172,6 +173,14 @@ def pci_bus_id(device: int) -> str:
     buf = C.create_string_buffer(64)
     check(load().gpdla_device_pci_bus_id(device, buf, len(buf)))
     return buf.value.decode()
+
+
+def last_call_kernel_ms() -> list[float]:
+    """Per-launch kernel times (ms) of this thread's last ingest / sampler call (gpdla_last_call_kernel_ms)."""
+    buf = (C.c_double * 8)()
+    n = C.c_int32(0)
+    check(load().gpdla_last_call_kernel_ms(buf, 8, C.byref(n)))
+    return [buf[i] for i in range(min(n.value, 8))]
 
 
 def check(rc: int) -> int:

@@ -262,6 +262,7 @@ int gpdla_halton_rr2_f64(int32_t device, int64_t start, int64_t stride, int64_t 
     if (bases[d] < 2 || bases[d] > kMaxHaltonBase)
       return set_error(GPDLA_EINVAL, "halton: base %d outside 2..%d", (int)bases[d], kMaxHaltonBase);
   if (int rc = check_device(device)) return rc;
+  launch_times().reset();
   if (num == 0) return GPDLA_OK;
   HIP_TRY(hipSetDevice(device));
   HaltonArgs a{};
@@ -281,9 +282,12 @@ int gpdla_halton_rr2_f64(int32_t device, int64_t start, int64_t stride, int64_t 
   HIP_TRY(hipMemcpy(dperm.p, perms.data(), perms.size() * 4, hipMemcpyHostToDevice));
   a.perms = (const int32_t*)dperm.p;
   a.out = (double*)dout.p;
+  launch_times().before();
   halton_rr2_kernel<<<(unsigned)((num + 255) / 256), 256>>>(a);
+  launch_times().after();
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipMemcpy(out, dout.p, (size_t)num * dims * 8, hipMemcpyDeviceToHost));
+  launch_times().finish();
   return GPDLA_OK;
 }
 
@@ -299,6 +303,7 @@ int gpdla_generate_dla_samples_f64(int32_t device, const double* log_nhis, int64
   for (int64_t i = 0; i < n_data; ++i)
     if (!std::isfinite(log_nhis[i])) return set_error(GPDLA_EINVAL, "generate_dla_samples: non-finite log_nhis[%lld]", (long long)i);
   if (int rc = check_device(device)) return rc;
+  launch_times().reset();
   HIP_TRY(hipSetDevice(device));
   // ksdensity's default bandwidth (host: two O(n) selections)
   std::vector<double> data(log_nhis, log_nhis + n_data);
@@ -314,7 +319,9 @@ int gpdla_generate_dla_samples_f64(int32_t device, const double* log_nhis, int64
   HIP_TRY(hipMalloc(&ddata.p, (size_t)n_data * 8));
   HIP_TRY(hipMalloc(&dkde.p, kFitPoints * 8));
   HIP_TRY(hipMemcpy(ddata.p, data.data(), (size_t)n_data * 8, hipMemcpyHostToDevice));
+  launch_times().before();
   kde_kernel<<<kFitPoints, kKdeThreads>>>((const double*)ddata.p, n_data, x0, step, x1, kFitPoints, h, (double*)dkde.p);
+  launch_times().after();
   HIP_TRY(hipGetLastError());
   std::vector<double> kde(kFitPoints), xs(kFitPoints), ly(kFitPoints);
   HIP_TRY(hipMemcpy(kde.data(), dkde.p, kFitPoints * 8, hipMemcpyDeviceToHost));
@@ -367,16 +374,21 @@ int gpdla_generate_dla_samples_f64(int32_t device, const double* log_nhis, int64
   a.perms = (const int32_t*)dperm.p;
   a.out = (double*)dhal.p;
   const unsigned grid = (unsigned)((num_samples + 255) / 256);
+  launch_times().before();
   halton_rr2_kernel<<<grid, 256>>>(a);                                       // :8-9
+  launch_times().after();
   HIP_TRY(hipGetLastError());
+  launch_times().before();
   inverse_cdf_kernel<<<grid, 256>>>(p, (const double*)dhal.p, 2, 1, num_samples, (double*)dlog.p,
                                     (double*)dnhi.p);                        // :51-57
+  launch_times().after();
   HIP_TRY(hipGetLastError());
   std::vector<double> hal((size_t)num_samples * 2);
   HIP_TRY(hipMemcpy(hal.data(), dhal.p, hal.size() * 8, hipMemcpyDeviceToHost));
   HIP_TRY(hipMemcpy(log_nhi_samples, dlog.p, (size_t)num_samples * 8, hipMemcpyDeviceToHost));
   HIP_TRY(hipMemcpy(nhi_samples, dnhi.p, (size_t)num_samples * 8, hipMemcpyDeviceToHost));
   for (int64_t j = 0; j < num_samples; ++j) offset_samples[j] = hal[(size_t)j * 2];   // :13
+  launch_times().finish();
   return GPDLA_OK;
 }
 

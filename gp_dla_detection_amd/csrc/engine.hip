@@ -18,6 +18,7 @@ using namespace gpdla;
 
 namespace {
 thread_local std::string g_last_error;
+thread_local LaunchTimes g_launch_times;
 }  // namespace
 
 namespace gpdla {
@@ -31,6 +32,8 @@ int set_error(int code, const char* fmt, ...) {
   g_last_error = buf;
   return code;
 }
+
+LaunchTimes& launch_times() { return g_launch_times; }
 
 int check_device(int32_t device) {
   int count = 0;
@@ -238,6 +241,15 @@ int upload(void* dst, const void* src, size_t bytes, hipStream_t s) {
 extern "C" {
 
 int32_t gpdla_version(void) { return GPDLA_ABI_VERSION; }
+
+int gpdla_last_call_kernel_ms(double* ms, int32_t capacity, int32_t* count) {
+  if (!count || capacity < 0 || (capacity > 0 && !ms))
+    return set_error(GPDLA_EINVAL, "last_call_kernel_ms: null argument or negative capacity");
+  const LaunchTimes& t = launch_times();
+  *count = t.done;
+  for (int i = 0; i < t.done && i < capacity; ++i) ms[i] = t.ms[i];
+  return GPDLA_OK;
+}
 
 int32_t gpdla_device_count(void) {
   int c = 0;

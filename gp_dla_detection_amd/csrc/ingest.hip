@@ -430,6 +430,7 @@ int gpdla_read_spec_f32(int32_t device, int64_t n, const float* loglam, const fl
   if (n < 0 || (n > 0 && (!loglam || !ivar || !and_mask || !wavelengths || !noise_variance || !pixel_mask)))
     return set_error(GPDLA_EINVAL, "read_spec: null argument or negative length");
   if (int rc = check_device(device)) return rc;
+  launch_times().reset();
   if (n == 0) return GPDLA_OK;
   HIP_TRY(hipSetDevice(device));
   DevBuf d_in, d_out;
@@ -440,13 +441,16 @@ int gpdla_read_spec_f32(int32_t device, int64_t n, const float* loglam, const fl
   HIP_TRY(hipMemcpy(in, loglam, (size_t)n * 4, hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(in + n * 4, ivar, (size_t)n * 4, hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(in + n * 8, and_mask, (size_t)n * 4, hipMemcpyHostToDevice));
+  launch_times().before();
   read_spec_kernel<<<(unsigned)((n + 255) / 256), 256>>>(n, (const float*)in, (const float*)(in + n * 4),
                                                          (const int32_t*)(in + n * 8), 24, (float*)out,
                                                          (float*)(out + n * 4), (uint8_t*)(out + n * 8));
+  launch_times().after();
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipMemcpy(wavelengths, out, (size_t)n * 4, hipMemcpyDeviceToHost));
   HIP_TRY(hipMemcpy(noise_variance, out + n * 4, (size_t)n * 4, hipMemcpyDeviceToHost));
   HIP_TRY(hipMemcpy(pixel_mask, out + n * 8, (size_t)n, hipMemcpyDeviceToHost));
+  launch_times().finish();
   return GPDLA_OK;
 }
 
@@ -468,6 +472,7 @@ int gpdla_preload_qsos_f32(int32_t device, int64_t num_quasars, const int64_t* o
   if (params->brightsky_bit < 1 || params->brightsky_bit > 32)
     return set_error(GPDLA_EINVAL, "preload_qsos: brightsky_bit %d outside 1..32", (int)params->brightsky_bit);
   if (int rc = check_device(device)) return rc;
+  launch_times().reset();
   out_offsets[0] = 0;
   if (Q == 0) return GPDLA_OK;
   HIP_TRY(hipSetDevice(device));
@@ -505,9 +510,13 @@ int gpdla_preload_qsos_f32(int32_t device, int64_t num_quasars, const int64_t* o
   a.ends = (int64_t*)(res + Q * 16);
   a.keys = (int32_t*)(res + Q * 48);
   // (median at [0, 4Q), count at [8Q, 16Q), ends at [16Q, 48Q), keys at [48Q, 72Q))
+  launch_times().before();
   preload_keys_kernel<<<(unsigned)((Q + kKeySpectraPerBlock - 1) / kKeySpectraPerBlock), 64 * kKeySpectraPerBlock>>>(a);
+  launch_times().after();
   HIP_TRY(hipGetLastError());
+  launch_times().before();
   preload_scan_kernel<<<(unsigned)Q, kIngestThreads>>>(a);
+  launch_times().after();
   HIP_TRY(hipGetLastError());
   std::vector<int64_t> count(Q);
   HIP_TRY(hipMemcpy(count.data(), a.count, (size_t)Q * 8, hipMemcpyDeviceToHost));
@@ -523,7 +532,9 @@ int gpdla_preload_qsos_f32(int32_t device, int64_t num_quasars, const int64_t* o
   a.normalizers = (double*)(out + M * 12 + ((8 - (M * 12) % 8) % 8));
   a.m_out = (uint8_t*)a.normalizers + Q * 8;
   HIP_TRY(hipMemset(a.normalizers, 0, (size_t)Q * 8));                           // zeros(num_quasars, 1)
+  launch_times().before();
   preload_write_kernel<<<(unsigned)Q, kIngestThreads>>>(a);
+  launch_times().after();
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipMemcpy(filter_flags, a.flags_out, (size_t)Q, hipMemcpyDeviceToHost));
   HIP_TRY(hipMemcpy(normalizers, a.normalizers, (size_t)Q * 8, hipMemcpyDeviceToHost));
@@ -534,6 +545,7 @@ int gpdla_preload_qsos_f32(int32_t device, int64_t num_quasars, const int64_t* o
     HIP_TRY(hipMemcpy(out_noise_variance, a.nv_out, (size_t)M * 4, hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(out_pixel_mask, a.m_out, (size_t)M, hipMemcpyDeviceToHost));
   }
+  launch_times().finish();
   return GPDLA_OK;
 }
 

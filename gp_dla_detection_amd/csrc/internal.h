@@ -25,6 +25,36 @@ int set_error(int code, const char* fmt, ...);
 // GPDLA_OK if `device` is a usable HIP device, else GPDLA_EDEVICE / GPDLA_EINVAL (no CPU fallback)
 int check_device(int32_t device);
 
+// Launch times of the calling thread's last one-shot call (ingest, sampler): HIP events around each
+// kernel on the null stream, read back by gpdla_last_call_kernel_ms (engine.hip).  Usage: reset()
+// at the call's start, before() / after() around each launch, then finish() once the call's last
+// synchronous copy has returned.
+struct LaunchTimes {
+  static constexpr int kMax = 8;
+  hipEvent_t ev[2 * kMax] = {};
+  double ms[kMax] = {};
+  int n = 0, done = 0;
+  void reset() { n = done = 0; }
+  void before() {
+    if (n < kMax && (ev[2 * n] || hipEventCreate(&ev[2 * n]) == hipSuccess)) (void)hipEventRecord(ev[2 * n], 0);
+  }
+  void after() {
+    if (n < kMax && (ev[2 * n + 1] || hipEventCreate(&ev[2 * n + 1]) == hipSuccess)) {
+      (void)hipEventRecord(ev[2 * n + 1], 0);
+      ++n;
+    }
+  }
+  void finish() {
+    for (int i = 0; i < n; ++i) {
+      float t = 0.0f;
+      ms[i] = hipEventSynchronize(ev[2 * i + 1]) == hipSuccess && hipEventElapsedTime(&t, ev[2 * i], ev[2 * i + 1]) ==
+                  hipSuccess ? (double)t : -1.0;
+    }
+    done = n;
+  }
+};
+LaunchTimes& launch_times();
+
 // ---------------------------------------------------------------------------------------------
 // Device data layout (HBM)
 //

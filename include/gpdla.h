@@ -48,8 +48,9 @@ extern "C" {
 /* ABI version (gpdla_version()).  2: gpdla_stats gained contraction_ms / contraction_launches
  * (its size changed: a caller compiled against a version-1 header must use gpdla_engine_get_stats_n
  * with its own sizeof(gpdla_stats), or be rebuilt).  3: gpdla_device_pci_bus_id.  4: the DLA-sample
- * generator (gpdla_halton_rr2_f64, gpdla_generate_dla_samples_f64) and the ingest kernels. */
-#define GPDLA_ABI_VERSION 4
+ * generator (gpdla_halton_rr2_f64, gpdla_generate_dla_samples_f64) and the ingest kernels.
+ * 5: gpdla_last_call_kernel_ms. */
+#define GPDLA_ABI_VERSION 5
 
 #define GPDLA_MEM_HOST 0
 #define GPDLA_MEM_DEVICE 1
@@ -291,6 +292,11 @@ int32_t gpdla_device_count(void);
 /* PCI bus id ("dddd:bb:dd.f") of a device, into buf (len >= 13): which physical GPU a rank drives
  * (the multi-GPU bench reports it per rank; process_qsos.m:88's spectra loop split over devices). */
 int gpdla_device_pci_bus_id(int32_t device, char* buf, int32_t len);
+/* Kernel times (ms, HIP events) of the calling thread's last call of gpdla_read_spec_f32,
+ * gpdla_preload_qsos_f32, gpdla_halton_rr2_f64 or gpdla_generate_dla_samples_f64, one per launch in
+ * launch order: read_spec 1; preload_qsos 3 (range keys, scan, write); halton 1; generate 3 (KDE,
+ * Halton, inverse CDF).  *count = launches recorded (0 for an empty call); at most capacity copied. */
+int gpdla_last_call_kernel_ms(double* ms, int32_t capacity, int32_t* count);
 
 #ifdef __cplusplus
 }

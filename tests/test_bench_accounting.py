@@ -93,3 +93,20 @@ def test_profiled_traffic_lookup(bench):
     # other workloads / paths: no profiled number is claimed
     assert bench.profiled_traffic(128, 100000, 50, "fused") == (None, None)
     assert bench.profiled_traffic(64, 10000, 20, "fused") == (None, None)
+
+def test_widened_cpu_baseline(bench):
+    """The widened rows' CPU restatements (beside alternatives.dla_samples / .ingest) run on the host
+    and report positive one-core rates with their samples named."""
+    w = bench.widened_cpu_baseline()
+    for key, unit in (("generate_dla_samples", "samples/s"), ("preload_qsos", "pixels/s")):
+        assert w[key]["value"] > 0 and w[key]["unit"] == unit and w[key]["cores"] == 1 and w[key]["kind"] == "port"
+        assert w[key]["sample"]
+
+
+def test_ingest_profile_summary(bench):
+    """alternatives.ingest's roofline traffic comes from the committed PMC summary of the same workload;
+    the PMC bytes of each kernel sit within 10% of its algorithmic bytes (no wasted re-reads)."""
+    kp = json.loads(bench.INGEST_PROFILE.read_text())["kernels"]
+    for k in ("preload_scan_kernel", "preload_write_kernel"):
+        assert kp[k]["launches"] == 11 and kp[k]["total_ms"] > 0
+        assert abs(kp[k]["pmc_bytes"] / kp[k]["algorithmic_bytes"] - 1) < 0.10

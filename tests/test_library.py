@@ -26,7 +26,7 @@ def test_library_exports_every_declared_symbol():
     for name in names:
         assert hasattr(lib, name), name
         assert name in L.SIGNATURES, f"{name} missing from the ctypes binding"
-    assert lib.gpdla_version() == L.ABI_VERSION == 4   # 2: gpdla_stats grew; 3: pci bus id; 4: samples + ingest
+    assert lib.gpdla_version() == L.ABI_VERSION == 5   # 2: gpdla_stats grew; 3: pci bus id; 4: samples + ingest; 5: kernel times
 
 
 def test_faddeeva_host_matches_scipy():

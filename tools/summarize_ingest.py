@@ -2,7 +2,9 @@
 """Summarise a tools/profile_ingest.sh run: per ingest kernel, launches, time, algorithmic bytes
 (tools/bench_ingest.py's accounting) over kernel time against the 8 TB/s HBM peak, and the PMC bytes
 per launch (FETCH_SIZE doubled for gfx950's wide streaming reads, WRITE_SIZE as is; both KiB;
-MI355X_MICROARCH.md's HBM section; they include Infinity-Cache hits)."""
+MI355X_MICROARCH.md's HBM section; they include Infinity-Cache hits).
+
+    python3 tools/summarize_ingest.py <profile_ingest.sh dir> [summary.json] > summary.md"""
 import collections
 import csv
 import json
@@ -20,8 +22,9 @@ def counters(path, name):
     return agg
 
 
-def main(src):
+def main(src, json_out=None):
     src = Path(src)
+    rec = {"source": str(src), "kernels": {}}
     bench = json.loads((src / "bench_trace.json").read_text())
     pq = bench["preload_qsos_dr12q"]
     warm = pq["warmup"]
@@ -49,6 +52,8 @@ def main(src):
         gbs = alg[short] / (ms * 1e-3) / 1e9
         tot_ms += ms
         tot_alg += alg[short]
+        rec["kernels"][short] = {"launches": int(row["Calls"]), "total_ms": ms, "algorithmic_bytes": alg[short],
+                                 "pmc_fetch_bytes_x2": fb, "pmc_write_bytes": wb, "pmc_bytes": fb + wb}
         print(f"| {short} | {row['Calls']} | {ms:.3f} | {float(row['AverageNs']) / 1e3:.1f} | {alg[short] / 1e9:.2f} | "
               f"{gbs:.0f} | {gbs / HBM_PEAK_GBS:.3f} | {(fb + wb) / 1e9:.2f} |")
     keys = next((r for r in other if "preload_keys_kernel" in r["Name"]), None)
@@ -69,7 +74,9 @@ def main(src):
               f"{float(r['AverageNs']) / 1e3:.1f} | {float(r['MaxNs']) / 1e3:.1f} |")
     for k in ("dla_samples_S10000", "dla_samples_S100000"):
         print(f"\n{k}: {bench[k]['wall_ms']:.3f} ms wall per call ({bench[k]['note']})")
+    if json_out:
+        Path(json_out).write_text(json.dumps(rec, indent=1))
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else None)
