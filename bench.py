@@ -645,7 +645,7 @@ def plan_only(wl: dict, world: int, rank: int, local_rank: int, dist, ndev: int 
 # SURVEY 8f-2 / 8f-4 (the widened rows) beside the headline: synthetic inputs of the reference's shape
 WIDENED_SAMPLES = 100_000                   # generate_dla_samples at configs[4]'s sample count
 DR12Q_COUNT, BOSS_POOL, INGEST_BATCH = 162_861, 4_096, 16_384
-INGEST_PROFILE = ROOT / "profiles" / "round6" / "r12p_ingest.json"
+INGEST_PROFILE = ROOT / "profiles" / "round6" / "r12w_ingest.json"
 
 
 def widened_catalogue() -> np.ndarray:

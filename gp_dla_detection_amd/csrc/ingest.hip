@@ -209,6 +209,7 @@ __global__ __launch_bounds__(kIngestThreads) void preload_scan_kernel(IngestArgs
   __shared__ int nwin;
   __shared__ int64_t red64[4];
   __shared__ int32_t red32[4];
+  __shared__ int64_t red4[3][4];
   const int64_t q = blockIdx.x;
   const int64_t b = a.off[q], e = a.off[q + 1];
   int64_t* ends = a.ends + q * 4;
@@ -261,16 +262,50 @@ __global__ __launch_bounds__(kIngestThreads) void preload_scan_kernel(IngestArgs
       }
     }
   }
-  nrange = block_reduce(nrange, red32, [](int32_t x, int32_t y) { return x + y; });
-  nload = block_reduce(nload, red64, [](int64_t x, int64_t y) { return x + y; });
-  first = block_reduce(first, red64, [](int64_t x, int64_t y) { return x < y ? x : y; });
-  last = block_reduce(last, red64, [](int64_t x, int64_t y) { return x > y ? x : y; });
+  // the four counts in one barrier (which also completes the window gather)
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    nrange += __shfl_xor(nrange, o);
+    nload += __shfl_xor(nload, o);
+    first = min(first, (int64_t)__shfl_xor(first, o));
+    last = max(last, (int64_t)__shfl_xor(last, o));
+  }
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (lane == 0) {
+    red32[wave] = nrange;
+    red4[0][wave] = nload;
+    red4[1][wave] = first;
+    red4[2][wave] = last;
+  }
   __syncthreads();
+  nrange = red32[0] + red32[1] + red32[2] + red32[3];
+  nload = red4[0][0] + red4[0][1] + red4[0][2] + red4[0][3];
+  first = min(min(red4[1][0], red4[1][1]), min(red4[1][2], red4[1][3]));
+  last = max(max(red4[2][0], red4[2][1]), max(red4[2][2], red4[2][3]));
   const int n = nwin;
   float lo = NAN, hi = NAN;                       // the set's middle values (the same one for odd n)
   if (n > kWindowCap) {
     hi = window_select(a, b, e, kr, n / 2, red64);
     lo = (n & 1) ? hi : window_select(a, b, e, kr, n / 2 - 1, red64);
+  } else if (n <= 64) {
+    // the usual case (~50 values at SDSS sampling): wave 0 sorts in registers, the same compare-exchange
+    // network as the LDS sort below (pairs (i, i ^ j) of np2 values, swap when (x_i > x_l) == up), so
+    // the two give the same order, signed zeros included; no barrier
+    if (wave == 0 && n > 0) {
+      int np2 = 1;
+      while (np2 < n) np2 <<= 1;
+      float v = lane < n ? win[lane] : INFINITY;
+      for (int k = 2; k <= np2; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+          const float o = __shfl_xor(v, j);
+          const bool lower = (lane & j) == 0;
+          const float xi = lower ? v : o, xl = lower ? o : v;
+          if ((xi > xl) == ((lane & k) == 0)) v = o;
+        }
+      }
+      hi = __shfl(v, n / 2);
+      lo = __shfl(v, (n & 1) ? n / 2 : n / 2 - 1);
+    }
   } else if (n > 0) {
     // bitonic sort of the window (padded with +inf to a power of two)
     int np2 = 1;
@@ -309,19 +344,26 @@ __global__ __launch_bounds__(kIngestThreads) void preload_scan_kernel(IngestArgs
   // range (they are its extreme indices), so the neighbours are the nearest unmasked pixels on either
   // side: found 256 at a time outward from the range, stopping at the first chunk that holds one.
   int64_t after = LLONG_MAX, before = -1;
-  if (last >= 0) {
-    for (int64_t c = b + last + 1; c < e; c += kIngestThreads) {
-      const int64_t i = c + threadIdx.x;
-      if (i < e && !pixel_mask(a, i)) after = min(after, i - b);
-      after = block_reduce(after, red64, [](int64_t x, int64_t y) { return x < y ? x : y; });
-      if (after != LLONG_MAX) break;
+  // both sides in one reduction per round (2 barriers; one round unless 256 pixels in a row are masked)
+  for (int64_t r = 0; last >= 0; r += kIngestThreads) {
+    const int64_t ia = b + last + 1 + r + threadIdx.x, ib = b + first - 1 - r - threadIdx.x;
+    const bool need_a = after == LLONG_MAX && b + last + 1 + r < e, need_b = before < 0 && b + first - 1 - r >= b;
+    if (!need_a && !need_b) break;                                                // block-uniform
+    int64_t va = need_a && ia < e && !pixel_mask(a, ia) ? ia - b : LLONG_MAX;
+    int64_t vb = need_b && ib >= b && !pixel_mask(a, ib) ? ib - b : -1;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      va = min(va, (int64_t)__shfl_xor(va, o));
+      vb = max(vb, (int64_t)__shfl_xor(vb, o));
     }
-    for (int64_t c = b + first - 1; c >= b; c -= kIngestThreads) {
-      const int64_t i = c - threadIdx.x;
-      if (i >= b && !pixel_mask(a, i)) before = max(before, i - b);
-      before = block_reduce(before, red64, [](int64_t x, int64_t y) { return x > y ? x : y; });
-      if (before >= 0) break;
+    __syncthreads();                                                              // red4 reuse
+    if (lane == 0) {
+      red4[0][wave] = va;
+      red4[1][wave] = vb;
     }
+    __syncthreads();
+    if (need_a) after = min(min(red4[0][0], red4[0][1]), min(red4[0][2], red4[0][3]));
+    if (need_b) before = max(max(red4[1][0], red4[1][1]), max(red4[1][2], red4[1][3]));
   }
   if (threadIdx.x != 0) return;
   ends[0] = last >= 0 ? first : -1;
