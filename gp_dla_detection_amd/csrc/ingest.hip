@@ -45,8 +45,15 @@
 namespace gpdla {
 namespace {
 
-constexpr int kIngestThreads = 256;
-constexpr int kWindowCap = 4096;            // median-set values per spectrum sorted in LDS (more: radix select)
+#ifndef GPDLA_INGEST_SCAN_THREADS
+#define GPDLA_INGEST_SCAN_THREADS 128          // with the 2,048 cap: 148 us per batch; 256 threads 159
+#endif
+#ifndef GPDLA_INGEST_WINDOW_CAP
+#define GPDLA_INGEST_WINDOW_CAP 2048            // LDS per block 8 KiB: more spectra per CU
+#endif
+constexpr int kIngestThreads = GPDLA_INGEST_SCAN_THREADS;   // the scan's block
+constexpr int kScanWaves = kIngestThreads / 64;
+constexpr int kWindowCap = GPDLA_INGEST_WINDOW_CAP;            // median-set values per spectrum sorted in LDS (more: radix select)
 #ifndef GPDLA_INGEST_SCAN_UNROLL
 #define GPDLA_INGEST_SCAN_UNROLL 4
 #endif
@@ -172,7 +179,10 @@ __device__ inline T block_reduce(T v, T* red, Op op) {
   __syncthreads();
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
   __syncthreads();
-  return op(op(red[0], red[1]), op(red[2], red[3]));
+  T r = red[0];
+#pragma unroll
+  for (int w = 1; w < kScanWaves; ++w) r = op(r, red[w]);
+  return r;
 }
 
 // A pixel of the median's set (preload_qsos.m:29-33): unmasked, in the normalisation window, flux
@@ -207,9 +217,9 @@ __device__ float window_select(const IngestArgs& a, int64_t b, int64_t e, const 
 __global__ __launch_bounds__(kIngestThreads) void preload_scan_kernel(IngestArgs a) {
   __shared__ float win[kWindowCap];
   __shared__ int nwin;
-  __shared__ int64_t red64[4];
-  __shared__ int32_t red32[4];
-  __shared__ int64_t red4[3][4];
+  __shared__ int64_t red64[kScanWaves];
+  __shared__ int32_t red32[kScanWaves];
+  __shared__ int64_t red4[3][kScanWaves];
   const int64_t q = blockIdx.x;
   const int64_t b = a.off[q], e = a.off[q + 1];
   int64_t* ends = a.ends + q * 4;
@@ -278,10 +288,17 @@ __global__ __launch_bounds__(kIngestThreads) void preload_scan_kernel(IngestArgs
     red4[2][wave] = last;
   }
   __syncthreads();
-  nrange = red32[0] + red32[1] + red32[2] + red32[3];
-  nload = red4[0][0] + red4[0][1] + red4[0][2] + red4[0][3];
-  first = min(min(red4[1][0], red4[1][1]), min(red4[1][2], red4[1][3]));
-  last = max(max(red4[2][0], red4[2][1]), max(red4[2][2], red4[2][3]));
+  nrange = red32[0];
+  nload = red4[0][0];
+  first = red4[1][0];
+  last = red4[2][0];
+#pragma unroll
+  for (int w = 1; w < kScanWaves; ++w) {
+    nrange += red32[w];
+    nload += red4[0][w];
+    first = min(first, red4[1][w]);
+    last = max(last, red4[2][w]);
+  }
   const int n = nwin;
   float lo = NAN, hi = NAN;                       // the set's middle values (the same one for odd n)
   if (n > kWindowCap) {
@@ -362,8 +379,14 @@ __global__ __launch_bounds__(kIngestThreads) void preload_scan_kernel(IngestArgs
       red4[1][wave] = vb;
     }
     __syncthreads();
-    if (need_a) after = min(min(red4[0][0], red4[0][1]), min(red4[0][2], red4[0][3]));
-    if (need_b) before = max(max(red4[1][0], red4[1][1]), max(red4[1][2], red4[1][3]));
+    int64_t ta = red4[0][0], tb = red4[1][0];
+#pragma unroll
+    for (int w = 1; w < kScanWaves; ++w) {
+      ta = min(ta, red4[0][w]);
+      tb = max(tb, red4[1][w]);
+    }
+    if (need_a) after = ta;
+    if (need_b) before = tb;
   }
   if (threadIdx.x != 0) return;
   ends[0] = last >= 0 ? first : -1;

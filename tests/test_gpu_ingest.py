@@ -181,7 +181,7 @@ def test_preload_range_ends_ulp_by_ulp():
 
 def _fine_spectra(rng, z, dex, ties=False):
     """A finely sampled spectrum whose normalisation window holds more values than the scan sorts in LDS
-    (4,096): the median then comes from the radix select.  Returned twice: as drawn, and with one more
+    (2,048): the median then comes from the radix select.  Returned twice: as drawn, and with one more
     window pixel masked (odd and even set sizes), with the set sizes."""
     ll = np.arange(np.log10(3400.0), np.log10(6000.0), dex).astype(np.float32)
     f = rng.normal(1.0, 2.0, ll.size).astype(np.float32)
@@ -209,7 +209,7 @@ def test_preload_median_of_a_window_beyond_lds():
         z += [zq, zq]
         cols += c
         sizes += n
-    assert min(sizes[:4]) > 4096 and max(sizes[4:]) < 4096
+    assert min(sizes[:4]) > 4096 and max(sizes[4:]) < 64       # radix select twice over; the register sort
     z = np.array(z)
     flags = np.zeros(z.size, np.uint8)
     got = I.preload_batch(z, flags, cols)
