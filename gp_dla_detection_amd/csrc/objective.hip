@@ -36,13 +36,55 @@ struct ObjArgs {
   const double* lya_1pz;     // [Q][ld]
   const double* noise;       // [Q][ld]
   const double* M;           // [P x k] column-major (x(1:P*k), objective.m:22-23)
+  const double* MT;          // [4 ceil(P / 4)][KP] the same M pixel-major, zero-padded (objective_mt_kernel)
   const double* log_omega;   // [P] (objective.m:25-26), or nullptr when omega2 is given
   const double* omega2;      // [P] spectrum_loss's omega2 argument directly, or nullptr
   double c_0, tau_0, beta;
   double* part_dM;           // [Q][k][P] per-spectrum dM (column-major per spectrum)
   double* part_dlo;          // [Q][P]
   double* part_s;            // [Q][kObjScalars]
+  double* part_px;           // [Q][4][P] pass 1's pixel terms for pass 6: an, da0, da1, da2 (:62-73)
 };
+
+// The tile plan of the matrix-core passes for a compile-time rank bound KB: [B - I | v] = M' [D^-1 M |
+// D^-1 y] as the upper 4x4 tile pairs (row tile rt of M', column tile ct of the right factor, whose
+// column k is D^-1 y), four pairs per v_mfma_f64_4x4x4_4b; and g = M' K^-1 y, four row tiles per
+// instruction.
+template <int KB>
+struct ObjTiles {
+  static constexpr int NTr = (KB + 3) / 4;
+  static constexpr int NTc = (KB + 4) / 4;
+  static constexpr int KP = 4 * NTc;                              // MT row length (doubles)
+  static constexpr int NP = NTr * NTc - NTr * (NTr - 1) / 2;      // pairs rt <= ct
+  static constexpr int NI = (NP + 3) / 4;
+  static constexpr int NG = (NTr + 3) / 4;
+};
+
+__host__ __device__ constexpr int obj_kb(int k) { return k <= 8 ? 8 : k <= 16 ? 16 : k <= 24 ? 24 : k <= 32 ? 32 : 64; }
+__host__ __device__ constexpr int obj_kp(int kb) { return 4 * ((kb + 4) / 4); }
+__host__ __device__ constexpr int obj_ni(int kb) {
+  return ((kb + 3) / 4 * ((kb + 4) / 4) - (kb + 3) / 4 * ((kb + 3) / 4 - 1) / 2 + 3) / 4;
+}
+
+// pair index (rt-major over rt <= ct < ntc) -> (rt, ct)
+__device__ inline void obj_pair(int idx, int ntc, int& rt, int& ct) {
+  rt = 0;
+  while (idx >= ntc - rt) {
+    idx -= ntc - rt;
+    ++rt;
+  }
+  ct = rt + idx;
+}
+
+// MT[p][r] = M[r][p] for p < P, r < k; zero elsewhere (the padding rows / columns the tiles read)
+__global__ __launch_bounds__(256) void objective_mt_kernel(const double* __restrict__ M, int32_t P, int32_t k,
+                                                           int32_t KP, int64_t rows, double* __restrict__ MT) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= rows * KP) return;
+  const int64_t p = e / KP;
+  const int r = (int)(e - p * KP);
+  MT[e] = (p < P && r < k) ? M[(int64_t)r * P + p] : 0.0;
+}
 
 __device__ inline double block_sum(double v, double* red) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -79,12 +121,11 @@ __global__ __launch_bounds__(kObjThreads) void objective_spectrum_kernel(ObjArgs
   const int64_t q = blockIdx.x;
   double* w = sm;              // [P] d^-1 (0 = excluded pixel)
   double* t = w + P;           // [P] D^-1 y, then K^-1 y
-  double* B = t + P;           // [k][k]
-  double* R = B + k * k;       // [k][k] upper Cholesky factor, then B^-1
-  double* v = R + k * k;       // [k] M' D^-1 y
-  double* s = v + k;           // [k] B^-1 M' D^-1 y  (= C y)
+  double* B = t + P;           // [k][k + 1]: [B | v] (pass 2), then [B^-1 | C y] (pass 3)
+  double* s = B + 2 * k * k + k;   // [k] B^-1 M' D^-1 y (= C y); B spans [k][k + 1] <= 2 k^2 + k doubles
   double* g = s + k;           // [k] (K^-1 y)' M
   double* red = g + k;         // [8] block reductions
+  double* scr = red + 8;       // [NI][64] the matrix-core passes' wave sums
   __shared__ int s_bad;
   const double* y = a.y + q * a.ld;
   const double* lya = a.lya_1pz + q * a.ld;
@@ -98,11 +139,20 @@ __global__ __launch_bounds__(kObjThreads) void objective_spectrum_kernel(ObjArgs
     const bool valid = !(yi != yi);                               // objective.m:43 ~isnan
     double wi = 0.0, ti = 0.0;
     if (valid) {
-      const PixelTerms p = pixel_terms(a, i, lya[i], nv[i]);
+      const double lyi = lya[i];
+      const PixelTerms p = pixel_terms(a, i, lyi, nv[i]);
       wi = 1.0 / p.d;                                             // :32
       ti = wi * yi;                                               // :33
       logd += log(p.d);                                           // :44
       cnt += 1.0;
+      // the gradient's pixel terms (:62-73) for pass 6, which would otherwise pay for the pow / exp /
+      // log again
+      double* px = a.part_px + q * 4 * (int64_t)P + i;
+      const double da1 = p.om2 * p.sf * p.tau * p.absorb;         // :69
+      px[0] = p.an;                                                // :62
+      px[P] = a.c_0 * p.om2 * p.sf;                               // :65
+      px[2 * P] = da1;
+      px[3 * P] = da1 * log(lyi) * a.beta;                        // :73
     }
     w[i] = wi;
     t[i] = ti;
@@ -110,78 +160,119 @@ __global__ __launch_bounds__(kObjThreads) void objective_spectrum_kernel(ObjArgs
   logd = block_sum(logd, red);
   cnt = block_sum(cnt, red);
 
-  // pass 2: B = M' (D^-1 M) + I (:41-42) and v = M' D^-1 y, one entry per thread
-  const int ngram = k * (k + 1) / 2;
-  for (int e = tid; e < ngram + k; e += kObjThreads) {
-    double acc = 0.0;
-    if (e < ngram) {
-      int r = 0, start = 0;
-      while (e >= start + (k - r)) { start += k - r; ++r; }
-      const int c = r + (e - start);
-      const double* Mr = a.M + (int64_t)r * P;
-      const double* Mc = a.M + (int64_t)c * P;
-      for (int i = 0; i < P; ++i) acc = fma(Mr[i], Mc[i] * w[i], acc);
-      B[r * k + c] = acc + (r == c ? 1.0 : 0.0);
-      B[c * k + r] = B[r * k + c];
-    } else {
-      const int r = e - ngram;
-      const double* Mr = a.M + (int64_t)r * P;
-      for (int i = 0; i < P; ++i) acc = fma(Mr[i], t[i], acc);
-      v[r] = acc;
+  // pass 2: [B | v] with B = M' (D^-1 M) + I (:41-42) and v = M' D^-1 y, k x (k + 1) row-major, on the
+  // f64 matrix cores (v_mfma_f64_4x4x4_4b:
+  // A[i][kk] at lane 16 kk + 4 b + i, B[kk][j] at 16 kk + 4 b + j, D[i][j] at 16 i + 4 b + j; block b of
+  // instruction m takes tile pair 4 m + b).  The waves take every 4th K step of 4 pixels, reading M from
+  // the pixel-major copy; their partial sums are added in wave order.
+  using TL = ObjTiles<KB>;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int kk = lane >> 4, bl = (lane >> 2) & 3, li = lane & 3;
+  const int nks = (P + 3) / 4;
+  {
+    int aoff[TL::NI], boff[TL::NI];
+    bool live[TL::NI];
+#pragma unroll
+    for (int m = 0; m < TL::NI; ++m) {
+      const int pair = 4 * m + bl;
+      live[m] = pair < TL::NP;
+      int rt, ct;
+      obj_pair(live[m] ? pair : 0, TL::NTc, rt, ct);
+      aoff[m] = 4 * rt + li;
+      boff[m] = 4 * ct + li;
+    }
+    double acc[TL::NI];
+#pragma unroll
+    for (int m = 0; m < TL::NI; ++m) acc[m] = 0.0;
+    // the operands of K step ks (zeros past the last one), loaded one step ahead of the MFMAs that use
+    // them (two register sets in turn)
+    auto load = [&](int ks, double (&av)[TL::NI], double (&bv)[TL::NI]) {
+      const bool in = ks < nks;
+      const int pp = 4 * ks + kk;
+      const double* row = a.MT + (int64_t)(in ? pp : 0) * TL::KP;
+      const double wv = (in && pp < P) ? w[pp] : 0.0, tv = (in && pp < P) ? t[pp] : 0.0;
+#pragma unroll
+      for (int m = 0; m < TL::NI; ++m) {
+        av[m] = (live[m] && in) ? row[aoff[m]] : 0.0;
+        bv[m] = fma(row[boff[m]], wv, boff[m] == k ? tv : 0.0);    // column k: D^-1 y
+      }
+    };
+    auto mma = [&](const double (&av)[TL::NI], const double (&bv)[TL::NI]) {
+#pragma unroll
+      for (int m = 0; m < TL::NI; ++m) acc[m] = __builtin_amdgcn_mfma_f64_4x4x4f64(av[m], bv[m], acc[m], 0, 0, 0);
+    };
+    double A0[TL::NI], B0[TL::NI];
+    if constexpr (TL::NI <= 16) {
+      double A1[TL::NI], B1[TL::NI];
+      load(wave, A0, B0);
+      for (int ks = wave; ks < nks; ks += 8) {
+        load(ks + 4, A1, B1);
+        mma(A0, B0);
+        if (ks + 4 < nks) {
+          load(ks + 8, A0, B0);
+          mma(A1, B1);
+        }
+      }
+    } else {  // (k > 32: two sets of 38 would spill)
+      for (int ks = wave; ks < nks; ks += 4) {
+        load(ks, A0, B0);
+        mma(A0, B0);
+      }
+    }
+    for (int wv = 0; wv < 4; ++wv) {
+      if (wave == wv)
+#pragma unroll
+        for (int m = 0; m < TL::NI; ++m) scr[m * 64 + lane] = (wv ? scr[m * 64 + lane] : 0.0) + acc[m];
+      __syncthreads();
+    }
+    for (int idx = tid; idx < TL::NI * 64; idx += kObjThreads) {
+      const int L = idx & 63, pair = 4 * (idx >> 6) + ((L >> 2) & 3);
+      if (pair >= TL::NP) continue;
+      int rt, ct;
+      obj_pair(pair, TL::NTc, rt, ct);
+      const int r = 4 * rt + (L >> 4), c = 4 * ct + (L & 3);
+      if (r >= k) continue;
+      if (c < k && r <= c) {
+        const double val = scr[idx] + (r == c ? 1.0 : 0.0);
+        B[r * (k + 1) + c] = val;
+        B[c * (k + 1) + r] = val;
+      } else if (c == k) {
+        B[r * (k + 1) + k] = scr[idx];                           // v, the augmented column
+      }
     }
   }
   __syncthreads();
 
-  // pass 3 (wave 0): upper Cholesky R'R = B (:43), log det, B^-1 = R^-1 R^-T, s = B^-1 v
-  if (tid < 64) {
-    const int lane = tid;
-    for (int r = lane; r < k * k; r += 64) R[r] = B[r];
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    for (int p = 0; p < k; ++p) {
-      const double dpp = R[p * k + p];
-      if (!(dpp > 0.0) && lane == 0) s_bad = 1;
-      const double rpp = sqrt(dpp);
-      __builtin_amdgcn_wave_barrier();
-      for (int c = p + 1 + lane; c < k; c += 64) R[p * k + c] /= rpp;
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      // trailing update R[r][c] -= R[p][r] R[p][c] for p < r <= c
-      for (int idx = lane; idx < (k - p - 1) * (k - p - 1); idx += 64) {
-        const int r = p + 1 + idx / (k - p - 1), c = p + 1 + idx % (k - p - 1);
-        if (c >= r) R[r * k + c] = fma(-R[p * k + r], R[p * k + c], R[r * k + c]);
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      if (lane == 0) R[p * k + p] = rpp;
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-    }
+  // pass 3: Gauss-Jordan on [B | v] by the whole block (B is symmetric positive definite with
+  // eigenvalues >= 1: no pivoting), 2 barriers per pivot: B^-1 in place, s = B^-1 v = C y in the
+  // augmented column (:46-48), log det B = the sum of the pivots' logs (= 2 sum log diag of
+  // spectrum_loss.m:43's Cholesky factor, :44); a non-positive pivot flags the spectrum as chol would
+  const int ld = k + 1;
+  {
     double ldb = 0.0;
-    for (int p = 0; p < k; ++p) ldb += log(R[p * k + p]);
-    if (lane == 0) red[6] = 2 * ldb;                              // 2 sum log diag L (:44)
-    // column j of B^-1 (lane j, in place in column j of B, which R has replaced): solve
-    // R' z = e_j, then R x = z
-    if (lane < k) {
-      const int j = lane;
-      for (int i = 0; i < k; ++i) {
-        double acc = (i == j) ? 1.0 : 0.0;
-        for (int m = 0; m < i; ++m) acc = fma(-R[m * k + i], B[m * k + j], acc);
-        B[i * k + j] = acc / R[i * k + i];
+    for (int p = 0; p < k; ++p) {
+      const double piv = B[p * ld + p];
+      if (tid == 0) {
+        if (!(piv > 0.0)) s_bad = 1;
+        ldb += log(piv);
       }
-      for (int i = k - 1; i >= 0; --i) {
-        double acc = B[i * k + j];
-        for (int m = i + 1; m < k; ++m) acc = fma(-R[i * k + m], B[m * k + j], acc);
-        B[i * k + j] = acc / R[i * k + i];
+      const double inv = 1.0 / piv;
+      for (int e = tid; e < k * ld; e += kObjThreads) {
+        const int i = e / ld, j = e - i * ld;
+        if (i != p && j != p) B[e] = fma(-B[i * ld + p] * inv, B[p * ld + j], B[e]);
       }
+      __syncthreads();
+      for (int e = tid; e < ld + k; e += kObjThreads) {
+        if (e < ld) {
+          B[p * ld + e] = e == p ? inv : B[p * ld + e] * inv;
+        } else if (e - ld != p) {
+          B[(e - ld) * ld + p] = -B[(e - ld) * ld + p] * inv;
+        }
+      }
+      __syncthreads();
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    if (lane < k) {
-      double acc = 0.0;
-      for (int c = 0; c < k; ++c) acc = fma(B[lane * k + c], v[c], acc);
-      s[lane] = acc;                                              // C y (:46-48)
-    }
+    if (tid == 0) red[6] = ldb;
+    for (int r = tid; r < k; r += kObjThreads) s[r] = B[r * ld + k];
   }
   __syncthreads();
   const double* Bi = B;
@@ -191,8 +282,14 @@ __global__ __launch_bounds__(kObjThreads) void objective_spectrum_kernel(ObjArgs
   for (int i = tid; i < P; i += kObjThreads) {
     const double wi = w[i];
     if (wi != 0.0) {
+      // the row's k loads issued together (a runtime-k loop waited on each in turn)
+      double Mi[KB];
+#pragma unroll
+      for (int r = 0; r < KB; ++r) Mi[r] = r < k ? a.M[(int64_t)r * P + i] : 0.0;
       double ms = 0.0;
-      for (int r = 0; r < k; ++r) ms = fma(a.M[(int64_t)r * P + i] * wi, s[r], ms);
+#pragma unroll
+      for (int r = 0; r < KB; ++r)
+        if (r < k) ms = fma(Mi[r] * wi, s[r], ms);
       const double ti = t[i] - ms;
       t[i] = ti;
       yky = fma(y[i], ti, yky);
@@ -200,12 +297,33 @@ __global__ __launch_bounds__(kObjThreads) void objective_spectrum_kernel(ObjArgs
   }
   yky = block_sum(yky, red);  // (its barriers also publish t)
 
-  // pass 5: g = (K^-1 y)' M (:55)
-  for (int r = tid; r < k; r += kObjThreads) {
-    const double* Mr = a.M + (int64_t)r * P;
-    double acc = 0.0;
-    for (int i = 0; i < P; ++i) acc = fma(t[i], Mr[i], acc);
-    g[r] = acc;
+  // pass 5: g = (K^-1 y)' M (:55) on the matrix cores: block b of instruction m takes row tile 4 m + b,
+  // with K^-1 y in column 0 of the B operand
+  {
+    double acc[TL::NG];
+#pragma unroll
+    for (int m = 0; m < TL::NG; ++m) acc[m] = 0.0;
+    for (int ks = wave; ks < nks; ks += 4) {
+      const int pp = 4 * ks + kk;
+      const double* row = a.MT + (int64_t)pp * TL::KP;
+      const double bv = (li == 0 && pp < P) ? t[pp] : 0.0;
+#pragma unroll
+      for (int m = 0; m < TL::NG; ++m) {
+        const int rt = 4 * m + bl;
+        const double av = rt < TL::NTr ? row[4 * rt + li] : 0.0;
+        acc[m] = __builtin_amdgcn_mfma_f64_4x4x4f64(av, bv, acc[m], 0, 0, 0);
+      }
+    }
+    for (int wv = 0; wv < 4; ++wv) {
+      if (wave == wv)
+#pragma unroll
+        for (int m = 0; m < TL::NG; ++m) scr[m * 64 + lane] = (wv ? scr[m * 64 + lane] : 0.0) + acc[m];
+      __syncthreads();
+    }
+    for (int idx = tid; idx < TL::NG * 64; idx += kObjThreads) {
+      const int L = idx & 63, r = 4 * (4 * (idx >> 6) + ((L >> 2) & 3)) + (L >> 4);
+      if ((L & 3) == 0 && r < k) g[r] = scr[idx];
+    }
   }
   __syncthreads();
 
@@ -225,24 +343,28 @@ __global__ __launch_bounds__(kObjThreads) void objective_spectrum_kernel(ObjArgs
     for (int r = 0; r < KB; ++r) Mi[r] = r < k ? a.M[(int64_t)r * P + i] : 0.0;
     const double ti = t[i];
     double qd = 0.0;
-    for (int c = 0; c < k; ++c) {
-      double u = 0.0;
+    // c unrolled to the compile-time bound too: M_ic is Mi[c] from the registers (a runtime c re-read
+    // it from memory and waited on that load at every column)
 #pragma unroll
-      for (int r = 0; r < KB; ++r)
-        if (r < k) u = fma(Mi[r], Bi[r * k + c], u);
-      // qd += u * M_ic (M_ic = Mi[c], read back from memory: c is a runtime index)
-      qd = fma(u, a.M[(int64_t)c * P + i], qd);
-      // dM = -(K^-1 y (K^-1 y' M) - K^-1 M), K^-1 M = D^-1 M B^-1 (:54-55)
-      dM[(int64_t)c * P + i] = -(ti * g[c] - wi * u);
+    for (int c = 0; c < KB; ++c) {
+      if (c < k) {
+        double u = 0.0;
+#pragma unroll
+        for (int r = 0; r < KB; ++r)
+          if (r < k) u = fma(Mi[r], Bi[r * ld + c], u);
+        qd = fma(u, Mi[c], qd);
+        // dM = -(K^-1 y (K^-1 y' M) - K^-1 M), K^-1 M = D^-1 M B^-1 (:54-55)
+        dM[(int64_t)c * P + i] = -(ti * g[c] - wi * u);
+      }
     }
     const double dk = wi - wi * wi * qd;                          // diag K^-1 (:59)
-    const PixelTerms p = pixel_terms(a, i, lya[i], nv[i]);
-    dlo[i] = -(p.an * (ti * ti - dk));                            // :62
-    const double da0 = a.c_0 * p.om2 * p.sf;                      // :65
+    const double* px = a.part_px + q * 4 * (int64_t)P + i;        // pass 1's terms
+    dlo[i] = -(px[0] * (ti * ti - dk));                           // :62
+    const double da0 = px[P];                                     // :65
     sc0 += -(ti * da0) * ti + dk * da0;                           // :66
-    const double da1 = p.om2 * p.sf * p.tau * p.absorb;           // :69
+    const double da1 = px[2 * P];                                 // :69
     stau += -(ti * da1) * ti + dk * da1;                          // :70
-    const double da2 = da1 * log(lya[i]) * a.beta;                // :73
+    const double da2 = px[3 * P];                                 // :73
     sbeta += -(ti * da2) * ti + dk * da2;                         // :74
   }
   sc0 = block_sum(sc0, red);
@@ -261,13 +383,29 @@ __global__ __launch_bounds__(kObjThreads) void objective_spectrum_kernel(ObjArgs
   }
 }
 
-// sum the per-spectrum partials in spectrum order into the running totals (objective.m:46-52)
-__global__ __launch_bounds__(256) void objective_sum_kernel(int64_t nq, int64_t per, const double* part,
-                                                            double* total) {
-  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+// sum the per-spectrum partials in spectrum order into the running totals (objective.m:46-52).  One
+// thread per element walks the spectra in order; kSumDepth partials are loaded before the adds that
+// use them, so a thread keeps that many loads in flight instead of one (the adds, and so the result,
+// stay in spectrum order)
+constexpr int kSumDepth = 32;
+
+constexpr int kSumThreads = 64;   // one wave per block: the few thousand elements spread over every CU
+
+__global__ __launch_bounds__(kSumThreads) void objective_sum_kernel(int64_t nq, int64_t per,
+                                                                    const double* __restrict__ part,
+                                                                    double* __restrict__ total) {
+  const int64_t e = (int64_t)blockIdx.x * kSumThreads + threadIdx.x;
   if (e >= per) return;
   double acc = total[e];
-  for (int64_t q = 0; q < nq; ++q) acc += part[q * per + e];
+  int64_t q = 0;
+  for (; q + kSumDepth <= nq; q += kSumDepth) {
+    double v[kSumDepth];
+#pragma unroll
+    for (int j = 0; j < kSumDepth; ++j) v[j] = part[(q + j) * per + e];
+#pragma unroll
+    for (int j = 0; j < kSumDepth; ++j) acc += v[j];
+  }
+  for (; q < nq; ++q) acc += part[q * per + e];
   total[e] = acc;
 }
 
@@ -291,7 +429,9 @@ struct gpdla_objective {
   double* part_dM = nullptr;  // [batch][k][P]
   double* part_dlo = nullptr;
   double* part_s = nullptr;
+  double* part_px = nullptr;  // [batch][4][P]
   double* tot = nullptr;      // [k P + P + kObjScalars]
+  double* mt = nullptr;       // [4 ceil(P / 4)][obj_kp(obj_kb(k))] pixel-major M
 };
 
 namespace {
@@ -301,7 +441,9 @@ int obj_fail(gpdla_objective* o, int rc) {
   return rc;
 }
 
-size_t obj_shared_bytes(int64_t P, int k) { return (size_t)(2 * P + 2 * k * k + 3 * k + 8) * sizeof(double); }
+size_t obj_shared_bytes(int64_t P, int k) {
+  return (size_t)(2 * P + 2 * k * k + 3 * k + 8 + 64 * obj_ni(obj_kb(k))) * sizeof(double);
+}
 
 // one pass over all spectra with the M / log omega / (c_0, tau_0, beta) already in place
 int obj_run(gpdla_objective* o, const double* dM_src, const double* lo_src, const double* om2_src,
@@ -311,6 +453,10 @@ int obj_run(gpdla_objective* o, const double* dM_src, const double* lo_src, cons
   const int64_t per_dM = (int64_t)k * P;
   HIP_TRY(hipMemsetAsync(o->tot, 0, (per_dM + P + kObjScalars) * sizeof(double), o->stream));
   const size_t shm = obj_shared_bytes(P, k);
+  const int KP = obj_kp(obj_kb(k));
+  const int64_t mt_rows = 4 * ((P + 3) / 4);
+  hipLaunchKernelGGL(objective_mt_kernel, dim3((unsigned)((mt_rows * KP + 255) / 256)), dim3(256), 0, o->stream,
+                     dM_src, (int32_t)P, (int32_t)k, (int32_t)KP, mt_rows, o->mt);
   for (int64_t q0 = 0; q0 < o->Q; q0 += o->batch) {
     const int64_t nq = std::min(o->batch, o->Q - q0);
     ObjArgs a{};
@@ -321,6 +467,7 @@ int obj_run(gpdla_objective* o, const double* dM_src, const double* lo_src, cons
     a.lya_1pz = o->lya + q0 * P;
     a.noise = o->noise + q0 * P;
     a.M = dM_src;
+    a.MT = o->mt;
     a.log_omega = lo_src;
     a.omega2 = om2_src;
     a.c_0 = c_0;
@@ -329,6 +476,7 @@ int obj_run(gpdla_objective* o, const double* dM_src, const double* lo_src, cons
     a.part_dM = o->part_dM;
     a.part_dlo = o->part_dlo;
     a.part_s = o->part_s;
+    a.part_px = o->part_px;
     const dim3 grid((unsigned)nq), blk(kObjThreads);
     // dynamic LDS above 64 KiB (long rest grids with high rank) must be opted into per kernel
     auto launch = [&](auto kern) -> int {
@@ -345,11 +493,13 @@ int obj_run(gpdla_objective* o, const double* dM_src, const double* lo_src, cons
              : k <= 32 ? launch(objective_spectrum_kernel<32>)
                        : launch(objective_spectrum_kernel<64>);
     if (rc) return rc;
-    hipLaunchKernelGGL(objective_sum_kernel, dim3((unsigned)((per_dM + 255) / 256)), dim3(256), 0, o->stream,
+    hipLaunchKernelGGL(objective_sum_kernel, dim3((unsigned)((per_dM + kSumThreads - 1) / kSumThreads)),
+                       dim3(kSumThreads), 0, o->stream,
                        nq, per_dM, (const double*)o->part_dM, o->tot);
-    hipLaunchKernelGGL(objective_sum_kernel, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, o->stream,
+    hipLaunchKernelGGL(objective_sum_kernel, dim3((unsigned)((P + kSumThreads - 1) / kSumThreads)), dim3(kSumThreads),
+                       0, o->stream,
                        nq, P, (const double*)o->part_dlo, o->tot + per_dM);
-    hipLaunchKernelGGL(objective_sum_kernel, dim3(1), dim3(256), 0, o->stream, nq, (int64_t)kObjScalars,
+    hipLaunchKernelGGL(objective_sum_kernel, dim3(1), dim3(kSumThreads), 0, o->stream, nq, (int64_t)kObjScalars,
                        (const double*)o->part_s, o->tot + per_dM + P);
     HIP_TRY(hipGetLastError());
   }
@@ -375,7 +525,9 @@ void gpdla_objective_destroy(gpdla_objective* o) {
   (void)hipFree(o->part_dM);
   (void)hipFree(o->part_dlo);
   (void)hipFree(o->part_s);
+  (void)hipFree(o->part_px);
   (void)hipFree(o->tot);
+  (void)hipFree(o->mt);
   if (o->stream) (void)hipStreamDestroy(o->stream);
   delete o;
 }
@@ -399,9 +551,10 @@ int gpdla_objective_create(int32_t device, int64_t num_quasars, int64_t num_pixe
   o->Q = num_quasars;
   o->P = num_pixels;
   o->k = k;
-  // spectra per launch: bounded by the partial-gradient buffer (<= 1 GiB)
+  // spectra per launch: bounded by the partial-gradient buffers (<= 4 GiB; a DR9-sized training set in one)
   const int64_t per = (int64_t)(k + 1) * num_pixels + kObjScalars;
-  o->batch = std::max<int64_t>(1, std::min<int64_t>(std::max<int64_t>(num_quasars, 1), (1LL << 27) / per));
+  o->batch = std::max<int64_t>(1, std::min<int64_t>(std::max<int64_t>(num_quasars, 1),
+                                                    (1LL << 29) / (per + 4 * num_pixels)));
   if (hipStreamCreateWithFlags(&o->stream, hipStreamNonBlocking) != hipSuccess)
     return obj_fail(o, set_error(GPDLA_EDEVICE, "hipStreamCreate failed"));
   const size_t data = (size_t)std::max<int64_t>(num_quasars, 1) * num_pixels * sizeof(double);
@@ -424,7 +577,9 @@ int gpdla_objective_create(int32_t device, int64_t num_quasars, int64_t num_pixe
       hipMalloc(&o->part_dM, (size_t)o->batch * k * num_pixels * sizeof(double)) != hipSuccess ||
       hipMalloc(&o->part_dlo, (size_t)o->batch * num_pixels * sizeof(double)) != hipSuccess ||
       hipMalloc(&o->part_s, (size_t)o->batch * kObjScalars * sizeof(double)) != hipSuccess ||
-      hipMalloc(&o->tot, (size_t)per * sizeof(double)) != hipSuccess)
+      hipMalloc(&o->part_px, (size_t)o->batch * 4 * num_pixels * sizeof(double)) != hipSuccess ||
+      hipMalloc(&o->tot, (size_t)per * sizeof(double)) != hipSuccess ||
+      hipMalloc(&o->mt, (size_t)(4 * ((num_pixels + 3) / 4)) * obj_kp(obj_kb(k)) * sizeof(double)) != hipSuccess)
     return obj_fail(o, set_error(GPDLA_ENOMEM, "objective workspace allocation failed"));
   *out = o;
   return GPDLA_OK;
