@@ -247,9 +247,15 @@ def cpu_baseline(model, samples, spectra, budget_s: float, k: int, widened: bool
 
 
 def widened_cpu_baseline() -> dict:
-    """The numpy restatements of the widened rows on one core, beside alternatives.dla_samples and
-    alternatives.ingest: generate_dla_samples at 10^5 samples (oracle/dla_samples_closed_form.py) and
-    preload_qsos over 1,024 of the ingest leg's BOSS coadds (oracle/ingest_oracle.py)."""
+    """The numpy restatements of the widened rows, beside alternatives.dla_samples, .ingest and .objective:
+    generate_dla_samples at 10^5 samples (oracle/dla_samples_closed_form.py), preload_qsos over 1,024 of
+    the ingest leg's BOSS coadds (oracle/ingest_oracle.py), the training objective over 200 spectra."""
+    from threadpoolctl import threadpool_limits
+    with threadpool_limits(limits=1):                 # one core, BLAS included
+        return _widened_cpu_baseline()
+
+
+def _widened_cpu_baseline() -> dict:
     from oracle import dla_samples_closed_form as DC
     from oracle import ingest_oracle as IO
     ln = widened_catalogue()
@@ -261,7 +267,17 @@ def widened_cpu_baseline() -> dict:
     IO.preload_from_columns(zp, np.zeros(zp.size, np.uint8), pool)
     el_p = time.perf_counter() - t0
     npx = sum(c[0].size for c in pool)
-    return {"generate_dla_samples": {"value": WIDENED_SAMPLES / el_s, "unit": "samples/s", "cores": 1, "kind": "port",
+    from oracle import gpdla_oracle as GO
+    y, lya, nv, x = objective_problem(Q=200)
+    GO.objective(x, y[:8], lya[:8], nv[:8])           # warm-up (first-call set-up)
+    t0 = time.perf_counter()
+    GO.objective(x, y, lya, nv)
+    el_o = time.perf_counter() - t0
+    return {"objective": {"value": y.shape[0] / el_o, "unit": "spectra/s", "cores": 1, "kind": "port",
+                          "sample": f"objective.m f + gradient over 200 spectra of the 5,000-spectrum problem's shape in "
+                                    f"{el_o:.2f} s (numpy restatement, oracle/gpdla_oracle.py, one BLAS "
+                                    "thread)"},
+            "generate_dla_samples": {"value": WIDENED_SAMPLES / el_s, "unit": "samples/s", "cores": 1, "kind": "port",
                                      "sample": f"{WIDENED_SAMPLES} samples in {el_s:.2f} s (numpy/scipy restatement)"},
             "preload_qsos": {"value": npx / el_p, "unit": "pixels/s", "cores": 1, "kind": "port",
                              "sample": f"1,024 synthetic BOSS coadds ({npx:,} pixels) in {el_p:.2f} s "
@@ -660,6 +676,55 @@ def boss_pool(npool: int, seed: int = 31):
     rng = np.random.default_rng(seed)
     zp = rng.uniform(2.15, 5.5, npool)
     return zp, [syn.make_boss_coadd_columns(rng, z) for z in zp]
+
+
+OBJ_Q, OBJ_P, OBJ_K = 5_000, 1_217, 20   # a DR9-training-set-sized problem on the 1,217-pixel rest grid
+
+
+def objective_problem(Q: int = OBJ_Q, P: int = OBJ_P, k: int = OBJ_K, seed: int = 3):
+    """learn_qso_model.m's objective inputs, synthetic: centred fluxes with ~30% missing pixels, (1 +
+    z_Lya) and noise per pixel, and a parameter vector [M; log omega; log c_0, log tau_0, log beta]."""
+    rng = np.random.default_rng(seed)
+    y = 0.3 * rng.standard_normal((Q, P))
+    y[rng.uniform(size=y.shape) < 0.3] = np.nan
+    lya = rng.uniform(2.5, 4.5, (Q, P))
+    nv = rng.uniform(0.01, 0.1, (Q, P))
+    x = np.concatenate([0.05 * rng.standard_normal(P * k), np.log(0.15) + 0.1 * rng.standard_normal(P),
+                        [np.log(0.1), np.log(0.0023), np.log(3.65)]])
+    return y, lya, nv, x
+
+
+def objective_flops(y, k: int) -> float:
+    """Algorithmic flops of objective.m's f + g (spectrum_loss.m:23-74 over every spectrum) as the
+    Woodbury form computes them: per valid pixel the Gram k(k+1), M'D^-1 y / M C y / (K^-1 y)'M 6k, the
+    u = M_i B^-1 rows 2k^2, diag K^-1 2k, dM 3k; per spectrum k^3 for B^-1."""
+    n = np.sum(~np.isnan(y), axis=1).astype(np.float64)
+    return float(np.sum(n * (3 * k * k + 12 * k) + k ** 3))
+
+
+def objective_alternative(dev: int, reps: int = 10) -> dict:
+    """objective.m's f and gradient (spectrum_loss.m summed over the training set in
+    spectrum order) on the device for a DR9-training-set-sized problem (5,000 spectra x 1,217 rest
+    pixels, k = 20): one warm-up evaluation, then ``reps`` timed ones; kernel times from a one-launch
+    evaluation under HIP events are not exposed, so the roofline is over the evaluation's wall time."""
+    from gp_dla_detection_amd import training as T
+    y, lya, nv, x = objective_problem()
+    with T.Objective(y, lya, nv, OBJ_K, device=dev) as obj:
+        f0, g0 = obj(x)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            f, g = obj(x)
+        el = (time.perf_counter() - t0) / reps
+    flops = objective_flops(y, OBJ_K)
+    ok = bool(np.isfinite(f) and np.all(np.isfinite(g)) and f == f0 and np.array_equal(g, g0))
+    return {"value": OBJ_Q / el, "unit": "spectra/s", "ms_per_step": el * 1e3, "steps": reps,
+            "config": {"workload": "objective.m f + gradient, 5,000 synthetic training spectra x 1,217 rest pixels "
+                                   "(~30% missing), k = 20 (SURVEY 8f-3)"},
+            "roofline": {"bound": "fp64", "unit": "TFLOP/s", "peak": FP64_PEAK_TFLOPS,
+                         "achieved": flops / el / 1e12, "frac": flops / el / 1e12 / FP64_PEAK_TFLOPS,
+                         "flops": flops, "note": "algorithmic flops (objective_flops) over the whole evaluation "
+                                                 "(spectrum kernel + the spectrum-ordered gradient sums + copies)"},
+            "checks_ok": ok, "repeat_bitwise_equal": ok}
 
 
 def dla_samples_alternative(dev: int, reps: int = 5) -> dict:
@@ -1213,6 +1278,7 @@ def main():
         if not args.no_widened:  # SURVEY 8f-2 and 8f-4 on the device, CPU restatements in cpu_baseline
             alt["dla_samples"] = dla_samples_alternative(dev)
             alt["ingest"] = ingest_alternative(dev)
+            alt["objective"] = objective_alternative(dev)
 
     # sanity: finite outputs and the calc_cddf.py:246 normalisation invariant on every spectrum
     inv = invariant_all_rows(o_s, o_dla, S)

@@ -5,6 +5,7 @@ import importlib.util
 import json
 from pathlib import Path
 
+import numpy as np
 import pytest
 
 ROOT = Path(__file__).resolve().parents[1]
@@ -98,7 +99,7 @@ def test_widened_cpu_baseline(bench):
     """The widened rows' CPU restatements (beside alternatives.dla_samples / .ingest) run on the host
     and report positive one-core rates with their samples named."""
     w = bench.widened_cpu_baseline()
-    for key, unit in (("generate_dla_samples", "samples/s"), ("preload_qsos", "pixels/s")):
+    for key, unit in (("generate_dla_samples", "samples/s"), ("preload_qsos", "pixels/s"), ("objective", "spectra/s")):
         assert w[key]["value"] > 0 and w[key]["unit"] == unit and w[key]["cores"] == 1 and w[key]["kind"] == "port"
         assert w[key]["sample"]
 
@@ -110,3 +111,9 @@ def test_ingest_profile_summary(bench):
     for k in ("preload_scan_kernel", "preload_write_kernel"):
         assert kp[k]["launches"] == 11 and kp[k]["total_ms"] > 0
         assert abs(kp[k]["pmc_bytes"] / kp[k]["algorithmic_bytes"] - 1) < 0.10
+
+
+def test_objective_flops_accounting(bench):
+    """The objective leg's algorithmic flops: per valid pixel 3k^2 + 12k, per spectrum k^3."""
+    y = np.array([[1.0, np.nan, 2.0], [np.nan, np.nan, 3.0]])
+    assert bench.objective_flops(y, 4) == 2 * (3 * 16 + 48) + 64 + 1 * (3 * 16 + 48) + 64
