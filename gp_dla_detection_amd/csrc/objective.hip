@@ -114,7 +114,10 @@ __device__ inline PixelTerms pixel_terms(const ObjArgs& a, int i, double lya, do
 
 // KB: compile-time bound on k (register arrays, unrolled loops); the rank itself is a.k <= KB
 template <int KB>
-__global__ __launch_bounds__(kObjThreads) void objective_spectrum_kernel(ObjArgs a) {
+// k <= 24 at 3 waves per SIMD (the compiler otherwise spends AGPRs on the Gram pass and settles at 2:
+// 1.73 vs 1.33 ms per 5,000 spectra)
+__global__ __launch_bounds__(kObjThreads) __attribute__((amdgpu_waves_per_eu(KB <= 24 ? 3 : 1)))
+void objective_spectrum_kernel(ObjArgs a) {
   extern __shared__ double sm[];
   const int P = a.P, k = a.k;
   const int tid = threadIdx.x;
@@ -169,7 +172,75 @@ __global__ __launch_bounds__(kObjThreads) void objective_spectrum_kernel(ObjArgs
   const int lane = tid & 63, wave = tid >> 6;
   const int kk = lane >> 4, bl = (lane >> 2) & 3, li = lane & 3;
   const int nks = (P + 3) / 4;
-  {
+  if constexpr (TL::NP <= 28) {
+    // k <= 24: the four blocks of an instruction split 16 pixels 4 ways and share one tile pair, so a
+    // lane's operands are its own pixel's row at columns 4 t + i of every column tile t (NTc loads per
+    // 16 pixels; each B operand w M (or D^-1 y) formed once per tile); the blocks' partial tiles are
+    // summed with two lane exchanges at the end
+    const int p_lane = 4 * bl + kk;                                 // pixel within the 16
+    double acc[TL::NP];
+#pragma unroll
+    for (int m = 0; m < TL::NP; ++m) acc[m] = 0.0;
+    auto load = [&](int s16, double (&v)[TL::NTc], double& wv, double& tv) {
+      const int pp = 16 * s16 + p_lane;
+      const bool in = pp < P;
+      const double* row = a.MT + (int64_t)(in ? pp : 0) * TL::KP + li;
+#pragma unroll
+      for (int c = 0; c < TL::NTc; ++c) v[c] = in ? row[4 * c] : 0.0;
+      wv = in ? w[pp] : 0.0;
+      tv = in ? t[pp] : 0.0;
+    };
+    auto mma = [&](const double (&v)[TL::NTc], double wv, double tv) {
+      double bw[TL::NTc];
+#pragma unroll
+      for (int ct = 0; ct < TL::NTc; ++ct) bw[ct] = fma(v[ct], wv, 4 * ct + li == k ? tv : 0.0);
+      int m = 0;
+#pragma unroll
+      for (int rt = 0; rt < TL::NTr; ++rt)
+#pragma unroll
+        for (int ct = rt; ct < TL::NTc; ++ct, ++m)
+          acc[m] = __builtin_amdgcn_mfma_f64_4x4x4f64(v[rt], bw[ct], acc[m], 0, 0, 0);
+    };
+    const int n16 = (P + 15) / 16;
+    double v0[TL::NTc], v1[TL::NTc], w0, t0, w1, t1;
+    load(wave, v0, w0, t0);
+    for (int s16 = wave; s16 < n16; s16 += 8) {
+      load(s16 + 4, v1, w1, t1);
+      mma(v0, w0, t0);
+      if (s16 + 4 < n16) {
+        load(s16 + 8, v0, w0, t0);
+        mma(v1, w1, t1);
+      }
+    }
+#pragma unroll
+    for (int m = 0; m < TL::NP; ++m) {
+      acc[m] += __shfl_xor(acc[m], 4);
+      acc[m] += __shfl_xor(acc[m], 8);
+    }
+    // lanes 16 i + j (b = 0) hold D[i][j] of every pair: scr[pair][i][j], added in wave order
+    for (int wv = 0; wv < 4; ++wv) {
+      if (wave == wv && bl == 0)
+#pragma unroll
+        for (int m = 0; m < TL::NP; ++m) {
+          double& d = scr[m * 16 + (lane >> 4) * 4 + li];
+          d = (wv ? d : 0.0) + acc[m];
+        }
+      __syncthreads();
+    }
+    for (int idx = tid; idx < TL::NP * 16; idx += kObjThreads) {
+      int rt, ct;
+      obj_pair(idx >> 4, TL::NTc, rt, ct);
+      const int r = 4 * rt + ((idx >> 2) & 3), c = 4 * ct + (idx & 3);
+      if (r >= k) continue;
+      if (c < k && r <= c) {
+        const double val = scr[idx] + (r == c ? 1.0 : 0.0);
+        B[r * (k + 1) + c] = val;
+        B[c * (k + 1) + r] = val;
+      } else if (c == k) {
+        B[r * (k + 1) + k] = scr[idx];                           // v, the augmented column
+      }
+    }
+  } else {
     int aoff[TL::NI], boff[TL::NI];
     bool live[TL::NI];
 #pragma unroll
