@@ -125,3 +125,9 @@ def test_run_generate_dla_samples_files(tmp_path):
     np.testing.assert_array_equal(s["nhi_samples"], out["nhi_samples"])
     np.testing.assert_allclose(out["log_nhi_samples"], CF.generate_dla_samples(cells, 500)["log_nhi_samples"],
                                rtol=0, atol=1e-12)
+
+
+def test_generate_reports_its_kernel_times():
+    DS.generate_dla_samples(np.r_[np.linspace(20.3, 21.5, 50), np.linspace(20.4, 22.0, 30)], 1000)
+    ms = L.last_call_kernel_ms()
+    assert len(ms) == 3 and all(0 < t < 1000 for t in ms)          # KDE, Halton, inverse CDF

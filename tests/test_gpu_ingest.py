@@ -316,3 +316,13 @@ def test_errors_are_loud():
                                          L.ptr(fl, C.c_uint8), L.ptr(np.zeros(3, np.int64), C.c_int64), None, None,
                                          None, None, L.ptr(np.zeros(2)), None)
     assert rc == L.GPDLA_EINVAL
+
+
+def test_last_call_kernel_times():
+    """gpdla_last_call_kernel_ms reports one HIP-event time per launch of this thread's last call."""
+    z, flags, cols = preload_cases()
+    I.preload_batch(z, flags, cols)
+    ms = L.last_call_kernel_ms()
+    assert len(ms) == 3 and all(0 < t < 1000 for t in ms)          # keys, scan, write
+    w, f, nv, pm = I.read_spec(str(GOLDEN / "speclite_fixture.fits"))
+    assert len(L.last_call_kernel_ms()) == 1
