@@ -398,45 +398,102 @@ void objective_spectrum_kernel(ObjArgs a) {
   }
   __syncthreads();
 
-  // pass 6: per pixel u = M_i B^-1, diag K^-1, dM row, d log omega, scalar gradient sums
+  // pass 6: per pixel u = M_i B^-1 (K^-1 M = D^-1 M B^-1, :55), diag K^-1 = d^-1 - d^-2 diag(M B^-1 M')
+  // (:59), the dM row (:54-55), d log omega (:62) and the scalar gradient sums (:65-74).  For k > 32 the
+  // u rows come from the matrix cores (k = 50: 22.5 -> 19.7 ms per 5,000 spectra); up to 32 the VALU
+  // form below is faster (1.33 vs 1.64 ms at k = 20)
   double sc0 = 0.0, stau = 0.0, sbeta = 0.0;
   double* dM = a.part_dM + q * (int64_t)k * P;
   double* dlo = a.part_dlo + q * (int64_t)P;
-  for (int i = tid; i < P; i += kObjThreads) {
-    const double wi = w[i];
-    if (wi == 0.0) {
-      for (int r = 0; r < k; ++r) dM[(int64_t)r * P + i] = 0.0;
-      dlo[i] = 0.0;
-      continue;
-    }
-    double Mi[KB];
+  if constexpr (KB > 32) {
+    // U = M B^-1 with 16 pixels x 4 columns per accumulator: block b of v_mfma_f64_4x4x4_4b takes
+    // pixels p16 + 4 b .. + 3 (A[i][kk] = B^-1[4 rc + kk][4 ct + i] at lane 16 kk + 4 b + i, the same for
+    // the four blocks; B[kk][j] = M[p16 + 4 b + j][4 rc + kk] at lane 16 kk + 4 b + j), so D[i][j] =
+    // U[p16 + 4 b + j][4 ct + i] sits at lane 16 i + 4 b + j: each column's 16 pixels in 16 consecutive
+    // lanes (whole-line dM stores)
+    constexpr int NCT = (KB + 3) / 4;
+    const double* px = a.part_px + q * 4 * (int64_t)P;
+    const int n16p = (P + 15) / 16;
+    const int pj = lane & 15, ci = lane >> 4;
+    for (int pt = wave; pt < n16p; pt += 4) {
+      const int p16 = 16 * pt;
+      const int pp = p16 + pj;
+      const int pb = pp < P ? pp : P - 1;
+      const double* mrow = a.MT + (int64_t)pb * TL::KP;
+      const double wi = pp < P ? w[pp] : 0.0, ti = pp < P ? t[pp] : 0.0;
+      double qd = 0.0;
 #pragma unroll
-    for (int r = 0; r < KB; ++r) Mi[r] = r < k ? a.M[(int64_t)r * P + i] : 0.0;
-    const double ti = t[i];
-    double qd = 0.0;
-    // c unrolled to the compile-time bound too: M_ic is Mi[c] from the registers (a runtime c re-read
-    // it from memory and waited on that load at every column)
+      for (int ct = 0; ct < NCT; ++ct) {
+        const int c = 4 * ct + ci;
+        double acc = 0.0;
 #pragma unroll
-    for (int c = 0; c < KB; ++c) {
-      if (c < k) {
-        double u = 0.0;
-#pragma unroll
-        for (int r = 0; r < KB; ++r)
-          if (r < k) u = fma(Mi[r], Bi[r * ld + c], u);
-        qd = fma(u, Mi[c], qd);
-        // dM = -(K^-1 y (K^-1 y' M) - K^-1 M), K^-1 M = D^-1 M B^-1 (:54-55)
-        dM[(int64_t)c * P + i] = -(ti * g[c] - wi * u);
+        for (int rc = 0; rc < TL::NTr; ++rc) {
+          const int ar = 4 * rc + (lane >> 4), ac = 4 * ct + (lane & 3);
+          const double av = (ar < k && ac < k) ? Bi[ar * ld + ac] : 0.0;
+          acc = __builtin_amdgcn_mfma_f64_4x4x4f64(av, mrow[4 * rc + (lane >> 4)], acc, 0, 0, 0);
+        }
+        if (pp < P && c < k) {
+          qd = fma(acc, mrow[c], qd);
+          dM[(int64_t)c * P + pp] = wi == 0.0 ? 0.0 : -(ti * g[c] - wi * acc);
+        }
+      }
+      qd += __shfl_xor(qd, 16);
+      qd += __shfl_xor(qd, 32);
+      if (ci == 0 && pp < P) {
+        if (wi == 0.0) {
+          dlo[pp] = 0.0;
+        } else {
+          const double dk = wi - wi * wi * qd;
+          dlo[pp] = -(px[pp] * (ti * ti - dk));
+          const double da0 = px[P + pp];
+          sc0 += -(ti * da0) * ti + dk * da0;
+          const double da1 = px[2 * P + pp];
+          stau += -(ti * da1) * ti + dk * da1;
+          const double da2 = px[3 * P + pp];
+          sbeta += -(ti * da2) * ti + dk * da2;
+        }
       }
     }
-    const double dk = wi - wi * wi * qd;                          // diag K^-1 (:59)
-    const double* px = a.part_px + q * 4 * (int64_t)P + i;        // pass 1's terms
-    dlo[i] = -(px[0] * (ti * ti - dk));                           // :62
-    const double da0 = px[P];                                     // :65
-    sc0 += -(ti * da0) * ti + dk * da0;                           // :66
-    const double da1 = px[2 * P];                                 // :69
-    stau += -(ti * da1) * ti + dk * da1;                          // :70
-    const double da2 = px[3 * P];                                 // :73
-    sbeta += -(ti * da2) * ti + dk * da2;                         // :74
+
+  } else {
+    // pass 6: per pixel u = M_i B^-1, diag K^-1, dM row, d log omega, scalar gradient sums
+    for (int i = tid; i < P; i += kObjThreads) {
+      const double wi = w[i];
+      if (wi == 0.0) {
+        for (int r = 0; r < k; ++r) dM[(int64_t)r * P + i] = 0.0;
+        dlo[i] = 0.0;
+        continue;
+      }
+      double Mi[KB];
+#pragma unroll
+      for (int r = 0; r < KB; ++r) Mi[r] = r < k ? a.M[(int64_t)r * P + i] : 0.0;
+      const double ti = t[i];
+      double qd = 0.0;
+      // c unrolled to the compile-time bound too: M_ic is Mi[c] from the registers (a runtime c re-read
+      // it from memory and waited on that load at every column)
+#pragma unroll
+      for (int c = 0; c < KB; ++c) {
+        if (c < k) {
+          double u = 0.0;
+#pragma unroll
+          for (int r = 0; r < KB; ++r)
+            if (r < k) u = fma(Mi[r], Bi[r * ld + c], u);
+          qd = fma(u, Mi[c], qd);
+          // dM = -(K^-1 y (K^-1 y' M) - K^-1 M), K^-1 M = D^-1 M B^-1 (:54-55)
+          dM[(int64_t)c * P + i] = -(ti * g[c] - wi * u);
+        }
+      }
+      const double dk = wi - wi * wi * qd;                          // diag K^-1 (:59)
+      const double* px = a.part_px + q * 4 * (int64_t)P + i;        // pass 1's terms
+      dlo[i] = -(px[0] * (ti * ti - dk));                           // :62
+      const double da0 = px[P];                                     // :65
+      sc0 += -(ti * da0) * ti + dk * da0;                           // :66
+      const double da1 = px[2 * P];                                 // :69
+      stau += -(ti * da1) * ti + dk * da1;                          // :70
+      const double da2 = px[3 * P];                                 // :73
+      sbeta += -(ti * da2) * ti + dk * da2;                         // :74
+    }
+
   }
   sc0 = block_sum(sc0, red);
   stau = block_sum(stau, red);
