@@ -7,8 +7,14 @@
 //   K^-1 M = D^-1 M B^-1                       (spectrum_loss.m:55, since C M = I - B^-1)
 //   diag K^-1 = d^-1 - d^-2 diag(M B^-1 M')    (spectrum_loss.m:59)
 // let one block per spectrum produce every term with k x k work per pixel and no n x n object.
-// Per-spectrum partial gradients go to a [spectrum][...] buffer that a second kernel sums in
-// spectrum order (objective.m:41-57's loop order; deterministic, no atomics).
+// The dM sum over spectra is never formed per spectrum: with u_i = M_i B^-1 the spectrum's row is
+//   dM_i = -(t_i g' - w_i M_i B^-1)      (t = K^-1 y, w = d^-1, g = M'K^-1 y)
+// so sum_s dM_i = M_i X_i - h_i with X_i = sum_s w_s,i B_s^-1 and h_i = sum_s t_s,i g_s: one
+// pixel x spectrum x (B^-1 entries, g) GEMM on the f64 matrix cores (objective_accum_kernel) and a
+// k^2-per-pixel finish (objective_dM_kernel), in place of k P partials written and re-read per
+// spectrum (973 MB per evaluation at k = 20, 5,000 spectra).  The remaining per-spectrum partials
+// (d log omega, the scalars) are summed in 64 spectrum chunks, then the chunks in order.  Every sum
+// has a fixed order: results are deterministic (no atomics).
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -40,7 +46,11 @@ struct ObjArgs {
   const double* log_omega;   // [P] (objective.m:25-26), or nullptr when omega2 is given
   const double* omega2;      // [P] spectrum_loss's omega2 argument directly, or nullptr
   double c_0, tau_0, beta;
-  double* part_dM;           // [Q][k][P] per-spectrum dM (column-major per spectrum)
+  int32_t ldw;               // row stride of part_w / part_t (P rounded up to 32, zero tail)
+  int32_t nep, nxp;          // part_bg row length; offset of g in it (see obj_nxp)
+  double* part_w;            // [Q][ldw] D^-1 (0 = excluded pixel)
+  double* part_t;            // [Q][ldw] K^-1 y (0 = excluded pixel)
+  double* part_bg;           // [Q][nep] B^-1's upper triangle (packed rows), then g = M'K^-1 y at nxp
   double* part_dlo;          // [Q][P]
   double* part_s;            // [Q][kObjScalars]
   double* part_px;           // [Q][4][P] pass 1's pixel terms for pass 6: an, da0, da1, da2 (:62-73)
@@ -61,6 +71,13 @@ struct ObjTiles {
 };
 
 __host__ __device__ constexpr int obj_kb(int k) { return k <= 8 ? 8 : k <= 16 ? 16 : k <= 24 ? 24 : k <= 32 ? 32 : 64; }
+// part_bg row: B^-1's k (k + 1) / 2 upper entries, padded to a multiple of 64 (the GEMM's entry tile,
+// so no tile mixes the D^-1- and the K^-1 y-weighted segments), then g in a 64-entry tile
+__host__ __device__ constexpr int obj_nxp(int k) { return (k * (k + 1) / 2 + 63) / 64 * 64; }
+__host__ __device__ constexpr int obj_nep(int k) { return obj_nxp(k) + 64; }
+__host__ __device__ constexpr int obj_ldw(int64_t P) { return (int)((P + 31) / 32 * 32); }
+// packed index of B^-1[r][c], r <= c
+__device__ inline int obj_packed(int r, int c, int k) { return r * k - r * (r - 1) / 2 + (c - r); }
 __host__ __device__ constexpr int obj_kp(int kb) { return 4 * ((kb + 4) / 4); }
 __host__ __device__ constexpr int obj_ni(int kb) {
   return ((kb + 3) / 4 * ((kb + 4) / 4) - (kb + 3) / 4 * ((kb + 3) / 4 - 1) / 2 + 3) / 4;
@@ -398,19 +415,30 @@ void objective_spectrum_kernel(ObjArgs a) {
   }
   __syncthreads();
 
-  // pass 6: per pixel u = M_i B^-1 (K^-1 M = D^-1 M B^-1, :55), diag K^-1 = d^-1 - d^-2 diag(M B^-1 M')
-  // (:59), the dM row (:54-55), d log omega (:62) and the scalar gradient sums (:65-74).  For k > 32 the
-  // u rows come from the matrix cores (k = 50: 22.5 -> 19.7 ms per 5,000 spectra); up to 32 the VALU
-  // form below is faster (1.33 vs 1.64 ms at k = 20)
+  // the GEMM's operands: this spectrum's B^-1 (upper triangle) and g (objective_accum_kernel)
+  {
+    double* bg = a.part_bg + q * (int64_t)a.nep;
+    for (int e = tid; e < k * k; e += kObjThreads) {
+      const int r = e / k, c = e - r * k;
+      if (r <= c) bg[obj_packed(r, c, k)] = Bi[r * ld + c];
+    }
+    for (int c = tid; c < k; c += kObjThreads) bg[a.nxp + c] = g[c];
+  }
+
+  // pass 6: diag K^-1 = d^-1 - d^-2 diag(M B^-1 M') (:59), d log omega (:62) and the scalar gradient
+  // sums (:65-74) per pixel; w and K^-1 y to the GEMM's operand rows.  (The dM row -(t_i g' - w_i M_i B^-1)
+  // of :54-55 is summed over spectra by objective_accum_kernel / objective_dM_kernel instead.)  For k > 32
+  // u = M_i B^-1 comes from the matrix cores; up to 32, diag(M B^-1 M') on the VALU over B^-1's upper
+  // triangle
   double sc0 = 0.0, stau = 0.0, sbeta = 0.0;
-  double* dM = a.part_dM + q * (int64_t)k * P;
   double* dlo = a.part_dlo + q * (int64_t)P;
+  double* wout = a.part_w + q * (int64_t)a.ldw;
+  double* tout = a.part_t + q * (int64_t)a.ldw;
   if constexpr (KB > 32) {
     // U = M B^-1 with 16 pixels x 4 columns per accumulator: block b of v_mfma_f64_4x4x4_4b takes
     // pixels p16 + 4 b .. + 3 (A[i][kk] = B^-1[4 rc + kk][4 ct + i] at lane 16 kk + 4 b + i, the same for
     // the four blocks; B[kk][j] = M[p16 + 4 b + j][4 rc + kk] at lane 16 kk + 4 b + j), so D[i][j] =
-    // U[p16 + 4 b + j][4 ct + i] sits at lane 16 i + 4 b + j: each column's 16 pixels in 16 consecutive
-    // lanes (whole-line dM stores)
+    // U[p16 + 4 b + j][4 ct + i] sits at lane 16 i + 4 b + j
     constexpr int NCT = (KB + 3) / 4;
     const double* px = a.part_px + q * 4 * (int64_t)P;
     const int n16p = (P + 15) / 16;
@@ -432,14 +460,13 @@ void objective_spectrum_kernel(ObjArgs a) {
           const double av = (ar < k && ac < k) ? Bi[ar * ld + ac] : 0.0;
           acc = __builtin_amdgcn_mfma_f64_4x4x4f64(av, mrow[4 * rc + (lane >> 4)], acc, 0, 0, 0);
         }
-        if (pp < P && c < k) {
-          qd = fma(acc, mrow[c], qd);
-          dM[(int64_t)c * P + pp] = wi == 0.0 ? 0.0 : -(ti * g[c] - wi * acc);
-        }
+        if (pp < P && c < k) qd = fma(acc, mrow[c], qd);
       }
       qd += __shfl_xor(qd, 16);
       qd += __shfl_xor(qd, 32);
       if (ci == 0 && pp < P) {
+        wout[pp] = wi;
+        tout[pp] = ti;
         if (wi == 0.0) {
           dlo[pp] = 0.0;
         } else {
@@ -456,31 +483,28 @@ void objective_spectrum_kernel(ObjArgs a) {
     }
 
   } else {
-    // pass 6: per pixel u = M_i B^-1, diag K^-1, dM row, d log omega, scalar gradient sums
     for (int i = tid; i < P; i += kObjThreads) {
       const double wi = w[i];
+      const double ti = t[i];
+      wout[i] = wi;
+      tout[i] = ti;
       if (wi == 0.0) {
-        for (int r = 0; r < k; ++r) dM[(int64_t)r * P + i] = 0.0;
         dlo[i] = 0.0;
         continue;
       }
       double Mi[KB];
 #pragma unroll
       for (int r = 0; r < KB; ++r) Mi[r] = r < k ? a.M[(int64_t)r * P + i] : 0.0;
-      const double ti = t[i];
+      // M_i B^-1 M_i' over the upper triangle: sum_r M_r (B_rr M_r + 2 sum_{c > r} B_rc M_c)
       double qd = 0.0;
-      // c unrolled to the compile-time bound too: M_ic is Mi[c] from the registers (a runtime c re-read
-      // it from memory and waited on that load at every column)
 #pragma unroll
-      for (int c = 0; c < KB; ++c) {
-        if (c < k) {
-          double u = 0.0;
+      for (int r = 0; r < KB; ++r) {
+        if (r < k) {
+          double off = 0.0;
 #pragma unroll
-          for (int r = 0; r < KB; ++r)
-            if (r < k) u = fma(Mi[r], Bi[r * ld + c], u);
-          qd = fma(u, Mi[c], qd);
-          // dM = -(K^-1 y (K^-1 y' M) - K^-1 M), K^-1 M = D^-1 M B^-1 (:54-55)
-          dM[(int64_t)c * P + i] = -(ti * g[c] - wi * u);
+          for (int c = r + 1; c < KB; ++c)
+            if (c < k) off = fma(Mi[c], Bi[r * ld + c], off);
+          qd = fma(Mi[r], fma(Mi[r], Bi[r * ld + r], 2.0 * off), qd);
         }
       }
       const double dk = wi - wi * wi * qd;                          // diag K^-1 (:59)
@@ -493,7 +517,6 @@ void objective_spectrum_kernel(ObjArgs a) {
       const double da2 = px[3 * P];                                 // :73
       sbeta += -(ti * da2) * ti + dk * da2;                         // :74
     }
-
   }
   sc0 = block_sum(sc0, red);
   stau = block_sum(stau, red);
@@ -516,7 +539,7 @@ void objective_spectrum_kernel(ObjArgs a) {
 // use them, so a thread keeps that many loads in flight instead of one (the adds, and so the result,
 // stay in spectrum order)
 #ifndef GPDLA_OBJ_SUM_DEPTH
-#define GPDLA_OBJ_SUM_DEPTH 64                   // 16: 206 us per sum, 32: 177, 64: 149 (k = 20, 5,000 spectra)
+#define GPDLA_OBJ_SUM_DEPTH 64                   // (over all 5,000 spectra: 16: 206 us per sum, 32: 177, 64: 149)
 #endif
 constexpr int kSumDepth = GPDLA_OBJ_SUM_DEPTH;
 
@@ -540,6 +563,153 @@ __global__ __launch_bounds__(kSumThreads) void objective_sum_kernel(int64_t nq, 
   total[e] = acc;
 }
 
+// the same in kSumChunks spectrum chunks: out[c][e] = sum over chunk c (in spectrum order); the chunks
+// are then added in order by objective_sum_kernel.  A per-element walk over all spectra is one dependent
+// chain per thread (d log omega: 1,217 threads x 5,000 spectra); the chunks put 64 x more in flight
+constexpr int kSumChunks = 64;
+
+__global__ __launch_bounds__(kSumThreads) void objective_chunk_sum_kernel(int64_t nq, int64_t per,
+                                                                          const double* __restrict__ part,
+                                                                          double* __restrict__ out) {
+  const int64_t e = (int64_t)blockIdx.x * kSumThreads + threadIdx.x;
+  if (e >= per) return;
+  const int64_t c = blockIdx.y;
+  const int64_t q0 = nq * c / kSumChunks, q1 = nq * (c + 1) / kSumChunks;
+  constexpr int kD = 16;
+  double acc = 0.0;
+  int64_t q = q0;
+  for (; q + kD <= q1; q += kD) {
+    double v[kD];
+#pragma unroll
+    for (int j = 0; j < kD; ++j) v[j] = part[(q + j) * per + e];
+#pragma unroll
+    for (int j = 0; j < kD; ++j) acc += v[j];
+  }
+  for (; q < q1; ++q) acc += part[q * per + e];
+  out[c * per + e] = acc;
+}
+
+// [X | h] partials: part[c][i][e] = sum_{s in chunk c} A[s][i] BG[s][e], A = part_w for the B^-1 entries
+// (e < nxp), part_t for g's (e >= nxp).  8 spectrum chunks, chunk c on XCD c (blockIdx % 8: the
+// dispatcher's XCD): a chunk's operand rows (3.9 MB at k = 20, 5,000 spectra) stay in one L2.
+// Block = 4 waves on one 32-pixel x 64-entry tile, taking every 4th K step of 4 spectra; their sums are
+// added in wave order.  v_mfma_f64_4x4x4_4b (A[i][kk] at lane 16 kk + 4 b + i, B[kk][j] at
+// 16 kk + 4 b + j, D[i][j] at 16 i + 4 b + j): instruction (g, eg) is pixels p0 + 8 i + g x entries
+// e0 + 4 (4 b + j) + eg, so a lane's 8 A operands are 64 contiguous bytes of its operand row and its 4
+// B operands 32.
+struct ObjAccArgs {
+  int32_t ldw, nep, nxp;
+  int64_t nq;
+  const double* W;
+  const double* T;
+  const double* BG;
+  double* part;   // [8][ldw][nep]
+};
+
+__global__ __launch_bounds__(256) void objective_accum_kernel(ObjAccArgs a) {
+  __shared__ double sred[32 * 64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int kk = lane >> 4, i4 = lane & 3, j16 = lane & 15;
+  const int chunk = blockIdx.x & 7, tile = blockIdx.x >> 3;
+  const int n_et = a.nep / 64;
+  const int pt = tile / n_et, et = tile - pt * n_et;
+  const int p0 = 32 * pt, e0 = 64 * et;
+  const double* __restrict__ A = e0 >= a.nxp ? a.T : a.W;
+  const int64_t s0 = a.nq * chunk / 8, s1 = a.nq * (chunk + 1) / 8;
+  const int64_t nks = (s1 - s0 + 3) / 4;
+  double acc[8][4];
+#pragma unroll
+  for (int g = 0; g < 8; ++g)
+#pragma unroll
+    for (int eg = 0; eg < 4; ++eg) acc[g][eg] = 0.0;
+  auto load = [&](int64_t ks, double (&av)[8], double (&bv)[4]) {
+    const int64_t s = s0 + 4 * ks + kk;
+    if (ks < nks && s < s1) {
+      const double2* ap = reinterpret_cast<const double2*>(A + s * a.ldw + p0 + 8 * i4);
+      const double2* bp = reinterpret_cast<const double2*>(a.BG + s * a.nep + e0 + 4 * j16);
+#pragma unroll
+      for (int h = 0; h < 4; ++h) {
+        const double2 v = ap[h];
+        av[2 * h] = v.x;
+        av[2 * h + 1] = v.y;
+      }
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const double2 v = bp[h];
+        bv[2 * h] = v.x;
+        bv[2 * h + 1] = v.y;
+      }
+    } else {
+#pragma unroll
+      for (int h = 0; h < 8; ++h) av[h] = 0.0;
+#pragma unroll
+      for (int h = 0; h < 4; ++h) bv[h] = 0.0;
+    }
+  };
+  auto mma = [&](const double (&av)[8], const double (&bv)[4]) {
+#pragma unroll
+    for (int g = 0; g < 8; ++g)
+#pragma unroll
+      for (int eg = 0; eg < 4; ++eg) acc[g][eg] = __builtin_amdgcn_mfma_f64_4x4x4f64(av[g], bv[eg], acc[g][eg], 0, 0, 0);
+  };
+  double A0[8], B0[4], A1[8], B1[4];
+  load(wave, A0, B0);
+  for (int64_t ks = wave; ks < nks; ks += 8) {
+    load(ks + 4, A1, B1);
+    mma(A0, B0);
+    if (ks + 4 < nks) {
+      load(ks + 8, A0, B0);
+      mma(A1, B1);
+    }
+  }
+  for (int wv = 0; wv < 4; ++wv) {
+    if (wave == wv)
+#pragma unroll
+      for (int g = 0; g < 8; ++g)
+#pragma unroll
+        for (int eg = 0; eg < 4; ++eg) {
+          double& d = sred[(4 * g + eg) * 64 + lane];
+          d = (wv ? d : 0.0) + acc[g][eg];
+        }
+    __syncthreads();
+  }
+  // pixel p0 + px (px = 8 i + g), entry e0 + e (e = 4 (4 b + j) + eg): lane 16 i + 4 b + j of (g, eg)
+  double* out = a.part + ((int64_t)chunk * a.ldw + p0) * a.nep + e0;
+  for (int idx = threadIdx.x; idx < 32 * 64; idx += 256) {
+    const int px = idx >> 6, e = idx & 63;
+    out[(int64_t)px * a.nep + e] = sred[(4 * (px & 7) + (e & 3)) * 64 + 16 * (px >> 3) + (e >> 2)];
+  }
+}
+
+// dM_i += M_i X_i - h_i (the chunks' partials added in order), one block per pixel
+constexpr int kDMThreads = 128;
+constexpr int kObjMaxNep = obj_nxp(kObjMaxK) + 64;
+
+__global__ __launch_bounds__(kDMThreads) void objective_dM_kernel(int32_t P, int32_t k, int32_t ldw, int32_t nep,
+                                                                  int32_t nxp, const double* __restrict__ part,
+                                                                  const double* __restrict__ M,
+                                                                  double* __restrict__ total) {
+  __shared__ double xs[kObjMaxNep];
+  const int i = blockIdx.x;
+  for (int e = threadIdx.x; e < nep; e += kDMThreads) {
+    double v[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) v[c] = part[((int64_t)c * ldw + i) * nep + e];
+    double x = 0.0;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) x += v[c];
+    xs[e] = x;
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < k; c += kDMThreads) {
+    double u = 0.0;
+    for (int r = 0; r < k; ++r)
+      u = fma(M[(int64_t)r * P + i], xs[r <= c ? obj_packed(r, c, k) : obj_packed(c, r, k)], u);
+    // -(h - M X): -(t g' - w M B^-1) summed over the spectra (spectrum_loss.m:54-55, objective.m:47)
+    total[(int64_t)c * P + i] += -(xs[nxp + c] - u);
+  }
+}
+
 }  // namespace
 
 }  // namespace gpdla
@@ -557,7 +727,11 @@ struct gpdla_objective {
   double* noise = nullptr;
   bool owns_data = true;
   double* x = nullptr;        // [P k + P + 3]
-  double* part_dM = nullptr;  // [batch][k][P]
+  double* part_w = nullptr;   // [batch][ldw]
+  double* part_t = nullptr;   // [batch][ldw]
+  double* part_bg = nullptr;  // [batch][nep]
+  double* part_acc = nullptr; // [8][ldw][nep] objective_accum_kernel's chunk partials
+  double* part_chunk = nullptr;  // [kSumChunks][P + kObjScalars] chunk sums
   double* part_dlo = nullptr;
   double* part_s = nullptr;
   double* part_px = nullptr;  // [batch][4][P]
@@ -604,7 +778,12 @@ int obj_run(gpdla_objective* o, const double* dM_src, const double* lo_src, cons
     a.c_0 = c_0;
     a.tau_0 = tau_0;
     a.beta = beta;
-    a.part_dM = o->part_dM;
+    a.ldw = obj_ldw(P);
+    a.nep = obj_nep(k);
+    a.nxp = obj_nxp(k);
+    a.part_w = o->part_w;
+    a.part_t = o->part_t;
+    a.part_bg = o->part_bg;
     a.part_dlo = o->part_dlo;
     a.part_s = o->part_s;
     a.part_px = o->part_px;
@@ -624,14 +803,31 @@ int obj_run(gpdla_objective* o, const double* dM_src, const double* lo_src, cons
              : k <= 32 ? launch(objective_spectrum_kernel<32>)
                        : launch(objective_spectrum_kernel<64>);
     if (rc) return rc;
-    hipLaunchKernelGGL(objective_sum_kernel, dim3((unsigned)((per_dM + kSumThreads - 1) / kSumThreads)),
-                       dim3(kSumThreads), 0, o->stream,
-                       nq, per_dM, (const double*)o->part_dM, o->tot);
+    // dM: the pixel x spectrum GEMM's chunk partials, then M_i X_i - h_i per pixel
+    ObjAccArgs g{};
+    g.ldw = a.ldw;
+    g.nep = a.nep;
+    g.nxp = a.nxp;
+    g.nq = nq;
+    g.W = o->part_w;
+    g.T = o->part_t;
+    g.BG = o->part_bg;
+    g.part = o->part_acc;
+    const int64_t n_tiles = (int64_t)(a.ldw / 32) * (a.nep / 64);
+    hipLaunchKernelGGL(objective_accum_kernel, dim3((unsigned)(8 * n_tiles)), dim3(256), 0, o->stream, g);
+    hipLaunchKernelGGL(objective_dM_kernel, dim3((unsigned)P), dim3(kDMThreads), 0, o->stream, (int32_t)P, (int32_t)k,
+                       a.ldw, a.nep, a.nxp, (const double*)o->part_acc, dM_src, o->tot);
+    // d log omega and the scalars: spectrum chunks, then the chunks in order
+    double* dlo_chunks = o->part_chunk;
+    double* s_chunks = o->part_chunk + kSumChunks * P;
+    hipLaunchKernelGGL(objective_chunk_sum_kernel, dim3((unsigned)((P + kSumThreads - 1) / kSumThreads), kSumChunks),
+                       dim3(kSumThreads), 0, o->stream, nq, P, (const double*)o->part_dlo, dlo_chunks);
+    hipLaunchKernelGGL(objective_chunk_sum_kernel, dim3(1, kSumChunks), dim3(kSumThreads), 0, o->stream, nq,
+                       (int64_t)kObjScalars, (const double*)o->part_s, s_chunks);
     hipLaunchKernelGGL(objective_sum_kernel, dim3((unsigned)((P + kSumThreads - 1) / kSumThreads)), dim3(kSumThreads),
-                       0, o->stream,
-                       nq, P, (const double*)o->part_dlo, o->tot + per_dM);
-    hipLaunchKernelGGL(objective_sum_kernel, dim3(1), dim3(kSumThreads), 0, o->stream, nq, (int64_t)kObjScalars,
-                       (const double*)o->part_s, o->tot + per_dM + P);
+                       0, o->stream, (int64_t)kSumChunks, P, (const double*)dlo_chunks, o->tot + per_dM);
+    hipLaunchKernelGGL(objective_sum_kernel, dim3(1), dim3(kSumThreads), 0, o->stream, (int64_t)kSumChunks,
+                       (int64_t)kObjScalars, (const double*)s_chunks, o->tot + per_dM + P);
     HIP_TRY(hipGetLastError());
   }
   HIP_TRY(hipMemcpyAsync(host_tot, o->tot, (per_dM + P + kObjScalars) * sizeof(double), hipMemcpyDeviceToHost,
@@ -653,7 +849,11 @@ void gpdla_objective_destroy(gpdla_objective* o) {
     (void)hipFree(o->noise);
   }
   (void)hipFree(o->x);
-  (void)hipFree(o->part_dM);
+  (void)hipFree(o->part_w);
+  (void)hipFree(o->part_t);
+  (void)hipFree(o->part_bg);
+  (void)hipFree(o->part_acc);
+  (void)hipFree(o->part_chunk);
   (void)hipFree(o->part_dlo);
   (void)hipFree(o->part_s);
   (void)hipFree(o->part_px);
@@ -684,8 +884,9 @@ int gpdla_objective_create(int32_t device, int64_t num_quasars, int64_t num_pixe
   o->k = k;
   // spectra per launch: bounded by the partial-gradient buffers (<= 4 GiB; a DR9-sized training set in one)
   const int64_t per = (int64_t)(k + 1) * num_pixels + kObjScalars;
-  o->batch = std::max<int64_t>(1, std::min<int64_t>(std::max<int64_t>(num_quasars, 1),
-                                                    (1LL << 29) / (per + 4 * num_pixels)));
+  const int64_t ldw = obj_ldw(num_pixels), nep = obj_nep(k);
+  const int64_t per_q = 2 * ldw + nep + 5 * num_pixels + kObjScalars;   // w, t, [B^-1 | g], d log omega, px
+  o->batch = std::max<int64_t>(1, std::min<int64_t>(std::max<int64_t>(num_quasars, 1), (1LL << 29) / per_q));
   if (hipStreamCreateWithFlags(&o->stream, hipStreamNonBlocking) != hipSuccess)
     return obj_fail(o, set_error(GPDLA_EDEVICE, "hipStreamCreate failed"));
   const size_t data = (size_t)std::max<int64_t>(num_quasars, 1) * num_pixels * sizeof(double);
@@ -705,13 +906,22 @@ int gpdla_objective_create(int32_t device, int64_t num_quasars, int64_t num_pixe
       return obj_fail(o, set_error(GPDLA_EDEVICE, "objective data upload failed"));
   }
   if (hipMalloc(&o->x, (size_t)((k + 1) * num_pixels + 3) * sizeof(double)) != hipSuccess ||
-      hipMalloc(&o->part_dM, (size_t)o->batch * k * num_pixels * sizeof(double)) != hipSuccess ||
+      hipMalloc(&o->part_w, (size_t)o->batch * ldw * sizeof(double)) != hipSuccess ||
+      hipMalloc(&o->part_t, (size_t)o->batch * ldw * sizeof(double)) != hipSuccess ||
+      hipMalloc(&o->part_bg, (size_t)o->batch * nep * sizeof(double)) != hipSuccess ||
+      hipMalloc(&o->part_acc, (size_t)8 * ldw * nep * sizeof(double)) != hipSuccess ||
+      hipMalloc(&o->part_chunk, (size_t)kSumChunks * (num_pixels + kObjScalars) * sizeof(double)) != hipSuccess ||
       hipMalloc(&o->part_dlo, (size_t)o->batch * num_pixels * sizeof(double)) != hipSuccess ||
       hipMalloc(&o->part_s, (size_t)o->batch * kObjScalars * sizeof(double)) != hipSuccess ||
       hipMalloc(&o->part_px, (size_t)o->batch * 4 * num_pixels * sizeof(double)) != hipSuccess ||
       hipMalloc(&o->tot, (size_t)per * sizeof(double)) != hipSuccess ||
       hipMalloc(&o->mt, (size_t)(4 * ((num_pixels + 3) / 4)) * obj_kp(obj_kb(k)) * sizeof(double)) != hipSuccess)
     return obj_fail(o, set_error(GPDLA_ENOMEM, "objective workspace allocation failed"));
+  // the operand rows' padding (pixels past P, entries past B^-1's triangle and g) is never written: zero
+  if (hipMemset(o->part_w, 0, (size_t)o->batch * ldw * sizeof(double)) != hipSuccess ||
+      hipMemset(o->part_t, 0, (size_t)o->batch * ldw * sizeof(double)) != hipSuccess ||
+      hipMemset(o->part_bg, 0, (size_t)o->batch * nep * sizeof(double)) != hipSuccess)
+    return obj_fail(o, set_error(GPDLA_EDEVICE, "objective workspace initialisation failed"));
   *out = o;
   return GPDLA_OK;
 }
