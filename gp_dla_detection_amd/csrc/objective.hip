@@ -51,6 +51,7 @@ struct ObjArgs {
   double* part_w;            // [Q][ldw] D^-1 (0 = excluded pixel)
   double* part_t;            // [Q][ldw] K^-1 y (0 = excluded pixel)
   double* part_bg;           // [Q][nep] B^-1's upper triangle (packed rows), then g = M'K^-1 y at nxp
+  const double* part_gram;   // [Q][nep] objective_gram_kernel: B - I (packed like part_bg), then v = M'D^-1 y
   double* part_dlo;          // [Q][P]
   double* part_s;            // [Q][kObjScalars]
   double* part_px;           // [Q][4][P] pass 1's pixel terms for pass 6: an, da0, da1, da2 (:62-73)
@@ -129,30 +130,18 @@ __device__ inline PixelTerms pixel_terms(const ObjArgs& a, int i, double lya, do
   return p;
 }
 
-// KB: compile-time bound on k (register arrays, unrolled loops); the rank itself is a.k <= KB
-template <int KB>
-// k <= 24 at 3 waves per SIMD (the compiler otherwise spends AGPRs on the Gram pass and settles at 2:
-// 1.73 vs 1.33 ms per 5,000 spectra)
-__global__ __launch_bounds__(kObjThreads) __attribute__((amdgpu_waves_per_eu(KB <= 24 ? 3 : 1)))
-void objective_spectrum_kernel(ObjArgs a) {
-  extern __shared__ double sm[];
-  const int P = a.P, k = a.k;
+// pass 1, one block per spectrum: D^-1 and D^-1 y per pixel (to the GEMM operand rows part_w /
+// part_t), sum log d and n (to part_s[4], [6]), and the gradient's pixel terms for pass 6
+__global__ __launch_bounds__(kObjThreads) void objective_pixel_kernel(ObjArgs a) {
+  __shared__ double red[8];
+  const int P = a.P;
   const int tid = threadIdx.x;
   const int64_t q = blockIdx.x;
-  double* w = sm;              // [P] d^-1 (0 = excluded pixel)
-  double* t = w + P;           // [P] D^-1 y, then K^-1 y
-  double* B = t + P;           // [k][k + 1]: [B | v] (pass 2), then [B^-1 | C y] (pass 3)
-  double* s = B + 2 * k * k + k;   // [k] B^-1 M' D^-1 y (= C y); B spans [k][k + 1] <= 2 k^2 + k doubles
-  double* g = s + k;           // [k] (K^-1 y)' M
-  double* red = g + k;         // [8] block reductions
-  double* scr = red + 8;       // [NI][64] the matrix-core passes' wave sums
-  __shared__ int s_bad;
   const double* y = a.y + q * a.ld;
   const double* lya = a.lya_1pz + q * a.ld;
   const double* nv = a.noise + q * a.ld;
-  if (tid == 0) s_bad = 0;
-
-  // pass 1: D^-1 and D^-1 y per pixel; sum log d; n
+  double* wout = a.part_w + q * (int64_t)a.ldw;
+  double* tout = a.part_t + q * (int64_t)a.ldw;
   double logd = 0.0, cnt = 0.0;
   for (int i = tid; i < P; i += kObjThreads) {
     const double yi = y[i];
@@ -174,161 +163,153 @@ void objective_spectrum_kernel(ObjArgs a) {
       px[2 * P] = da1;
       px[3 * P] = da1 * log(lyi) * a.beta;                        // :73
     }
-    w[i] = wi;
-    t[i] = ti;
+    wout[i] = wi;
+    tout[i] = ti;
   }
   logd = block_sum(logd, red);
   cnt = block_sum(cnt, red);
+  if (tid == 0) {
+    a.part_s[q * kObjScalars + 4] = cnt;
+    a.part_s[q * kObjScalars + 6] = logd;
+  }
+}
 
-  // pass 2: [B | v] with B = M' (D^-1 M) + I (:41-42) and v = M' D^-1 y, k x (k + 1) row-major, on the
-  // f64 matrix cores (v_mfma_f64_4x4x4_4b:
-  // A[i][kk] at lane 16 kk + 4 b + i, B[kk][j] at 16 kk + 4 b + j, D[i][j] at 16 i + 4 b + j; block b of
-  // instruction m takes tile pair 4 m + b).  The waves take every 4th K step of 4 pixels, reading M from
-  // the pixel-major copy; their partial sums are added in wave order.
+// pass 2 for every spectrum at once: [B - I | v][s][e] = sum_i A[s][i] KR[i][e] with KR[i] = the
+// Khatri-Rao row (M_ir M_ic, r <= c, packed) then M_i at nxp (objective_kr_kernel), A = D^-1 for the
+// B entries and D^-1 y for v (spectrum_loss.m:41-42, :46).  Block = 4 waves on a 32-spectrum x
+// 64-entry tile, taking every 4th super-step of 16 pixels, added in wave order.  v_mfma_f64_4x4x4_4b
+// with the K index permuted inside a super-step: step q's K index kk is pixel pix0 + 4 kk + q (A and B
+// alike), so a lane's A operands for 4 steps are 32 contiguous bytes of an operand row; instruction
+// (g, eg) is spectra s0 + 8 i + g x entries e0 + 4 (4 b + j) + eg
+struct ObjGramArgs {
+  int32_t ldw, nep, nxp, nss;   // nss = ldw / 16 super-steps
+  const double* W;
+  const double* T;
+  const double* KR;             // [ldw][nep]
+  double* out;                  // [rows][nep]
+};
+
+__global__ __launch_bounds__(256) void objective_gram_kernel(ObjGramArgs a) {
+  __shared__ double sred[32 * 64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int kk = lane >> 4, i4 = lane & 3, j16 = lane & 15;
+  const int n_et = a.nep / 64;
+  const int st = blockIdx.x / n_et, et = blockIdx.x - st * n_et;
+  const int64_t s0 = 32 * (int64_t)st;
+  const int e0 = 64 * et;
+  const double* __restrict__ A = e0 >= a.nxp ? a.T : a.W;
+  double acc[8][4];
+#pragma unroll
+  for (int g = 0; g < 8; ++g)
+#pragma unroll
+    for (int eg = 0; eg < 4; ++eg) acc[g][eg] = 0.0;
+  for (int ss = wave; ss < a.nss; ss += 4) {
+    const int pix0 = 16 * ss;
+    double av[8][4];
+#pragma unroll
+    for (int g = 0; g < 8; ++g) {
+      const double2* ap = reinterpret_cast<const double2*>(A + (s0 + 8 * i4 + g) * a.ldw + pix0 + 4 * kk);
+      const double2 v0 = ap[0], v1 = ap[1];
+      av[g][0] = v0.x;
+      av[g][1] = v0.y;
+      av[g][2] = v1.x;
+      av[g][3] = v1.y;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const double2* bp = reinterpret_cast<const double2*>(a.KR + (int64_t)(pix0 + 4 * kk + q) * a.nep + e0 + 4 * j16);
+      const double2 b0 = bp[0], b1 = bp[1];
+      const double bv[4] = {b0.x, b0.y, b1.x, b1.y};
+#pragma unroll
+      for (int g = 0; g < 8; ++g)
+#pragma unroll
+        for (int eg = 0; eg < 4; ++eg) acc[g][eg] = __builtin_amdgcn_mfma_f64_4x4x4f64(av[g][q], bv[eg], acc[g][eg], 0, 0, 0);
+    }
+  }
+  for (int wv = 0; wv < 4; ++wv) {
+    if (wave == wv)
+#pragma unroll
+      for (int g = 0; g < 8; ++g)
+#pragma unroll
+        for (int eg = 0; eg < 4; ++eg) {
+          double& d = sred[(4 * g + eg) * 64 + lane];
+          d = (wv ? d : 0.0) + acc[g][eg];
+        }
+    __syncthreads();
+  }
+  double* out = a.out + s0 * a.nep + e0;
+  for (int idx = threadIdx.x; idx < 32 * 64; idx += 256) {
+    const int sp = idx >> 6, e = idx & 63;
+    out[(int64_t)sp * a.nep + e] = sred[(4 * (sp & 7) + (e & 3)) * 64 + 16 * (sp >> 3) + (e >> 2)];
+  }
+}
+
+// KR[i][e]: M_ir M_ic for packed e = (r, c), r <= c; M_ir at nxp + r; zero elsewhere (pixel rows past P,
+// the padding entries)
+__global__ __launch_bounds__(256) void objective_kr_kernel(const double* __restrict__ M, int32_t P, int32_t k,
+                                                           int32_t nxp, int32_t nep, int64_t rows,
+                                                           double* __restrict__ KR) {
+  const int64_t el = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (el >= rows * nep) return;
+  const int64_t i = el / nep;
+  const int e = (int)(el - i * nep);
+  double v = 0.0;
+  if (i < P) {
+    if (e >= nxp) {
+      if (e - nxp < k) v = M[(int64_t)(e - nxp) * P + i];
+    } else if (e < k * (k + 1) / 2) {
+      int r = 0, start = 0;
+      while (e >= start + (k - r)) {
+        start += k - r;
+        ++r;
+      }
+      const int c = r + (e - start);
+      v = M[(int64_t)r * P + i] * M[(int64_t)c * P + i];
+    }
+  }
+  KR[el] = v;
+}
+
+// passes 3-6, one block per spectrum.  KB: compile-time bound on k (register arrays, unrolled loops);
+// the rank itself is a.k <= KB
+template <int KB>
+__global__ __launch_bounds__(kObjThreads) __attribute__((amdgpu_waves_per_eu(KB <= 24 ? 3 : 1)))
+void objective_spectrum_kernel(ObjArgs a) {
+  extern __shared__ double sm[];
+  const int P = a.P, k = a.k;
+  const int tid = threadIdx.x;
+  const int64_t q = blockIdx.x;
+  double* w = sm;              // [P] d^-1 (0 = excluded pixel)
+  double* t = w + P;           // [P] D^-1 y, then K^-1 y
+  double* B = t + P;           // [k][k + 1]: [B | v], then [B^-1 | C y] (pass 3)
+  double* s = B + 2 * k * k + k;   // [k] B^-1 M' D^-1 y (= C y); B spans [k][k + 1] <= 2 k^2 + k doubles
+  double* g = s + k;           // [k] (K^-1 y)' M
+  double* red = g + k;         // [8] block reductions
+  double* scr = red + 8;       // [NI][64] the matrix-core passes' wave sums
+  __shared__ int s_bad;
+  const double* y = a.y + q * a.ld;
+  if (tid == 0) s_bad = 0;
+
+  // pass 1's w, D^-1 y, sum log d, n (objective_pixel_kernel); [B - I | v] (objective_gram_kernel)
+  {
+    const double* win = a.part_w + q * (int64_t)a.ldw;
+    const double* tin = a.part_t + q * (int64_t)a.ldw;
+    for (int i = tid; i < P; i += kObjThreads) {
+      w[i] = win[i];
+      t[i] = tin[i];
+    }
+    const double* gr = a.part_gram + q * (int64_t)a.nep;
+    for (int e = tid; e < k * k; e += kObjThreads) {
+      const int r = e / k, c = e - r * k;
+      B[r * (k + 1) + c] = gr[r <= c ? obj_packed(r, c, k) : obj_packed(c, r, k)] + (r == c ? 1.0 : 0.0);
+    }
+    for (int r = tid; r < k; r += kObjThreads) B[r * (k + 1) + k] = gr[a.nxp + r];
+  }
+  const double cnt = a.part_s[q * kObjScalars + 4], logd = a.part_s[q * kObjScalars + 6];
   using TL = ObjTiles<KB>;
   const int lane = tid & 63, wave = tid >> 6;
   const int kk = lane >> 4, bl = (lane >> 2) & 3, li = lane & 3;
   const int nks = (P + 3) / 4;
-  if constexpr (TL::NP <= 28) {
-    // k <= 24: the four blocks of an instruction split 16 pixels 4 ways and share one tile pair, so a
-    // lane's operands are its own pixel's row at columns 4 t + i of every column tile t (NTc loads per
-    // 16 pixels; each B operand w M (or D^-1 y) formed once per tile); the blocks' partial tiles are
-    // summed with two lane exchanges at the end
-    const int p_lane = 4 * bl + kk;                                 // pixel within the 16
-    double acc[TL::NP];
-#pragma unroll
-    for (int m = 0; m < TL::NP; ++m) acc[m] = 0.0;
-    auto load = [&](int s16, double (&v)[TL::NTc], double& wv, double& tv) {
-      const int pp = 16 * s16 + p_lane;
-      const bool in = pp < P;
-      const double* row = a.MT + (int64_t)(in ? pp : 0) * TL::KP + li;
-#pragma unroll
-      for (int c = 0; c < TL::NTc; ++c) v[c] = in ? row[4 * c] : 0.0;
-      wv = in ? w[pp] : 0.0;
-      tv = in ? t[pp] : 0.0;
-    };
-    auto mma = [&](const double (&v)[TL::NTc], double wv, double tv) {
-      double bw[TL::NTc];
-#pragma unroll
-      for (int ct = 0; ct < TL::NTc; ++ct) bw[ct] = fma(v[ct], wv, 4 * ct + li == k ? tv : 0.0);
-      int m = 0;
-#pragma unroll
-      for (int rt = 0; rt < TL::NTr; ++rt)
-#pragma unroll
-        for (int ct = rt; ct < TL::NTc; ++ct, ++m)
-          acc[m] = __builtin_amdgcn_mfma_f64_4x4x4f64(v[rt], bw[ct], acc[m], 0, 0, 0);
-    };
-    const int n16 = (P + 15) / 16;
-    double v0[TL::NTc], v1[TL::NTc], w0, t0, w1, t1;
-    load(wave, v0, w0, t0);
-    for (int s16 = wave; s16 < n16; s16 += 8) {
-      load(s16 + 4, v1, w1, t1);
-      mma(v0, w0, t0);
-      if (s16 + 4 < n16) {
-        load(s16 + 8, v0, w0, t0);
-        mma(v1, w1, t1);
-      }
-    }
-#pragma unroll
-    for (int m = 0; m < TL::NP; ++m) {
-      acc[m] += __shfl_xor(acc[m], 4);
-      acc[m] += __shfl_xor(acc[m], 8);
-    }
-    // lanes 16 i + j (b = 0) hold D[i][j] of every pair: scr[pair][i][j], added in wave order
-    for (int wv = 0; wv < 4; ++wv) {
-      if (wave == wv && bl == 0)
-#pragma unroll
-        for (int m = 0; m < TL::NP; ++m) {
-          double& d = scr[m * 16 + (lane >> 4) * 4 + li];
-          d = (wv ? d : 0.0) + acc[m];
-        }
-      __syncthreads();
-    }
-    for (int idx = tid; idx < TL::NP * 16; idx += kObjThreads) {
-      int rt, ct;
-      obj_pair(idx >> 4, TL::NTc, rt, ct);
-      const int r = 4 * rt + ((idx >> 2) & 3), c = 4 * ct + (idx & 3);
-      if (r >= k) continue;
-      if (c < k && r <= c) {
-        const double val = scr[idx] + (r == c ? 1.0 : 0.0);
-        B[r * (k + 1) + c] = val;
-        B[c * (k + 1) + r] = val;
-      } else if (c == k) {
-        B[r * (k + 1) + k] = scr[idx];                           // v, the augmented column
-      }
-    }
-  } else {
-    int aoff[TL::NI], boff[TL::NI];
-    bool live[TL::NI];
-#pragma unroll
-    for (int m = 0; m < TL::NI; ++m) {
-      const int pair = 4 * m + bl;
-      live[m] = pair < TL::NP;
-      int rt, ct;
-      obj_pair(live[m] ? pair : 0, TL::NTc, rt, ct);
-      aoff[m] = 4 * rt + li;
-      boff[m] = 4 * ct + li;
-    }
-    double acc[TL::NI];
-#pragma unroll
-    for (int m = 0; m < TL::NI; ++m) acc[m] = 0.0;
-    // the operands of K step ks (zeros past the last one), loaded one step ahead of the MFMAs that use
-    // them (two register sets in turn)
-    auto load = [&](int ks, double (&av)[TL::NI], double (&bv)[TL::NI]) {
-      const bool in = ks < nks;
-      const int pp = 4 * ks + kk;
-      const double* row = a.MT + (int64_t)(in ? pp : 0) * TL::KP;
-      const double wv = (in && pp < P) ? w[pp] : 0.0, tv = (in && pp < P) ? t[pp] : 0.0;
-#pragma unroll
-      for (int m = 0; m < TL::NI; ++m) {
-        av[m] = (live[m] && in) ? row[aoff[m]] : 0.0;
-        bv[m] = fma(row[boff[m]], wv, boff[m] == k ? tv : 0.0);    // column k: D^-1 y
-      }
-    };
-    auto mma = [&](const double (&av)[TL::NI], const double (&bv)[TL::NI]) {
-#pragma unroll
-      for (int m = 0; m < TL::NI; ++m) acc[m] = __builtin_amdgcn_mfma_f64_4x4x4f64(av[m], bv[m], acc[m], 0, 0, 0);
-    };
-    double A0[TL::NI], B0[TL::NI];
-    if constexpr (TL::NI <= 16) {
-      double A1[TL::NI], B1[TL::NI];
-      load(wave, A0, B0);
-      for (int ks = wave; ks < nks; ks += 8) {
-        load(ks + 4, A1, B1);
-        mma(A0, B0);
-        if (ks + 4 < nks) {
-          load(ks + 8, A0, B0);
-          mma(A1, B1);
-        }
-      }
-    } else {  // (k > 32: two sets of 38 would spill)
-      for (int ks = wave; ks < nks; ks += 4) {
-        load(ks, A0, B0);
-        mma(A0, B0);
-      }
-    }
-    for (int wv = 0; wv < 4; ++wv) {
-      if (wave == wv)
-#pragma unroll
-        for (int m = 0; m < TL::NI; ++m) scr[m * 64 + lane] = (wv ? scr[m * 64 + lane] : 0.0) + acc[m];
-      __syncthreads();
-    }
-    for (int idx = tid; idx < TL::NI * 64; idx += kObjThreads) {
-      const int L = idx & 63, pair = 4 * (idx >> 6) + ((L >> 2) & 3);
-      if (pair >= TL::NP) continue;
-      int rt, ct;
-      obj_pair(pair, TL::NTc, rt, ct);
-      const int r = 4 * rt + (L >> 4), c = 4 * ct + (L & 3);
-      if (r >= k) continue;
-      if (c < k && r <= c) {
-        const double val = scr[idx] + (r == c ? 1.0 : 0.0);
-        B[r * (k + 1) + c] = val;
-        B[c * (k + 1) + r] = val;
-      } else if (c == k) {
-        B[r * (k + 1) + k] = scr[idx];                           // v, the augmented column
-      }
-    }
-  }
   __syncthreads();
 
   // pass 3: Gauss-Jordan on [B | v] by the whole block (B is symmetric positive definite with
@@ -432,8 +413,7 @@ void objective_spectrum_kernel(ObjArgs a) {
   // triangle
   double sc0 = 0.0, stau = 0.0, sbeta = 0.0;
   double* dlo = a.part_dlo + q * (int64_t)P;
-  double* wout = a.part_w + q * (int64_t)a.ldw;
-  double* tout = a.part_t + q * (int64_t)a.ldw;
+  double* tout = a.part_t + q * (int64_t)a.ldw;   // D^-1 y -> K^-1 y, the dM GEMM's operand
   if constexpr (KB > 32) {
     // U = M B^-1 with 16 pixels x 4 columns per accumulator: block b of v_mfma_f64_4x4x4_4b takes
     // pixels p16 + 4 b .. + 3 (A[i][kk] = B^-1[4 rc + kk][4 ct + i] at lane 16 kk + 4 b + i, the same for
@@ -465,7 +445,6 @@ void objective_spectrum_kernel(ObjArgs a) {
       qd += __shfl_xor(qd, 16);
       qd += __shfl_xor(qd, 32);
       if (ci == 0 && pp < P) {
-        wout[pp] = wi;
         tout[pp] = ti;
         if (wi == 0.0) {
           dlo[pp] = 0.0;
@@ -486,7 +465,6 @@ void objective_spectrum_kernel(ObjArgs a) {
     for (int i = tid; i < P; i += kObjThreads) {
       const double wi = w[i];
       const double ti = t[i];
-      wout[i] = wi;
       tout[i] = ti;
       if (wi == 0.0) {
         dlo[i] = 0.0;
@@ -529,7 +507,7 @@ void objective_spectrum_kernel(ObjArgs a) {
     o[3] = sbeta;
     o[4] = cnt;
     o[5] = s_bad ? 1.0 : 0.0;
-    o[6] = 0.0;
+    o[6] = 0.0;   // (objective_pixel_kernel's sum log d)
     o[7] = 0.0;
   }
 }
@@ -730,6 +708,9 @@ struct gpdla_objective {
   double* part_w = nullptr;   // [batch][ldw]
   double* part_t = nullptr;   // [batch][ldw]
   double* part_bg = nullptr;  // [batch][nep]
+  double* part_gram = nullptr;  // [rows][nep] objective_gram_kernel's [B - I | v]
+  double* kr = nullptr;       // [ldw][nep] the Khatri-Rao panel of M
+  int64_t rows = 0;           // batch rounded up to the Gram's 32-spectrum tiles
   double* part_acc = nullptr; // [8][ldw][nep] objective_accum_kernel's chunk partials
   double* part_chunk = nullptr;  // [kSumChunks][P + kObjScalars] chunk sums
   double* part_dlo = nullptr;
@@ -762,6 +743,9 @@ int obj_run(gpdla_objective* o, const double* dM_src, const double* lo_src, cons
   const int64_t mt_rows = 4 * ((P + 3) / 4);
   hipLaunchKernelGGL(objective_mt_kernel, dim3((unsigned)((mt_rows * KP + 255) / 256)), dim3(256), 0, o->stream,
                      dM_src, (int32_t)P, (int32_t)k, (int32_t)KP, mt_rows, o->mt);
+  const int ldw = obj_ldw(P), nep = obj_nep(k), nxp = obj_nxp(k);
+  hipLaunchKernelGGL(objective_kr_kernel, dim3((unsigned)(((int64_t)ldw * nep + 255) / 256)), dim3(256), 0, o->stream,
+                     dM_src, (int32_t)P, (int32_t)k, (int32_t)nxp, (int32_t)nep, (int64_t)ldw, o->kr);
   for (int64_t q0 = 0; q0 < o->Q; q0 += o->batch) {
     const int64_t nq = std::min(o->batch, o->Q - q0);
     ObjArgs a{};
@@ -784,10 +768,22 @@ int obj_run(gpdla_objective* o, const double* dM_src, const double* lo_src, cons
     a.part_w = o->part_w;
     a.part_t = o->part_t;
     a.part_bg = o->part_bg;
+    a.part_gram = o->part_gram;
     a.part_dlo = o->part_dlo;
     a.part_s = o->part_s;
     a.part_px = o->part_px;
     const dim3 grid((unsigned)nq), blk(kObjThreads);
+    hipLaunchKernelGGL(objective_pixel_kernel, grid, blk, 0, o->stream, a);
+    ObjGramArgs gm{};
+    gm.ldw = ldw;
+    gm.nep = nep;
+    gm.nxp = nxp;
+    gm.nss = ldw / 16;
+    gm.W = o->part_w;
+    gm.T = o->part_t;
+    gm.KR = o->kr;
+    gm.out = o->part_gram;
+    hipLaunchKernelGGL(objective_gram_kernel, dim3((unsigned)((nq + 31) / 32 * (nep / 64))), dim3(256), 0, o->stream, gm);
     // dynamic LDS above 64 KiB (long rest grids with high rank) must be opted into per kernel
     auto launch = [&](auto kern) -> int {
       if (shm > 65536)
@@ -852,6 +848,8 @@ void gpdla_objective_destroy(gpdla_objective* o) {
   (void)hipFree(o->part_w);
   (void)hipFree(o->part_t);
   (void)hipFree(o->part_bg);
+  (void)hipFree(o->part_gram);
+  (void)hipFree(o->kr);
   (void)hipFree(o->part_acc);
   (void)hipFree(o->part_chunk);
   (void)hipFree(o->part_dlo);
@@ -885,8 +883,9 @@ int gpdla_objective_create(int32_t device, int64_t num_quasars, int64_t num_pixe
   // spectra per launch: bounded by the partial-gradient buffers (<= 4 GiB; a DR9-sized training set in one)
   const int64_t per = (int64_t)(k + 1) * num_pixels + kObjScalars;
   const int64_t ldw = obj_ldw(num_pixels), nep = obj_nep(k);
-  const int64_t per_q = 2 * ldw + nep + 5 * num_pixels + kObjScalars;   // w, t, [B^-1 | g], d log omega, px
+  const int64_t per_q = 2 * ldw + 2 * nep + 5 * num_pixels + kObjScalars;   // w, t, Gram, [B^-1 | g], d log omega, px
   o->batch = std::max<int64_t>(1, std::min<int64_t>(std::max<int64_t>(num_quasars, 1), (1LL << 29) / per_q));
+  o->rows = (o->batch + 31) / 32 * 32;
   if (hipStreamCreateWithFlags(&o->stream, hipStreamNonBlocking) != hipSuccess)
     return obj_fail(o, set_error(GPDLA_EDEVICE, "hipStreamCreate failed"));
   const size_t data = (size_t)std::max<int64_t>(num_quasars, 1) * num_pixels * sizeof(double);
@@ -906,8 +905,10 @@ int gpdla_objective_create(int32_t device, int64_t num_quasars, int64_t num_pixe
       return obj_fail(o, set_error(GPDLA_EDEVICE, "objective data upload failed"));
   }
   if (hipMalloc(&o->x, (size_t)((k + 1) * num_pixels + 3) * sizeof(double)) != hipSuccess ||
-      hipMalloc(&o->part_w, (size_t)o->batch * ldw * sizeof(double)) != hipSuccess ||
-      hipMalloc(&o->part_t, (size_t)o->batch * ldw * sizeof(double)) != hipSuccess ||
+      hipMalloc(&o->part_w, (size_t)o->rows * ldw * sizeof(double)) != hipSuccess ||
+      hipMalloc(&o->part_t, (size_t)o->rows * ldw * sizeof(double)) != hipSuccess ||
+      hipMalloc(&o->part_gram, (size_t)o->rows * nep * sizeof(double)) != hipSuccess ||
+      hipMalloc(&o->kr, (size_t)ldw * nep * sizeof(double)) != hipSuccess ||
       hipMalloc(&o->part_bg, (size_t)o->batch * nep * sizeof(double)) != hipSuccess ||
       hipMalloc(&o->part_acc, (size_t)8 * ldw * nep * sizeof(double)) != hipSuccess ||
       hipMalloc(&o->part_chunk, (size_t)kSumChunks * (num_pixels + kObjScalars) * sizeof(double)) != hipSuccess ||
@@ -918,8 +919,8 @@ int gpdla_objective_create(int32_t device, int64_t num_quasars, int64_t num_pixe
       hipMalloc(&o->mt, (size_t)(4 * ((num_pixels + 3) / 4)) * obj_kp(obj_kb(k)) * sizeof(double)) != hipSuccess)
     return obj_fail(o, set_error(GPDLA_ENOMEM, "objective workspace allocation failed"));
   // the operand rows' padding (pixels past P, entries past B^-1's triangle and g) is never written: zero
-  if (hipMemset(o->part_w, 0, (size_t)o->batch * ldw * sizeof(double)) != hipSuccess ||
-      hipMemset(o->part_t, 0, (size_t)o->batch * ldw * sizeof(double)) != hipSuccess ||
+  if (hipMemset(o->part_w, 0, (size_t)o->rows * ldw * sizeof(double)) != hipSuccess ||
+      hipMemset(o->part_t, 0, (size_t)o->rows * ldw * sizeof(double)) != hipSuccess ||
       hipMemset(o->part_bg, 0, (size_t)o->batch * nep * sizeof(double)) != hipSuccess)
     return obj_fail(o, set_error(GPDLA_EDEVICE, "objective workspace initialisation failed"));
   *out = o;
