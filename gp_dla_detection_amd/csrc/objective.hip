@@ -57,18 +57,12 @@ struct ObjArgs {
   double* part_px;           // [Q][4][P] pass 1's pixel terms for pass 6: an, da0, da1, da2 (:62-73)
 };
 
-// The tile plan of the matrix-core passes for a compile-time rank bound KB: [B - I | v] = M' [D^-1 M |
-// D^-1 y] as the upper 4x4 tile pairs (row tile rt of M', column tile ct of the right factor, whose
-// column k is D^-1 y), four pairs per v_mfma_f64_4x4x4_4b; and g = M' K^-1 y, four row tiles per
-// instruction.
+// The 4x4 tiles of pass 6's matrix-core U = M B^-1 (k > 32) for a compile-time rank bound KB
 template <int KB>
 struct ObjTiles {
   static constexpr int NTr = (KB + 3) / 4;
   static constexpr int NTc = (KB + 4) / 4;
   static constexpr int KP = 4 * NTc;                              // MT row length (doubles)
-  static constexpr int NP = NTr * NTc - NTr * (NTr - 1) / 2;      // pairs rt <= ct
-  static constexpr int NI = (NP + 3) / 4;
-  static constexpr int NG = (NTr + 3) / 4;
 };
 
 __host__ __device__ constexpr int obj_kb(int k) { return k <= 8 ? 8 : k <= 16 ? 16 : k <= 24 ? 24 : k <= 32 ? 32 : 64; }
@@ -80,19 +74,6 @@ __host__ __device__ constexpr int obj_ldw(int64_t P) { return (int)((P + 31) / 3
 // packed index of B^-1[r][c], r <= c
 __device__ inline int obj_packed(int r, int c, int k) { return r * k - r * (r - 1) / 2 + (c - r); }
 __host__ __device__ constexpr int obj_kp(int kb) { return 4 * ((kb + 4) / 4); }
-__host__ __device__ constexpr int obj_ni(int kb) {
-  return ((kb + 3) / 4 * ((kb + 4) / 4) - (kb + 3) / 4 * ((kb + 3) / 4 - 1) / 2 + 3) / 4;
-}
-
-// pair index (rt-major over rt <= ct < ntc) -> (rt, ct)
-__device__ inline void obj_pair(int idx, int ntc, int& rt, int& ct) {
-  rt = 0;
-  while (idx >= ntc - rt) {
-    idx -= ntc - rt;
-    ++rt;
-  }
-  ct = rt + idx;
-}
 
 // MT[p][r] = M[r][p] for p < P, r < k; zero elsewhere (the padding rows / columns the tiles read)
 __global__ __launch_bounds__(256) void objective_mt_kernel(const double* __restrict__ M, int32_t P, int32_t k,
@@ -183,6 +164,7 @@ __global__ __launch_bounds__(kObjThreads) void objective_pixel_kernel(ObjArgs a)
 // (g, eg) is spectra s0 + 8 i + g x entries e0 + 4 (4 b + j) + eg
 struct ObjGramArgs {
   int32_t ldw, nep, nxp, nss;   // nss = ldw / 16 super-steps
+  int32_t et0, n_et;            // the entry tiles launched: et0 .. et0 + n_et - 1
   const double* W;
   const double* T;
   const double* KR;             // [ldw][nep]
@@ -193,8 +175,7 @@ __global__ __launch_bounds__(256) void objective_gram_kernel(ObjGramArgs a) {
   __shared__ double sred[32 * 64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int kk = lane >> 4, i4 = lane & 3, j16 = lane & 15;
-  const int n_et = a.nep / 64;
-  const int st = blockIdx.x / n_et, et = blockIdx.x - st * n_et;
+  const int st = blockIdx.x / a.n_et, et = a.et0 + (blockIdx.x - st * a.n_et);
   const int64_t s0 = 32 * (int64_t)st;
   const int e0 = 64 * et;
   const double* __restrict__ A = e0 >= a.nxp ? a.T : a.W;
@@ -283,9 +264,7 @@ void objective_spectrum_kernel(ObjArgs a) {
   double* t = w + P;           // [P] D^-1 y, then K^-1 y
   double* B = t + P;           // [k][k + 1]: [B | v], then [B^-1 | C y] (pass 3)
   double* s = B + 2 * k * k + k;   // [k] B^-1 M' D^-1 y (= C y); B spans [k][k + 1] <= 2 k^2 + k doubles
-  double* g = s + k;           // [k] (K^-1 y)' M
-  double* red = g + k;         // [8] block reductions
-  double* scr = red + 8;       // [NI][64] the matrix-core passes' wave sums
+  double* red = s + 2 * k;     // [8] block reductions (after s and a spare [k])
   __shared__ int s_bad;
   const double* y = a.y + q * a.ld;
   if (tid == 0) s_bad = 0;
@@ -308,8 +287,6 @@ void objective_spectrum_kernel(ObjArgs a) {
   const double cnt = a.part_s[q * kObjScalars + 4], logd = a.part_s[q * kObjScalars + 6];
   using TL = ObjTiles<KB>;
   const int lane = tid & 63, wave = tid >> 6;
-  const int kk = lane >> 4, bl = (lane >> 2) & 3, li = lane & 3;
-  const int nks = (P + 3) / 4;
   __syncthreads();
 
   // pass 3: Gauss-Jordan on [B | v] by the whole block (B is symmetric positive definite with
@@ -346,7 +323,9 @@ void objective_spectrum_kernel(ObjArgs a) {
   __syncthreads();
   const double* Bi = B;
 
-  // pass 4: K^-1 y = D^-1 y - D^-1 M (C y) (:48); y' K^-1 y
+  // pass 4: K^-1 y = D^-1 y - D^-1 M (C y) (:48), in place over D^-1 y in part_t (the operand of g's and
+  // the dM GEMMs; excluded pixels stay 0); y' K^-1 y
+  double* tout = a.part_t + q * (int64_t)a.ldw;
   double yky = 0.0;
   for (int i = tid; i < P; i += kObjThreads) {
     const double wi = w[i];
@@ -361,49 +340,20 @@ void objective_spectrum_kernel(ObjArgs a) {
         if (r < k) ms = fma(Mi[r] * wi, s[r], ms);
       const double ti = t[i] - ms;
       t[i] = ti;
+      tout[i] = ti;
       yky = fma(y[i], ti, yky);
     }
   }
   yky = block_sum(yky, red);  // (its barriers also publish t)
 
-  // pass 5: g = (K^-1 y)' M (:55) on the matrix cores: block b of instruction m takes row tile 4 m + b,
-  // with K^-1 y in column 0 of the B operand
-  {
-    double acc[TL::NG];
-#pragma unroll
-    for (int m = 0; m < TL::NG; ++m) acc[m] = 0.0;
-    for (int ks = wave; ks < nks; ks += 4) {
-      const int pp = 4 * ks + kk;
-      const double* row = a.MT + (int64_t)pp * TL::KP;
-      const double bv = (li == 0 && pp < P) ? t[pp] : 0.0;
-#pragma unroll
-      for (int m = 0; m < TL::NG; ++m) {
-        const int rt = 4 * m + bl;
-        const double av = rt < TL::NTr ? row[4 * rt + li] : 0.0;
-        acc[m] = __builtin_amdgcn_mfma_f64_4x4x4f64(av, bv, acc[m], 0, 0, 0);
-      }
-    }
-    for (int wv = 0; wv < 4; ++wv) {
-      if (wave == wv)
-#pragma unroll
-        for (int m = 0; m < TL::NG; ++m) scr[m * 64 + lane] = (wv ? scr[m * 64 + lane] : 0.0) + acc[m];
-      __syncthreads();
-    }
-    for (int idx = tid; idx < TL::NG * 64; idx += kObjThreads) {
-      const int L = idx & 63, r = 4 * (4 * (idx >> 6) + ((L >> 2) & 3)) + (L >> 4);
-      if ((L & 3) == 0 && r < k) g[r] = scr[idx];
-    }
-  }
-  __syncthreads();
-
-  // the GEMM's operands: this spectrum's B^-1 (upper triangle) and g (objective_accum_kernel)
+  // the dM GEMM's operand: this spectrum's B^-1 (upper triangle; g = M'K^-1 y (:55) lands at nxp from
+  // objective_gram_kernel's second launch on K^-1 y)
   {
     double* bg = a.part_bg + q * (int64_t)a.nep;
     for (int e = tid; e < k * k; e += kObjThreads) {
       const int r = e / k, c = e - r * k;
       if (r <= c) bg[obj_packed(r, c, k)] = Bi[r * ld + c];
     }
-    for (int c = tid; c < k; c += kObjThreads) bg[a.nxp + c] = g[c];
   }
 
   // pass 6: diag K^-1 = d^-1 - d^-2 diag(M B^-1 M') (:59), d log omega (:62) and the scalar gradient
@@ -413,7 +363,6 @@ void objective_spectrum_kernel(ObjArgs a) {
   // triangle
   double sc0 = 0.0, stau = 0.0, sbeta = 0.0;
   double* dlo = a.part_dlo + q * (int64_t)P;
-  double* tout = a.part_t + q * (int64_t)a.ldw;   // D^-1 y -> K^-1 y, the dM GEMM's operand
   if constexpr (KB > 32) {
     // U = M B^-1 with 16 pixels x 4 columns per accumulator: block b of v_mfma_f64_4x4x4_4b takes
     // pixels p16 + 4 b .. + 3 (A[i][kk] = B^-1[4 rc + kk][4 ct + i] at lane 16 kk + 4 b + i, the same for
@@ -445,7 +394,6 @@ void objective_spectrum_kernel(ObjArgs a) {
       qd += __shfl_xor(qd, 16);
       qd += __shfl_xor(qd, 32);
       if (ci == 0 && pp < P) {
-        tout[pp] = ti;
         if (wi == 0.0) {
           dlo[pp] = 0.0;
         } else {
@@ -465,7 +413,6 @@ void objective_spectrum_kernel(ObjArgs a) {
     for (int i = tid; i < P; i += kObjThreads) {
       const double wi = w[i];
       const double ti = t[i];
-      tout[i] = ti;
       if (wi == 0.0) {
         dlo[i] = 0.0;
         continue;
@@ -707,7 +654,7 @@ struct gpdla_objective {
   double* x = nullptr;        // [P k + P + 3]
   double* part_w = nullptr;   // [batch][ldw]
   double* part_t = nullptr;   // [batch][ldw]
-  double* part_bg = nullptr;  // [batch][nep]
+  double* part_bg = nullptr;  // [rows][nep] (g's tile is written for whole 32-spectrum tiles)
   double* part_gram = nullptr;  // [rows][nep] objective_gram_kernel's [B - I | v]
   double* kr = nullptr;       // [ldw][nep] the Khatri-Rao panel of M
   int64_t rows = 0;           // batch rounded up to the Gram's 32-spectrum tiles
@@ -728,7 +675,7 @@ int obj_fail(gpdla_objective* o, int rc) {
 }
 
 size_t obj_shared_bytes(int64_t P, int k) {
-  return (size_t)(2 * P + 2 * k * k + 3 * k + 8 + 64 * obj_ni(obj_kb(k))) * sizeof(double);
+  return (size_t)(2 * P + 2 * k * k + 3 * k + 8) * sizeof(double);
 }
 
 // one pass over all spectra with the M / log omega / (c_0, tau_0, beta) already in place
@@ -783,7 +730,9 @@ int obj_run(gpdla_objective* o, const double* dM_src, const double* lo_src, cons
     gm.T = o->part_t;
     gm.KR = o->kr;
     gm.out = o->part_gram;
-    hipLaunchKernelGGL(objective_gram_kernel, dim3((unsigned)((nq + 31) / 32 * (nep / 64))), dim3(256), 0, o->stream, gm);
+    gm.et0 = 0;
+    gm.n_et = nep / 64;
+    hipLaunchKernelGGL(objective_gram_kernel, dim3((unsigned)((nq + 31) / 32 * gm.n_et)), dim3(256), 0, o->stream, gm);
     // dynamic LDS above 64 KiB (long rest grids with high rank) must be opted into per kernel
     auto launch = [&](auto kern) -> int {
       if (shm > 65536)
@@ -799,6 +748,12 @@ int obj_run(gpdla_objective* o, const double* dM_src, const double* lo_src, cons
              : k <= 32 ? launch(objective_spectrum_kernel<32>)
                        : launch(objective_spectrum_kernel<64>);
     if (rc) return rc;
+    // g = M'K^-1 y for every spectrum (spectrum_loss.m:55): the Gram GEMM's v tile on K^-1 y, into g's
+    // tile of part_bg
+    gm.out = o->part_bg;
+    gm.et0 = nep / 64 - 1;
+    gm.n_et = 1;
+    hipLaunchKernelGGL(objective_gram_kernel, dim3((unsigned)((nq + 31) / 32)), dim3(256), 0, o->stream, gm);
     // dM: the pixel x spectrum GEMM's chunk partials, then M_i X_i - h_i per pixel
     ObjAccArgs g{};
     g.ldw = a.ldw;
@@ -909,7 +864,7 @@ int gpdla_objective_create(int32_t device, int64_t num_quasars, int64_t num_pixe
       hipMalloc(&o->part_t, (size_t)o->rows * ldw * sizeof(double)) != hipSuccess ||
       hipMalloc(&o->part_gram, (size_t)o->rows * nep * sizeof(double)) != hipSuccess ||
       hipMalloc(&o->kr, (size_t)ldw * nep * sizeof(double)) != hipSuccess ||
-      hipMalloc(&o->part_bg, (size_t)o->batch * nep * sizeof(double)) != hipSuccess ||
+      hipMalloc(&o->part_bg, (size_t)o->rows * nep * sizeof(double)) != hipSuccess ||
       hipMalloc(&o->part_acc, (size_t)8 * ldw * nep * sizeof(double)) != hipSuccess ||
       hipMalloc(&o->part_chunk, (size_t)kSumChunks * (num_pixels + kObjScalars) * sizeof(double)) != hipSuccess ||
       hipMalloc(&o->part_dlo, (size_t)o->batch * num_pixels * sizeof(double)) != hipSuccess ||
@@ -921,7 +876,7 @@ int gpdla_objective_create(int32_t device, int64_t num_quasars, int64_t num_pixe
   // the operand rows' padding (pixels past P, entries past B^-1's triangle and g) is never written: zero
   if (hipMemset(o->part_w, 0, (size_t)o->rows * ldw * sizeof(double)) != hipSuccess ||
       hipMemset(o->part_t, 0, (size_t)o->rows * ldw * sizeof(double)) != hipSuccess ||
-      hipMemset(o->part_bg, 0, (size_t)o->batch * nep * sizeof(double)) != hipSuccess)
+      hipMemset(o->part_bg, 0, (size_t)o->rows * nep * sizeof(double)) != hipSuccess)
     return obj_fail(o, set_error(GPDLA_EDEVICE, "objective workspace initialisation failed"));
   *out = o;
   return GPDLA_OK;
