@@ -65,7 +65,9 @@ struct ObjTiles {
   static constexpr int KP = 4 * NTc;                              // MT row length (doubles)
 };
 
-__host__ __device__ constexpr int obj_kb(int k) { return k <= 8 ? 8 : k <= 16 ? 16 : k <= 24 ? 24 : k <= 32 ? 32 : 64; }
+__host__ __device__ constexpr int obj_kb(int k) {
+  return k <= 8 ? 8 : k <= 16 ? 16 : k <= 20 ? 20 : k <= 24 ? 24 : k <= 32 ? 32 : 64;
+}
 // part_bg row: B^-1's k (k + 1) / 2 upper entries, padded to a multiple of 64 (the GEMM's entry tile,
 // so no tile mixes the D^-1- and the K^-1 y-weighted segments), then g in a 64-entry tile
 __host__ __device__ constexpr int obj_nxp(int k) { return (k * (k + 1) / 2 + 63) / 64 * 64; }
@@ -265,6 +267,9 @@ void objective_spectrum_kernel(ObjArgs a) {
   double* B = t + P;           // [k][k + 1]: [B | v], then [B^-1 | C y] (pass 3)
   double* s = B + 2 * k * k + k;   // [k] B^-1 M' D^-1 y (= C y); B spans [k][k + 1] <= 2 k^2 + k doubles
   double* red = s + 2 * k;     // [8] block reductions (after s and a spare [k])
+  // KB <= 32: B^-1 and C y zero-padded to KB (passes 4 and 6 run unguarded, fully unrolled loops)
+  double* Bp = red + 8;        // [KB][KB]
+  double* sp = Bp + KB * KB;   // [KB]
   __shared__ int s_bad;
   const double* y = a.y + q * a.ld;
   if (tid == 0) s_bad = 0;
@@ -319,6 +324,13 @@ void objective_spectrum_kernel(ObjArgs a) {
     }
     if (tid == 0) red[6] = ldb;
     for (int r = tid; r < k; r += kObjThreads) s[r] = B[r * ld + k];
+    if constexpr (KB <= 32) {
+      for (int e = tid; e < KB * KB; e += kObjThreads) {
+        const int r = e / KB, c = e - r * KB;
+        Bp[e] = (r < k && c < k) ? B[r * ld + c] : 0.0;
+      }
+      for (int r = tid; r < KB; r += kObjThreads) sp[r] = r < k ? B[r * ld + k] : 0.0;
+    }
   }
   __syncthreads();
   const double* Bi = B;
@@ -330,14 +342,19 @@ void objective_spectrum_kernel(ObjArgs a) {
   for (int i = tid; i < P; i += kObjThreads) {
     const double wi = w[i];
     if (wi != 0.0) {
-      // the row's k loads issued together (a runtime-k loop waited on each in turn)
+      // the row's loads issued together; rows past k repeat row k - 1 (finite) against the zero padding
       double Mi[KB];
 #pragma unroll
-      for (int r = 0; r < KB; ++r) Mi[r] = r < k ? a.M[(int64_t)r * P + i] : 0.0;
+      for (int r = 0; r < KB; ++r) Mi[r] = a.M[(int64_t)(r < k ? r : k - 1) * P + i];
       double ms = 0.0;
+      if constexpr (KB <= 32) {
 #pragma unroll
-      for (int r = 0; r < KB; ++r)
-        if (r < k) ms = fma(Mi[r] * wi, s[r], ms);
+        for (int r = 0; r < KB; ++r) ms = fma(Mi[r] * wi, sp[r], ms);
+      } else {
+#pragma unroll
+        for (int r = 0; r < KB; ++r)
+          if (r < k) ms = fma(Mi[r] * wi, s[r], ms);
+      }
       const double ti = t[i] - ms;
       t[i] = ti;
       tout[i] = ti;
@@ -419,18 +436,16 @@ void objective_spectrum_kernel(ObjArgs a) {
       }
       double Mi[KB];
 #pragma unroll
-      for (int r = 0; r < KB; ++r) Mi[r] = r < k ? a.M[(int64_t)r * P + i] : 0.0;
-      // M_i B^-1 M_i' over the upper triangle: sum_r M_r (B_rr M_r + 2 sum_{c > r} B_rc M_c)
+      for (int r = 0; r < KB; ++r) Mi[r] = a.M[(int64_t)(r < k ? r : k - 1) * P + i];
+      // M_i B^-1 M_i' over the upper triangle: sum_r M_r (B_rr M_r + 2 sum_{c > r} B_rc M_c), over the
+      // zero-padded copy (compile-time LDS offsets, no per-entry guards)
       double qd = 0.0;
 #pragma unroll
       for (int r = 0; r < KB; ++r) {
-        if (r < k) {
-          double off = 0.0;
+        double off = 0.0;
 #pragma unroll
-          for (int c = r + 1; c < KB; ++c)
-            if (c < k) off = fma(Mi[c], Bi[r * ld + c], off);
-          qd = fma(Mi[r], fma(Mi[r], Bi[r * ld + r], 2.0 * off), qd);
-        }
+        for (int c = r + 1; c < KB; ++c) off = fma(Mi[c], Bp[r * KB + c], off);
+        qd = fma(Mi[r], fma(Mi[r], Bp[r * KB + r], 2.0 * off), qd);
       }
       const double dk = wi - wi * wi * qd;                          // diag K^-1 (:59)
       const double* px = a.part_px + q * 4 * (int64_t)P + i;        // pass 1's terms
@@ -675,7 +690,8 @@ int obj_fail(gpdla_objective* o, int rc) {
 }
 
 size_t obj_shared_bytes(int64_t P, int k) {
-  return (size_t)(2 * P + 2 * k * k + 3 * k + 8) * sizeof(double);
+  const int kb = obj_kb(k);
+  return (size_t)(2 * P + 2 * k * k + 3 * k + 8 + (kb <= 32 ? kb * kb + kb : 0)) * sizeof(double);
 }
 
 // one pass over all spectra with the M / log omega / (c_0, tau_0, beta) already in place
@@ -744,6 +760,7 @@ int obj_run(gpdla_objective* o, const double* dM_src, const double* lo_src, cons
     };
     int rc = k <= 8 ? launch(objective_spectrum_kernel<8>)
              : k <= 16 ? launch(objective_spectrum_kernel<16>)
+             : k <= 20 ? launch(objective_spectrum_kernel<20>)
              : k <= 24 ? launch(objective_spectrum_kernel<24>)
              : k <= 32 ? launch(objective_spectrum_kernel<32>)
                        : launch(objective_spectrum_kernel<64>);
