@@ -703,8 +703,8 @@ def objective_flops(y, k: int) -> float:
 
 
 def objective_alternative(dev: int, reps: int = 10) -> dict:
-    """objective.m's f and gradient (spectrum_loss.m summed over the training set in
-    spectrum order) on the device for a DR9-training-set-sized problem (5,000 spectra x 1,217 rest
+    """objective.m's f and gradient (spectrum_loss.m summed over the training set in a
+    fixed order: the Gram and dM sums as pixel x spectrum GEMMs, the rest in spectrum chunks) on the device for a DR9-training-set-sized problem (5,000 spectra x 1,217 rest
     pixels, k = 20): one warm-up evaluation, then ``reps`` timed ones; kernel times from a one-launch
     evaluation under HIP events are not exposed, so the roofline is over the evaluation's wall time."""
     from gp_dla_detection_amd import training as T
@@ -723,7 +723,7 @@ def objective_alternative(dev: int, reps: int = 10) -> dict:
             "roofline": {"bound": "fp64", "unit": "TFLOP/s", "peak": FP64_PEAK_TFLOPS,
                          "achieved": flops / el / 1e12, "frac": flops / el / 1e12 / FP64_PEAK_TFLOPS,
                          "flops": flops, "note": "algorithmic flops (objective_flops) over the whole evaluation "
-                                                 "(spectrum kernel + the spectrum-ordered gradient sums + copies)"},
+                                                 "(pixel, Gram / g / dM GEMM and spectrum kernels, the sums, copies)"},
             "checks_ok": ok, "repeat_bitwise_equal": ok}
 
 
