@@ -19,6 +19,7 @@
 
 #include <cmath>
 #include <cstdint>
+#include <cstdlib>
 #include <vector>
 
 #include "../../include/gpdla.h"
@@ -857,6 +858,12 @@ int gpdla_objective_create(int32_t device, int64_t num_quasars, int64_t num_pixe
   const int64_t ldw = obj_ldw(num_pixels), nep = obj_nep(k);
   const int64_t per_q = 2 * ldw + 2 * nep + 5 * num_pixels + kObjScalars;   // w, t, Gram, [B^-1 | g], d log omega, px
   o->batch = std::max<int64_t>(1, std::min<int64_t>(std::max<int64_t>(num_quasars, 1), (1LL << 29) / per_q));
+  // GPDLA_OBJECTIVE_BATCH caps the spectra per launch further (smaller workspaces; the tests use it to
+  // run the multi-launch path on a small set)
+  if (const char* cap = std::getenv("GPDLA_OBJECTIVE_BATCH")) {
+    const long long v = std::atoll(cap);
+    if (v > 0) o->batch = std::min<int64_t>(o->batch, v);
+  }
   o->rows = (o->batch + 31) / 32 * 32;
   if (hipStreamCreateWithFlags(&o->stream, hipStreamNonBlocking) != hipSuccess)
     return obj_fail(o, set_error(GPDLA_EDEVICE, "hipStreamCreate failed"));

@@ -203,7 +203,9 @@ int gpdla_log_mvnpdf_low_rank_f64(const double* y, const double* mu, const doubl
  * As in the reference, the tau_0 and beta priors enter g only, not f (objective.m:59-71).
  * gpdla_objective_create copies host data to the device (memory = GPDLA_MEM_HOST) or borrows
  * device arrays (GPDLA_MEM_DEVICE, which must outlive the handle); each _eval takes host x and
- * writes host f and g (g may be NULL).  num_pixels <= 4096, k <= 64. */
+ * writes host f and g (g may be NULL).  num_pixels <= 4096, k <= 64.  Spectra go through the
+ * kernels in launches of up to 2^29 doubles of workspace; the environment variable
+ * GPDLA_OBJECTIVE_BATCH (read at create) caps the spectra per launch further. */
 typedef struct gpdla_objective gpdla_objective;
 int gpdla_objective_create(int32_t device, int64_t num_quasars, int64_t num_pixels, int32_t k,
                            const double* centered_rest_fluxes, const double* lya_1pzs,

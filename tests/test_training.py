@@ -188,3 +188,18 @@ def test_gpu_objective_large_grid_high_rank():
     fr, gr = O.objective(x, y, lya, nv)
     assert f == pytest.approx(fr, rel=1e-11)
     np.testing.assert_allclose(g, gr, rtol=1e-8, atol=1e-11 * np.abs(gr).max())
+
+
+@pytest.mark.gpu
+def test_gpu_objective_multi_launch_matches_one_launch(monkeypatch):
+    """Spectra in launches of 7 (a ragged last one; GPDLA_OBJECTIVE_BATCH) against one launch and the
+    oracle: the per-launch Gram / dM GEMM tiles are 32 spectra, so every launch has padding rows."""
+    y, lya, nv, x0, k = _training_set(Q=40, k=20, seed=11)
+    f1, g1 = T.objective(x0, y, lya, nv)
+    monkeypatch.setenv("GPDLA_OBJECTIVE_BATCH", "7")
+    f7, g7 = T.objective(x0, y, lya, nv)
+    fr, gr = O.objective(x0, y, lya, nv)
+    assert f7 == pytest.approx(f1, rel=1e-13) and f7 == pytest.approx(fr, rel=1e-11)
+    scale = np.abs(gr).max()
+    np.testing.assert_allclose(g7, g1, rtol=1e-11, atol=1e-13 * scale)
+    np.testing.assert_allclose(g7, gr, rtol=1e-8, atol=1e-11 * scale)
