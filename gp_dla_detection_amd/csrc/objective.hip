@@ -265,8 +265,8 @@ void objective_spectrum_kernel(ObjArgs a) {
   const int64_t q = blockIdx.x;
   double* w = sm;              // [P] d^-1 (0 = excluded pixel)
   double* t = w + P;           // [P] D^-1 y, then K^-1 y
-  double* B = t + P;           // [k][k + 1]: [B | v], then [B^-1 | C y] (pass 3)
-  double* s = B + 2 * k * k + k;   // [k] B^-1 M' D^-1 y (= C y); B spans [k][k + 1] <= 2 k^2 + k doubles
+  double* B = t + P;           // 2 x [k][k + 1]: [B | v], then [B^-1 | C y] (pass 3's two buffers)
+  double* s = B + 2 * k * k + 2 * k;   // [k] B^-1 M' D^-1 y (= C y)
   double* red = s + 2 * k;     // [8] block reductions (after s and a spare [k])
   // KB <= 32: B^-1 and C y zero-padded to KB (passes 4 and 6 run unguarded, fully unrolled loops)
   double* Bp = red + 8;        // [KB][KB]
@@ -296,45 +296,65 @@ void objective_spectrum_kernel(ObjArgs a) {
   __syncthreads();
 
   // pass 3: Gauss-Jordan on [B | v] by the whole block (B is symmetric positive definite with
-  // eigenvalues >= 1: no pivoting), 2 barriers per pivot: B^-1 in place, s = B^-1 v = C y in the
-  // augmented column (:46-48), log det B = the sum of the pivots' logs (= 2 sum log diag of
-  // spectrum_loss.m:43's Cholesky factor, :44); a non-positive pivot flags the spectrum as chol would
+  // eigenvalues >= 1: no pivoting): B^-1 in place, s = B^-1 v = C y in the augmented column (:46-48),
+  // log det B = the sum of the pivots' logs (= 2 sum log diag of spectrum_loss.m:43's Cholesky factor,
+  // :44); a non-positive pivot flags the spectrum as chol would.  Each pivot reads one buffer and writes
+  // the other (one barrier per pivot); a thread's entries (and their row / column) are fixed across
+  // pivots, so the divisions are done once
   const int ld = k + 1;
+  const double* Bi;
   {
+    constexpr int NE = (KB * (KB + 1) + kObjThreads - 1) / kObjThreads;
+    const int ne = k * ld;
+    int ei[NE], ej[NE];
+#pragma unroll
+    for (int n = 0; n < NE; ++n) {
+      const int e = tid + n * kObjThreads;
+      ei[n] = e / ld;
+      ej[n] = e - ei[n] * ld;
+    }
+    double* cur = B;
+    double* nxt = B + ne;
     double ldb = 0.0;
     for (int p = 0; p < k; ++p) {
-      const double piv = B[p * ld + p];
+      const double piv = cur[p * ld + p];
       if (tid == 0) {
         if (!(piv > 0.0)) s_bad = 1;
         ldb += log(piv);
       }
       const double inv = 1.0 / piv;
-      for (int e = tid; e < k * ld; e += kObjThreads) {
-        const int i = e / ld, j = e - i * ld;
-        if (i != p && j != p) B[e] = fma(-B[i * ld + p] * inv, B[p * ld + j], B[e]);
-      }
-      __syncthreads();
-      for (int e = tid; e < ld + k; e += kObjThreads) {
-        if (e < ld) {
-          B[p * ld + e] = e == p ? inv : B[p * ld + e] * inv;
-        } else if (e - ld != p) {
-          B[(e - ld) * ld + p] = -B[(e - ld) * ld + p] * inv;
+#pragma unroll
+      for (int n = 0; n < NE; ++n) {
+        const int e = tid + n * kObjThreads;
+        if (e < ne) {
+          const int i = ei[n], j = ej[n];
+          double v;
+          if (i == p)
+            v = j == p ? inv : cur[e] * inv;
+          else if (j == p)
+            v = -cur[e] * inv;
+          else
+            v = fma(-cur[i * ld + p] * inv, cur[p * ld + j], cur[e]);
+          nxt[e] = v;
         }
       }
       __syncthreads();
+      double* sw = cur;
+      cur = nxt;
+      nxt = sw;
     }
     if (tid == 0) red[6] = ldb;
-    for (int r = tid; r < k; r += kObjThreads) s[r] = B[r * ld + k];
+    for (int r = tid; r < k; r += kObjThreads) s[r] = cur[r * ld + k];
     if constexpr (KB <= 32) {
       for (int e = tid; e < KB * KB; e += kObjThreads) {
         const int r = e / KB, c = e - r * KB;
-        Bp[e] = (r < k && c < k) ? B[r * ld + c] : 0.0;
+        Bp[e] = (r < k && c < k) ? cur[r * ld + c] : 0.0;
       }
-      for (int r = tid; r < KB; r += kObjThreads) sp[r] = r < k ? B[r * ld + k] : 0.0;
+      for (int r = tid; r < KB; r += kObjThreads) sp[r] = r < k ? cur[r * ld + k] : 0.0;
     }
+    Bi = cur;
   }
   __syncthreads();
-  const double* Bi = B;
 
   // pass 4: K^-1 y = D^-1 y - D^-1 M (C y) (:48), in place over D^-1 y in part_t (the operand of g's and
   // the dM GEMMs; excluded pixels stay 0); y' K^-1 y
@@ -692,7 +712,7 @@ int obj_fail(gpdla_objective* o, int rc) {
 
 size_t obj_shared_bytes(int64_t P, int k) {
   const int kb = obj_kb(k);
-  return (size_t)(2 * P + 2 * k * k + 3 * k + 8 + (kb <= 32 ? kb * kb + kb : 0)) * sizeof(double);
+  return (size_t)(2 * P + 2 * k * k + 4 * k + 8 + (kb <= 32 ? kb * kb + kb : 0)) * sizeof(double);
 }
 
 // one pass over all spectra with the M / log omega / (c_0, tau_0, beta) already in place
