@@ -44,8 +44,7 @@ struct ObjArgs {
   const double* noise;       // [Q][ld]
   const double* M;           // [P x k] column-major (x(1:P*k), objective.m:22-23)
   const double* MT;          // [4 ceil(P / 4)][KP] the same M pixel-major, zero-padded (objective_mt_kernel)
-  const double* log_omega;   // [P] (objective.m:25-26), or nullptr when omega2 is given
-  const double* omega2;      // [P] spectrum_loss's omega2 argument directly, or nullptr
+  const double* omega2;      // [P] spectrum_loss's omega2 argument, or exp(2 log omega) (objective.m:25-32)
   double c_0, tau_0, beta;
   int32_t ldw;               // row stride of part_w / part_t (P rounded up to 32, zero tail)
   int32_t nep, nxp;          // part_bg row length; offset of g in it (see obj_nxp)
@@ -78,6 +77,13 @@ __host__ __device__ constexpr int obj_ldw(int64_t P) { return (int)((P + 31) / 3
 __device__ inline int obj_packed(int r, int c, int k) { return r * k - r * (r - 1) / 2 + (c - r); }
 __host__ __device__ constexpr int obj_kp(int kb) { return 4 * ((kb + 4) / 4); }
 
+// omega^2 = exp(2 log omega) per pixel (objective.m:32), once per evaluation rather than per spectrum
+__global__ __launch_bounds__(256) void objective_omega2_kernel(const double* __restrict__ log_omega, int32_t P,
+                                                               double* __restrict__ om2) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < P) om2[i] = exp(2 * log_omega[i]);
+}
+
 // MT[p][r] = M[r][p] for p < P, r < k; zero elsewhere (the padding rows / columns the tiles read)
 __global__ __launch_bounds__(256) void objective_mt_kernel(const double* __restrict__ M, int32_t P, int32_t k,
                                                            int32_t KP, int64_t rows, double* __restrict__ MT) {
@@ -105,7 +111,7 @@ struct PixelTerms {
 
 __device__ inline PixelTerms pixel_terms(const ObjArgs& a, int i, double lya, double nv) {
   PixelTerms p;
-  p.om2 = a.omega2 ? a.omega2[i] : exp(2 * a.log_omega[i]);     // objective.m:32
+  p.om2 = a.omega2[i];                                            // objective.m:32 (objective_omega2_kernel)
   p.tau = a.tau_0 * pow(lya, a.beta);                             // spectrum_loss.m:23
   p.absorb = exp(-p.tau);                                         // :24
   p.sf = 1 - p.absorb + a.c_0;                                    // :27
@@ -701,6 +707,7 @@ struct gpdla_objective {
   double* part_px = nullptr;  // [batch][4][P]
   double* tot = nullptr;      // [k P + P + kObjScalars]
   double* mt = nullptr;       // [4 ceil(P / 4)][obj_kp(obj_kb(k))] pixel-major M
+  double* om2 = nullptr;      // [P] omega^2 of the evaluation's log omega
 };
 
 namespace {
@@ -730,6 +737,9 @@ int obj_run(gpdla_objective* o, const double* dM_src, const double* lo_src, cons
   const int ldw = obj_ldw(P), nep = obj_nep(k), nxp = obj_nxp(k);
   hipLaunchKernelGGL(objective_kr_kernel, dim3((unsigned)(((int64_t)ldw * nep + 255) / 256)), dim3(256), 0, o->stream,
                      dM_src, (int32_t)P, (int32_t)k, (int32_t)nxp, (int32_t)nep, (int64_t)ldw, o->kr);
+  if (!om2_src)
+    hipLaunchKernelGGL(objective_omega2_kernel, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, o->stream, lo_src,
+                       (int32_t)P, o->om2);
   for (int64_t q0 = 0; q0 < o->Q; q0 += o->batch) {
     const int64_t nq = std::min(o->batch, o->Q - q0);
     ObjArgs a{};
@@ -741,8 +751,7 @@ int obj_run(gpdla_objective* o, const double* dM_src, const double* lo_src, cons
     a.noise = o->noise + q0 * P;
     a.M = dM_src;
     a.MT = o->mt;
-    a.log_omega = lo_src;
-    a.omega2 = om2_src;
+    a.omega2 = om2_src ? om2_src : o->om2;
     a.c_0 = c_0;
     a.tau_0 = tau_0;
     a.beta = beta;
@@ -850,6 +859,7 @@ void gpdla_objective_destroy(gpdla_objective* o) {
   (void)hipFree(o->part_px);
   (void)hipFree(o->tot);
   (void)hipFree(o->mt);
+  (void)hipFree(o->om2);
   if (o->stream) (void)hipStreamDestroy(o->stream);
   delete o;
 }
@@ -915,7 +925,8 @@ int gpdla_objective_create(int32_t device, int64_t num_quasars, int64_t num_pixe
       hipMalloc(&o->part_s, (size_t)o->batch * kObjScalars * sizeof(double)) != hipSuccess ||
       hipMalloc(&o->part_px, (size_t)o->batch * 4 * num_pixels * sizeof(double)) != hipSuccess ||
       hipMalloc(&o->tot, (size_t)per * sizeof(double)) != hipSuccess ||
-      hipMalloc(&o->mt, (size_t)(4 * ((num_pixels + 3) / 4)) * obj_kp(obj_kb(k)) * sizeof(double)) != hipSuccess)
+      hipMalloc(&o->mt, (size_t)(4 * ((num_pixels + 3) / 4)) * obj_kp(obj_kb(k)) * sizeof(double)) != hipSuccess ||
+      hipMalloc(&o->om2, (size_t)num_pixels * sizeof(double)) != hipSuccess)
     return obj_fail(o, set_error(GPDLA_ENOMEM, "objective workspace allocation failed"));
   // the operand rows' padding (pixels past P, entries past B^-1's triangle and g) is never written: zero
   if (hipMemset(o->part_w, 0, (size_t)o->rows * ldw * sizeof(double)) != hipSuccess ||
